@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident FEC encode + reconstruct throughput on MI355X.
+
+Metric (BASELINE.json): "FEC encode+decode GiB/s device-resident, (10+3)x1350B
+groups; %HBM roofline".  One step = one pass of the hot path over one batch:
+  1. ugo_fec_encode       -- Encoder.Encode (ugo/fec.go:238) on every group
+  2. ugo_fec_reconstruct  -- Encoder.Reconstruct (ugo/fec.go:202) on every group
+                             with exactly 2 distinct erased shards (uniform over
+                             the 78 patterns, BASELINE configs[2])
+Inputs are resident in HBM before the timed region (synthetic, device-generated
+random bytes).  Algorithmic bytes per group: encode (d+p)*S,
+reconstruct (d+e)*S; value = sum over ranks / max-over-ranks time, in GiB/s.
+
+Multi-GPU (torchrun, one process per GPU): packet groups are independent, so
+each rank owns its own batch (weak scaling) -- or a contiguous 1/N slice of
+--total-groups (strong scaling) -- and no data-path collective runs; only the
+timing barrier and a max-reduction.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--groups G]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from ugo_amd import fec  # noqa: E402
+from ugo_amd.shard import dist_env, partition  # noqa: E402
+
+METRIC = "FEC encode+decode GiB/s device-resident, (10+3)×1350B groups; %HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, GB/s (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
+    ap.add_argument("--total-groups", type=int, default=0, help="if set: strong scaling over this many groups")
+    ap.add_argument("--data-shards", type=int, default=10)
+    ap.add_argument("--parity-shards", type=int, default=3)
+    ap.add_argument("--shard-size", type=int, default=1350)
+    ap.add_argument("--pitch", type=int, default=0, help="row pitch in HBM (default: shard size rounded to 16)")
+    ap.add_argument("--erasures", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def make_masks(G, n, e, seed, device):
+    """Presence masks with exactly e distinct erased shards per group."""
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    keys = torch.rand((G, n), generator=gen)
+    erased = keys.argsort(dim=1)[:, :e]  # e distinct indices, uniform over C(n, e)
+    masks = torch.full((G,), (1 << n) - 1, dtype=torch.int64)
+    for j in range(e):
+        masks ^= (1 << erased[:, j]).to(torch.int64)
+    return masks.to(device), erased
+
+
+def cpu_baseline(args, d, p, S, n, sample_groups=512):
+    """The CPU oracle (oracle/rs_oracle.c, scalar C restatement of the upstream
+    algorithm) timed on this host on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import rs_ref  # checker / CPU baseline only
+
+    rs_ref.load_c_oracle()
+    rng = np.random.default_rng(args.seed)
+    sh = rng.integers(0, 256, size=(sample_groups, n, S), dtype=np.uint8)
+    masks = np.full(sample_groups, (1 << n) - 1, np.uint64)
+    for g in range(sample_groups):
+        for r in rng.choice(n, args.erasures, replace=False):
+            masks[g] &= ~np.uint64(1 << int(r))
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        rs_ref.c_encode(d, p, sh, threads=args.cpu_threads)
+        rs_ref.c_reconstruct(d, p, sh, masks, threads=args.cpu_threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_baseline_seconds:
+            break
+    per_pass = sample_groups * ((d + p) * S + (d + args.erasures) * S)
+    return {"value": round(per_pass * passes / el / 2**30, 4), "unit": "GiB/s", "cores": args.cpu_threads,
+            "kind": "port",
+            "sample": f"{sample_groups} groups ({d}+{p})x{S}B, encode + {args.erasures}-erasure reconstruct, "
+                      f"{passes} passes in {el:.1f}s, oracle/rs_oracle.c (scalar C restatement of the "
+                      f"klauspost algorithm; the Go reference cannot run: no Go toolchain)"}
+
+
+def main():
+    args = parse()
+    rank, local_rank, world = dist_env()
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    d, p, S = args.data_shards, args.parity_shards, args.shard_size
+    n = d + p
+    pitch = args.pitch or (S + 15) // 16 * 16
+    if args.total_groups:
+        g0, g1 = partition(args.total_groups, world, rank)
+        G = g1 - g0
+        scaling = "strong"
+    else:
+        G = args.groups
+        g0 = rank * G
+        scaling = "weak"
+    e = args.erasures
+
+    enc = fec.New(d, p, device=local_rank)
+    gen = torch.Generator(device=dev).manual_seed(args.seed + rank)
+    shards = torch.randint(0, 256, (G, n, pitch), dtype=torch.uint8, device=dev, generator=gen)
+    masks, erased = make_masks(G, n, e, args.seed + 1000 + rank, dev)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        enc.encode_batch(shards, shard_size=S, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        enc.reconstruct_batch(shards, masks, shard_size=S, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    enc_ms = sum(ev[0].elapsed_time(ev[1]) for ev in evs) / args.steps
+    dec_ms = sum(ev[1].elapsed_time(ev[2]) for ev in evs) / args.steps
+
+    t = torch.tensor([elapsed, enc_ms, dec_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, enc_ms_max, dec_ms_max = t.tolist()
+    total_groups = G * world if scaling == "weak" else args.total_groups
+
+    enc_bytes = G * n * S            # per launch, this rank
+    dec_bytes = G * (d + e) * S
+    step_bytes_all = total_groups * (n * S + (d + e) * S)
+    value = step_bytes_all * args.steps / elapsed / 2**30
+
+    # bit-exactness at full size (outside the timed region): erase, reconstruct, compare
+    verify = None
+    if not args.no_verify:
+        ref = shards.clone()
+        gi = torch.arange(G, device=dev)
+        for j in range(e):
+            shards[gi, erased[:, j].to(dev)] = 0
+        enc.reconstruct_batch(shards, masks, shard_size=S, stream=stream)
+        ok_rt = bool(torch.equal(shards[:, :, :S], ref[:, :, :S]))
+        par = ref[:, d:, :S].clone()
+        shards[:, d:, :] = 0
+        enc.encode_batch(shards, shard_size=S, stream=stream)
+        ok_idem = bool(torch.equal(shards[:, d:, :S], par))
+        del ref, par
+        verify = {"round_trip_full_size": ok_rt, "encode_idempotent": ok_idem}
+        okt = torch.tensor([int(ok_rt and ok_idem)], device=dev)
+        if world > 1:
+            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        verify["all_ranks_ok"] = bool(okt.item())
+
+    if rank == 0:
+        kern = {
+            "encode": {"avg_ms": round(enc_ms, 5), "bytes_per_launch": enc_bytes,
+                       "GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1)},
+            "reconstruct": {"avg_ms": round(dec_ms, 5), "bytes_per_launch": dec_bytes,
+                            "GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1)},
+        }
+        dom = "encode" if enc_ms >= dec_ms else "reconstruct"
+        traffic = None
+        try:
+            tj = json.load(open(args.traffic_json))
+            key = f"{dom}:{d}+{p}x{S}/{pitch}:G{G}"
+            traffic = tj.get(key)
+        except Exception:
+            pass
+        ach = kern[dom]["GBps"]
+        roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "note": f"achieved = algorithmic bytes per launch ({'(d+p)*S' if dom == 'encode' else '(d+e)*S'}"
+                        f" per group x {G} groups) / avg launch time from HIP events on the launch stream"}
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: device-generated uniform random bytes (seeded), "
+                    f"{e} distinct uniformly random erased shards per group",
+            "config": {"workload": f"({d}+{p})x{S}B groups, encode + {e}-erasure reconstruct, device-resident, "
+                                   f"{G} groups/GPU", "groups_per_gpu": G, "total_groups": total_groups,
+                       "data_shards": d, "parity_shards": p, "shard_size": S, "pitch": pitch, "erasures": e,
+                       "parallelism": f"dp{world} (independent packet groups, no collective)"},
+            "pct_hbm_roofline": round(step_bytes_all / world * args.steps / elapsed / (HBM_PEAK_GBS * 1e9), 4),
+            "roofline": roof, "kernels": kern, "verify": verify,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, d, p, S, n)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

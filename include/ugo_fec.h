@@ -1,0 +1,120 @@
+/*
+ * ugo_fec.h -- C-ABI of the MI355X-native Reed-Solomon FEC engine for
+ * jflyup/ugo's per-packet-group FEC (ugo/fec.go).
+ *
+ * The boundary is the klauspost/reedsolomon Encoder subset that ugo/fec.go
+ * actually uses (New at ugo/fec.go:59, Reconstruct at :202, Encode at :238),
+ * lifted from one group per call to a batch of independent groups so one
+ * gfx950 kernel launch covers thousands of packet groups.  Plain pointers and
+ * sizes only; no exceptions cross the ABI; every entry point returns a
+ * ugo_fec_status.
+ *
+ * Batch layout (device or host memory, caller-owned):
+ *     shards[g][r][pitch]   g in [0, groups), r in [0, d+p)
+ *   Row r < d is data shard r, row d+i is parity shard i, exactly the index
+ *   order of the [][]byte passed to Encode/Reconstruct.  Bytes [0, shard_size)
+ *   of a row are the shard; bytes [shard_size, pitch) are padding the engine
+ *   never reads into a result and never writes.
+ *   Fast path: shards 16-byte aligned and pitch % 16 == 0 (any shard_size).
+ *   Any other layout is accepted and runs a slower byte-granular kernel.
+ *
+ * Erasures: present[g] bit r == 1  <=>  len(shards[r]) != 0 in Go terms.
+ *   Batch presence masks are 64-bit, so the batch entry points need d+p <= 64
+ *   (upstream allows 256; ugo uses (10,3)).
+ *
+ * Threading: a context is single-owner (like ugo's FEC, used only from the
+ * Conn.run goroutine, ugo/conn.go:106-127).  Distinct contexts -- e.g. one per
+ * GPU -- may be driven concurrently from different threads.
+ *
+ * Not thread-safe per context; all device work is enqueued on `stream`
+ * (hipStream_t passed as void*, NULL = the legacy default stream).
+ */
+#ifndef UGO_FEC_H
+#define UGO_FEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UGO_FEC_ABI_VERSION 1
+
+/* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
+ * that ugo/fec.go logs and swallows (ugo/fec.go:60-63, 208-210, 239-241). */
+typedef enum ugo_fec_status {
+  UGO_FEC_OK = 0,
+  UGO_FEC_ERR_INV_SHARD_NUM = 1,  /* reedsolomon.ErrInvShardNum: d <= 0 or p < 0    */
+  UGO_FEC_ERR_MAX_SHARD_NUM = 2,  /* reedsolomon.ErrMaxShardNum: d + p > 256         */
+  UGO_FEC_ERR_TOO_FEW_SHARDS = 3, /* reedsolomon.ErrTooFewShards                     */
+  UGO_FEC_ERR_SHARD_NO_DATA = 4,  /* reedsolomon.ErrShardNoData                      */
+  UGO_FEC_ERR_SHARD_SIZE = 5,     /* reedsolomon.ErrShardSize                        */
+  UGO_FEC_ERR_INVALID_ARG = 6,    /* NULL pointer, pitch < shard_size, d+p > 64 ... */
+  UGO_FEC_ERR_SINGULAR = 7,       /* errSingular (cannot occur for this MDS code)    */
+  UGO_FEC_ERR_HIP = 8,            /* HIP runtime failure (alloc, copy, launch)       */
+  UGO_FEC_ERR_NO_DEVICE = 9       /* no usable gfx950 device / bad device ordinal    */
+} ugo_fec_status;
+
+/* Flags for ugo_fec_reconstruct*.  Default (0) = Reconstruct: every erased row,
+ * data AND parity, is rebuilt (ugo/fec.go:202).  DATA_ONLY = ReconstructData. */
+#define UGO_FEC_RECONSTRUCT_DATA_ONLY 1u
+
+typedef struct ugo_fec ugo_fec; /* opaque: one (d,p) code bound to one device */
+
+/* reedsolomon.New(d, p) as called at ugo/fec.go:59 (and validated by newFEC,
+ * ugo/fec.go:45-64).  Binds the code to HIP device `device`, builds the
+ * systematic Vandermonde-derived (d+p) x d matrix, uploads it, and (d+p <= 16)
+ * precomputes the decode descriptor of every erasure pattern. */
+int ugo_fec_create(int device, int data_shards, int parity_shards, ugo_fec** out);
+void ugo_fec_destroy(ugo_fec* ctx);
+
+/* Geometry and the (d+p) x d encoding matrix, row-major (test/inspection). */
+int ugo_fec_geometry(const ugo_fec* ctx, int* data_shards, int* parity_shards, int* device);
+int ugo_fec_matrix(const ugo_fec* ctx, uint8_t* out /* (d+p)*d bytes */);
+
+/* ---- device-resident batch (asynchronous on `stream`) -------------------
+ * Encoder.Encode(shards) (ugo/fec.go:238) for every group: reads rows [0,d),
+ * writes parity rows [d, d+p) in place.  shard_size == 0 -> ERR_SHARD_NO_DATA
+ * (checkShards).  `shards` is a device pointer. */
+int ugo_fec_encode(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_size,
+                   size_t pitch, void* stream);
+
+/* Encoder.Reconstruct(shards) (ugo/fec.go:202) for every group.  `present`
+ * (device, u64 per group) marks the non-empty shards.  Survivors are the first
+ * d present rows in index order (upstream rule), every erased row is written.
+ * Groups with fewer than d present shards are left untouched and get
+ * status UGO_FEC_ERR_TOO_FEW_SHARDS; all others UGO_FEC_OK.  `status`
+ * (device, int8 per group) may be NULL.  Returns launch status only. */
+int ugo_fec_reconstruct(ugo_fec* ctx, uint8_t* shards, const uint64_t* present, size_t groups,
+                        size_t shard_size, size_t pitch, unsigned flags, int8_t* status,
+                        void* stream);
+
+/* ---- host-buffer batch (synchronous) ------------------------------------
+ * Same contracts with HOST pointers: the engine stages through its own device
+ * buffers, pipelining H2D -> kernel -> D2H over chunks on internal streams.
+ * Use ugo_fec_host_alloc() buffers for full-rate DMA.  The reconstruct form
+ * returns the first failing group's status (UGO_FEC_OK if none); `status`
+ * (host, nullable) receives every group's status. */
+int ugo_fec_encode_host(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_size,
+                        size_t pitch);
+int ugo_fec_reconstruct_host(ugo_fec* ctx, uint8_t* shards, const uint64_t* present,
+                             size_t groups, size_t shard_size, size_t pitch, unsigned flags,
+                             int8_t* status);
+
+/* ---- per-call validation shared with the Go shim ------------------------
+ * checkShards(shards, nilok) [klauspost] over a list of n shard lengths:
+ * ERR_SHARD_NO_DATA if all are empty, ERR_SHARD_SIZE if a non-empty length
+ * differs (or an empty one with nil_ok == 0).  Host-only, no device needed. */
+int ugo_fec_check_shards(int n, const size_t* lens, int nil_ok, size_t* shard_size);
+
+/* ---- helpers ------------------------------------------------------------- */
+int ugo_fec_host_alloc(size_t bytes, void** out);  /* pinned host memory */
+int ugo_fec_host_free(void* p);
+const char* ugo_fec_strerror(int status);
+int ugo_fec_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UGO_FEC_H */

@@ -1,0 +1,399 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY.  NOT PART OF THE PRODUCT PATH.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this code, and only as the checker (or the timed CPU baseline).  The product
+ * library (ugo_amd/libugofec.so) never links or calls it.
+ *
+ * What it is: a plain-C, scalar restatement of the Reed-Solomon arithmetic that
+ * jflyup/ugo's FEC delegates to.  ugo/fec.go:9 imports
+ * github.com/klauspost/reedsolomon (un-vendored, no go.mod, so no version pin;
+ * GOPATH-era "go get" = upstream HEAD).  That dependency is absent from
+ * /root/reference and from this container, so its *published* algorithm is
+ * restated here [upstream]:
+ *
+ *   - GF(2^8), field polynomial 0x11D, generator 2          (galois.go)
+ *   - galExp(a, 0) = 1, galExp(0, n>0) = 0                   (galois.go)
+ *   - vandermonde(r, c) = galExp(r, c)                       (matrix.go)
+ *   - buildMatrix(d, n) = V * inverse(V[0:d][0:d])           (reedsolomon.go)
+ *   - Encode:  parity[i][j] = XOR_k m[d+i][k] * data[k][j]   (codeSomeShards)
+ *   - Reconstruct: first d present shards in index order -> sub-matrix -> invert
+ *     -> rebuild missing data rows; then missing parity rows are re-encoded
+ *     from the completed data rows (two stages, exactly as upstream).
+ *   - checkShards / error values ErrTooFewShards, ErrShardNoData, ErrShardSize,
+ *     ErrInvShardNum, ErrMaxShardNum.
+ *
+ * Wrapper semantics follow the reference call sites:
+ *   ugo/fec.go:45-72  newFEC (geometry validation, reedsolomon.New(d,p) at :59)
+ *   ugo/fec.go:196-217 input -> Reconstruct(shards) at :202
+ *   ugo/fec.go:228-243 calcECC -> Encode(shards) at :238, over data[k][offset:maxlen]
+ *
+ * Parity pinning: the reference holds NO test for this path,
+ * so parity against the reference itself is UNPINNED.  This restatement is
+ * checked (tests/test_oracle.py) against known-answer vectors recalled from the
+ * upstream klauspost test suite (tests/golden/klauspost_kat.json: TestGalois,
+ * TestMatrixMultiply, TestMatrixInverse, TestOneEncode) and against an
+ * independent pure-Python mirror (oracle/rs_ref.py) that multiplies by
+ * shift-and-reduce instead of log/exp tables.
+ *
+ * Batch layout (same as the product C-ABI, include/ugo_fec.h):
+ *   shards[g][r][pitch], r in [0, d+p), bytes [0, S) of each row significant.
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+#include <stdlib.h>
+#include <pthread.h>
+
+/* status values mirror include/ugo_fec.h (kept literal so the oracle stays
+ * self-contained and does not include product headers) */
+enum {
+  OR_OK = 0,
+  OR_ERR_INV_SHARD_NUM = 1,
+  OR_ERR_MAX_SHARD_NUM = 2,
+  OR_ERR_TOO_FEW_SHARDS = 3,
+  OR_ERR_SHARD_NO_DATA = 4,
+  OR_ERR_SHARD_SIZE = 5,
+  OR_ERR_INVALID_ARG = 6,
+  OR_ERR_SINGULAR = 7,
+};
+
+static uint8_t LOG[256];
+static uint8_t EXP[512];
+static uint8_t MUL[256][256];
+static int g_init = 0;
+
+/* galois.go [upstream]: exp/log tables for generator 2 over x^8+x^4+x^3+x^2+1 */
+void oracle_init(void) {
+  if (g_init) return;
+  int x = 1;
+  for (int i = 0; i < 255; i++) {
+    EXP[i] = (uint8_t)x;
+    LOG[x] = (uint8_t)i;
+    x <<= 1;
+    if (x & 0x100) x ^= 0x11d;
+  }
+  for (int i = 255; i < 512; i++) EXP[i] = EXP[i - 255];
+  LOG[0] = 0; /* unused: mul by 0 handled explicitly */
+  for (int a = 0; a < 256; a++)
+    for (int b = 0; b < 256; b++)
+      MUL[a][b] = (a == 0 || b == 0) ? 0 : EXP[LOG[a] + LOG[b]];
+  g_init = 1;
+}
+
+uint8_t oracle_gf_mul(uint8_t a, uint8_t b) { oracle_init(); return MUL[a][b]; }
+
+/* galDivide [upstream]: a / b, b != 0 */
+static uint8_t gf_div(uint8_t a, uint8_t b) {
+  if (a == 0) return 0;
+  int l = (int)LOG[a] - (int)LOG[b];
+  if (l < 0) l += 255;
+  return EXP[l];
+}
+
+/* galExp [upstream] */
+uint8_t oracle_gf_exp(uint8_t a, int n) {
+  oracle_init();
+  if (n == 0) return 1;
+  if (a == 0) return 0;
+  int l = ((int)LOG[a] * n) % 255;
+  return EXP[l];
+}
+
+/* matrix.go Invert / gaussianElimination [upstream] on an n x n row-major
+ * matrix.  Returns OR_ERR_SINGULAR if singular.  in and out may alias. */
+int oracle_invert(int n, const uint8_t* in, uint8_t* out) {
+  oracle_init();
+  if (n <= 0 || n > 256) return OR_ERR_INVALID_ARG;
+  int w = 2 * n;
+  uint8_t* a = (uint8_t*)malloc((size_t)n * w);
+  if (!a) return OR_ERR_INVALID_ARG;
+  for (int r = 0; r < n; r++) {
+    memcpy(a + (size_t)r * w, in + (size_t)r * n, (size_t)n);
+    memset(a + (size_t)r * w + n, 0, (size_t)n);
+    a[(size_t)r * w + n + r] = 1;
+  }
+  for (int r = 0; r < n; r++) {
+    if (a[(size_t)r * w + r] == 0) {
+      int below;
+      for (below = r + 1; below < n; below++)
+        if (a[(size_t)below * w + r] != 0) break;
+      if (below == n) { free(a); return OR_ERR_SINGULAR; }
+      for (int c = 0; c < w; c++) {
+        uint8_t t = a[(size_t)r * w + c];
+        a[(size_t)r * w + c] = a[(size_t)below * w + c];
+        a[(size_t)below * w + c] = t;
+      }
+    }
+    uint8_t piv = a[(size_t)r * w + r];
+    if (piv != 1) {
+      uint8_t s = gf_div(1, piv);
+      for (int c = 0; c < w; c++) a[(size_t)r * w + c] = MUL[s][a[(size_t)r * w + c]];
+    }
+    for (int rb = r + 1; rb < n; rb++) {
+      uint8_t s = a[(size_t)rb * w + r];
+      if (s) for (int c = 0; c < w; c++) a[(size_t)rb * w + c] ^= MUL[s][a[(size_t)r * w + c]];
+    }
+  }
+  for (int d = 0; d < n; d++) {
+    for (int ra = 0; ra < d; ra++) {
+      uint8_t s = a[(size_t)ra * w + d];
+      if (s) for (int c = 0; c < w; c++) a[(size_t)ra * w + c] ^= MUL[s][a[(size_t)d * w + c]];
+    }
+  }
+  for (int r = 0; r < n; r++) memcpy(out + (size_t)r * n, a + (size_t)r * w + n, (size_t)n);
+  free(a);
+  return OR_OK;
+}
+
+/* matrix.go Multiply [upstream]: (r x k) * (k x c) */
+void oracle_matmul(int r, int k, int c, const uint8_t* A, const uint8_t* B, uint8_t* C) {
+  oracle_init();
+  for (int i = 0; i < r; i++)
+    for (int j = 0; j < c; j++) {
+      uint8_t v = 0;
+      for (int t = 0; t < k; t++) v ^= MUL[A[i * k + t]][B[t * c + j]];
+      C[i * c + j] = v;
+    }
+}
+
+/* reedsolomon.New validation [upstream] as reached from ugo/fec.go:59.
+ * (ugo's own newFEC additionally rejects p <= 0 and rxlimit < d+p, :46-51.) */
+int oracle_check_geometry(int d, int p) {
+  if (d <= 0 || p < 0) return OR_ERR_INV_SHARD_NUM;
+  if (d + p > 256) return OR_ERR_MAX_SHARD_NUM;
+  return OR_OK;
+}
+
+/* buildMatrix [upstream]: (d+p) x d systematic encoding matrix. */
+int oracle_matrix(int d, int p, uint8_t* out) {
+  oracle_init();
+  int st = oracle_check_geometry(d, p);
+  if (st) return st;
+  int n = d + p;
+  uint8_t* V = (uint8_t*)malloc((size_t)n * d);
+  uint8_t* Ti = (uint8_t*)malloc((size_t)d * d);
+  for (int r = 0; r < n; r++)
+    for (int c = 0; c < d; c++) V[r * d + c] = oracle_gf_exp((uint8_t)r, c);
+  st = oracle_invert(d, V, Ti); /* top d x d */
+  if (st == OR_OK) oracle_matmul(n, d, d, V, Ti, out);
+  free(V);
+  free(Ti);
+  return st;
+}
+
+/* codeSomeShards [upstream]: out[o][j] = XOR_i rows[o][i] * in[i][j] */
+static void code_some(const uint8_t* rows, int nin, int nout,
+                      const uint8_t* const* in, uint8_t* const* out, size_t S) {
+  for (int o = 0; o < nout; o++) {
+    uint8_t* dst = out[o];
+    memset(dst, 0, S);
+    for (int i = 0; i < nin; i++) {
+      const uint8_t* mt = MUL[rows[o * nin + i]];
+      const uint8_t* src = in[i];
+      for (size_t j = 0; j < S; j++) dst[j] ^= mt[src[j]];
+    }
+  }
+}
+
+/* Encode(shards) on each group of a batch: reads rows [0,d), writes [d,d+p).
+ * ugo/fec.go:238 (calcECC passes data[k][offset:maxlen]; a caller models that
+ * window by pointing `shards` at offset and setting S = maxlen - offset). */
+int oracle_encode(int d, int p, uint8_t* shards, size_t G, size_t S, size_t pitch) {
+  oracle_init();
+  int st = oracle_check_geometry(d, p);
+  if (st) return st;
+  if (S == 0) return OR_ERR_SHARD_NO_DATA;
+  if (pitch < S) return OR_ERR_INVALID_ARG;
+  int n = d + p;
+  uint8_t* M = (uint8_t*)malloc((size_t)n * d);
+  oracle_matrix(d, p, M);
+  const uint8_t** in = (const uint8_t**)malloc(sizeof(void*) * d);
+  uint8_t** out = (uint8_t**)malloc(sizeof(void*) * (p ? p : 1));
+  for (size_t g = 0; g < G; g++) {
+    uint8_t* grp = shards + g * (size_t)n * pitch;
+    for (int k = 0; k < d; k++) in[k] = grp + (size_t)k * pitch;
+    for (int k = 0; k < p; k++) out[k] = grp + (size_t)(d + k) * pitch;
+    code_some(M + (size_t)d * d, d, p, in, out, S);
+  }
+  free(in); free(out); free(M);
+  return OR_OK;
+}
+
+/* Reconstruct(shards) [upstream], one group.  present_mask bit r = shard r is
+ * non-empty (len(shards[r]) != 0).  Erased rows are (over)written. */
+static int recon_group(int d, int p, const uint8_t* M, uint8_t* grp, uint64_t present_mask,
+                       size_t S, size_t pitch, int data_only) {
+  int n = d + p;
+  int npresent = 0, dpresent = 0;
+  for (int r = 0; r < n; r++)
+    if ((present_mask >> r) & 1) { npresent++; if (r < d) dpresent++; }
+  if (npresent == n || (data_only && dpresent == d)) return OR_OK;
+  if (npresent < d) return OR_ERR_TOO_FEW_SHARDS;
+
+  int* valid = (int*)malloc(sizeof(int) * d);
+  uint8_t* sub = (uint8_t*)malloc((size_t)d * d);
+  uint8_t* inv = (uint8_t*)malloc((size_t)d * d);
+  const uint8_t** subsh = (const uint8_t**)malloc(sizeof(void*) * d);
+  int cnt = 0;
+  /* first d present rows in index order */
+  for (int r = 0; r < n && cnt < d; r++)
+    if ((present_mask >> r) & 1) { valid[cnt] = r; subsh[cnt] = grp + (size_t)r * pitch; cnt++; }
+  for (int i = 0; i < d; i++) memcpy(sub + (size_t)i * d, M + (size_t)valid[i] * d, (size_t)d);
+  int st = oracle_invert(d, sub, inv);
+  if (st) { free(valid); free(sub); free(inv); free(subsh); return st; }
+
+  /* stage 1: missing data rows from the survivors */
+  for (int r = 0; r < d; r++) {
+    if ((present_mask >> r) & 1) continue;
+    uint8_t* dst = grp + (size_t)r * pitch;
+    code_some(inv + (size_t)r * d, d, 1, subsh, &dst, S);
+  }
+  if (!data_only) {
+    /* stage 2: missing parity rows re-encoded from the completed data rows */
+    const uint8_t** data = (const uint8_t**)malloc(sizeof(void*) * d);
+    for (int k = 0; k < d; k++) data[k] = grp + (size_t)k * pitch;
+    for (int r = d; r < n; r++) {
+      if ((present_mask >> r) & 1) continue;
+      uint8_t* dst = grp + (size_t)r * pitch;
+      code_some(M + (size_t)r * d, d, 1, data, &dst, S);
+    }
+    free(data);
+  }
+  free(valid); free(sub); free(inv); free(subsh);
+  return OR_OK;
+}
+
+typedef struct {
+  int d, p, data_only;
+  const uint8_t* M;
+  uint8_t* shards;
+  const uint64_t* present;
+  size_t S, pitch, g0, g1;
+  int8_t* status;
+  int rc;
+} recon_job;
+
+static void* recon_worker(void* arg) {
+  recon_job* j = (recon_job*)arg;
+  int n = j->d + j->p;
+  j->rc = OR_OK;
+  for (size_t g = j->g0; g < j->g1; g++) {
+    int st = recon_group(j->d, j->p, j->M, j->shards + g * (size_t)n * j->pitch,
+                         j->present[g], j->S, j->pitch, j->data_only);
+    if (j->status) j->status[g] = (int8_t)st;
+    if (st && !j->rc) j->rc = st;
+  }
+  return NULL;
+}
+
+/* Reconstruct over a batch.  Returns the first failing group's status (or OK);
+ * status[g] (nullable) receives each group's status.  threads >= 1 splits the
+ * groups into contiguous ranges (CPU baseline only). */
+int oracle_reconstruct_mt(int d, int p, uint8_t* shards, const uint64_t* present, size_t G,
+                          size_t S, size_t pitch, int data_only, int8_t* status, int threads) {
+  oracle_init();
+  int st = oracle_check_geometry(d, p);
+  if (st) return st;
+  if (d + p > 64) return OR_ERR_INVALID_ARG; /* batch masks are 64-bit */
+  if (S == 0) return OR_ERR_SHARD_NO_DATA;
+  if (pitch < S) return OR_ERR_INVALID_ARG;
+  int n = d + p;
+  uint8_t* M = (uint8_t*)malloc((size_t)n * d);
+  oracle_matrix(d, p, M);
+  if (threads < 1) threads = 1;
+  if ((size_t)threads > G) threads = G ? (int)G : 1;
+  recon_job* jobs = (recon_job*)calloc((size_t)threads, sizeof(recon_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  for (int t = 0; t < threads; t++) {
+    recon_job* j = &jobs[t];
+    j->d = d; j->p = p; j->data_only = data_only; j->M = M; j->shards = shards;
+    j->present = present; j->S = S; j->pitch = pitch; j->status = status;
+    j->g0 = G * (size_t)t / (size_t)threads;
+    j->g1 = G * (size_t)(t + 1) / (size_t)threads;
+  }
+  if (threads == 1) recon_worker(&jobs[0]);
+  else {
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, recon_worker, &jobs[t]);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  }
+  int rc = OR_OK;
+  for (int t = 0; t < threads; t++) if (jobs[t].rc && !rc) rc = jobs[t].rc;
+  free(jobs); free(th); free(M);
+  return rc;
+}
+
+int oracle_reconstruct(int d, int p, uint8_t* shards, const uint64_t* present, size_t G,
+                       size_t S, size_t pitch, int data_only, int8_t* status) {
+  return oracle_reconstruct_mt(d, p, shards, present, G, S, pitch, data_only, status, 1);
+}
+
+typedef struct {
+  int d, p;
+  uint8_t* shards;
+  size_t S, pitch, g0, g1;
+} enc_job;
+
+static void* enc_worker(void* arg) {
+  enc_job* j = (enc_job*)arg;
+  int n = j->d + j->p;
+  oracle_encode(j->d, j->p, j->shards + j->g0 * (size_t)n * j->pitch, j->g1 - j->g0, j->S, j->pitch);
+  return NULL;
+}
+
+/* multi-threaded encode (CPU baseline only) */
+int oracle_encode_mt(int d, int p, uint8_t* shards, size_t G, size_t S, size_t pitch, int threads) {
+  oracle_init();
+  int st = oracle_check_geometry(d, p);
+  if (st) return st;
+  if (threads <= 1 || G < 2) return oracle_encode(d, p, shards, G, S, pitch);
+  if ((size_t)threads > G) threads = (int)G;
+  enc_job* jobs = (enc_job*)calloc((size_t)threads, sizeof(enc_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  for (int t = 0; t < threads; t++) {
+    enc_job* j = &jobs[t];
+    j->d = d; j->p = p; j->shards = shards; j->S = S; j->pitch = pitch;
+    j->g0 = G * (size_t)t / (size_t)threads;
+    j->g1 = G * (size_t)(t + 1) / (size_t)threads;
+    pthread_create(&th[t], NULL, enc_worker, j);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  free(jobs); free(th);
+  return OR_OK;
+}
+
+/* checkShards(shards, nilok) [upstream] on a list of shard lengths.
+ * Returns the common size through *size_out. */
+int oracle_check_shards(int n, const size_t* lens, int nil_ok, size_t* size_out) {
+  size_t size = 0;
+  for (int i = 0; i < n; i++) if (lens[i] != 0) { size = lens[i]; break; }
+  if (size_out) *size_out = size;
+  if (size == 0) return OR_ERR_SHARD_NO_DATA;
+  for (int i = 0; i < n; i++)
+    if (lens[i] != size && (lens[i] != 0 || !nil_ok)) return OR_ERR_SHARD_SIZE;
+  return OR_OK;
+}
+
+/* splitmix64 -- the synthetic-data generator shared with the product's bench
+ * (SURVEY.md §8d): byte stream of row r of group g = splitmix64 counter stream
+ * seeded with seed ^ (g*(d+p)+r). */
+static inline uint64_t splitmix64(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void oracle_fill(uint8_t* shards, int n, size_t G, size_t S, size_t pitch, uint64_t seed, int rows) {
+  /* fills rows [0, rows) of every group; bytes [S, pitch) left as is */
+  for (size_t g = 0; g < G; g++)
+    for (int r = 0; r < rows; r++) {
+      uint64_t st = seed ^ (g * (uint64_t)n + (uint64_t)r);
+      uint8_t* row = shards + (g * (size_t)n + (size_t)r) * pitch;
+      size_t j = 0;
+      while (j < S) {
+        uint64_t v = splitmix64(&st);
+        for (int b = 0; b < 8 && j < S; b++, j++) row[j] = (uint8_t)(v >> (8 * b));
+      }
+    }
+}

@@ -1,0 +1,279 @@
+"""GPU parity: the gfx950 kernels (through the C-ABI) are bit-exact against the
+CPU oracle (oracle/rs_oracle.c) on the same seeded inputs, on the committed
+golden fixtures, and -- at BASELINE sizes -- on size-independent properties
+(encode -> erase -> reconstruct round trip, linearity).
+
+Oracle = checker only; every result compared here was computed on the GPU.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import rs_ref
+from ugo_amd import fec
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _rand(G, n, pitch, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randint(0, 256, (G, n, pitch), dtype=torch.uint8, generator=g)
+
+
+def _dev(x):
+    return torch.as_tensor(x).contiguous().cuda()
+
+
+def _masks_to_dev(masks):
+    return torch.as_tensor(np.asarray(masks, dtype=np.uint64).view(np.int64)).cuda()
+
+
+def _erase(arr, masks, n):
+    arr = arr.copy()
+    for g, m in enumerate(masks):
+        for r in range(n):
+            if not (int(m) >> r) & 1:
+                arr[g, r] = 0
+    return arr
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return dict(np.load(os.path.join(GOLD, "fixtures_v1.npz")))
+
+
+def test_matrix_matches_oracle(gpu):
+    for d, p in [(10, 3), (32, 8), (5, 5), (1, 1), (20, 4)]:
+        enc = fec.New(d, p)
+        assert np.array_equal(enc.matrix(), rs_ref.c_matrix(d, p))
+
+
+@pytest.mark.parametrize("S,pitch", [(1350, 1360), (1350, 1350), (1476, 1488), (16, 16), (1, 16), (1000, 1024)])
+def test_encode_10_3_vs_oracle(gpu, S, pitch):
+    d, p, n, G = 10, 3, 13, 777
+    host = _rand(G, n, pitch, 1 + S).numpy()
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    t = _dev(host)
+    enc = fec.New(d, p)
+    enc.encode_batch(t, shard_size=S)
+    torch.cuda.synchronize()
+    got = t.cpu().numpy()
+    assert np.array_equal(got[:, :, :S], want[:, :, :S])
+    assert np.array_equal(got[:, :, S:], host[:, :, S:]), "padding columns must not be written"
+
+
+def test_golden_fixtures_on_gpu(gpu, fx):
+    enc = fec.New(10, 3)
+    data = fx["g10_enc_data"]
+    t = torch.zeros((data.shape[0], 13, 1360), dtype=torch.uint8)
+    t[:, :10, :1350] = torch.as_tensor(data)
+    t = t.cuda()
+    enc.encode_batch(t, shard_size=1350)
+    assert np.array_equal(t.cpu().numpy()[:, 10:, :1350], fx["g10_enc_parity"])
+    for key in ("g10", "g10x"):
+        src = fx[f"{key}_in"]
+        pitch = ((src.shape[2] + 15) // 16) * 16
+        t = torch.zeros((src.shape[0], 13, pitch), dtype=torch.uint8)
+        t[:, :, :src.shape[2]] = torch.as_tensor(src)
+        t = t.cuda()
+        st = torch.full((src.shape[0],), -1, dtype=torch.int8, device="cuda")
+        enc.reconstruct_batch(t, _masks_to_dev(fx[f"{key}_mask"]), shard_size=src.shape[2], status=st)
+        assert np.array_equal(t.cpu().numpy()[:, :, :src.shape[2]], fx[f"{key}_out"])
+        assert (st.cpu() == 0).all()
+    # jumbo (32+8)x9000, 8 mixed erasures: d+p = 40 > 16 -> per-group device descriptors
+    j = fx["g32_out"]
+    mk = fx["g32_mask"]
+    jin = _erase(j, mk, 40)
+    enc32 = fec.New(32, 8)
+    t = torch.zeros((1, 40, 9008), dtype=torch.uint8)
+    t[:, :, :9000] = torch.as_tensor(jin)
+    t = t.cuda()
+    enc32.reconstruct_batch(t, _masks_to_dev(mk), shard_size=9000)
+    assert np.array_equal(t.cpu().numpy()[:, :, :9000], j)
+    # calcECC window (offset 6 -> unaligned base): byte-granular kernel path
+    buf = fx["calcecc_in"]
+    t = _dev(buf)
+    base = t[:, :, 6:]
+    lib = fec.load_library()
+    rc = lib.ugo_fec_encode(enc._h, base.data_ptr(), 1, 1100 - 6, 1476, fec._stream_handle(None))
+    assert rc == 0
+    assert np.array_equal(t.cpu().numpy(), fx["calcecc_out"])
+
+
+def test_reconstruct_every_pattern_10_3(gpu):
+    """All 8192 presence masks of a (10+3) group, one group each, in one batch."""
+    d, p, n, S, pitch = 10, 3, 13, 1350, 1360
+    masks = np.arange(1 << n, dtype=np.uint64)
+    G = len(masks)
+    host = _rand(G, n, pitch, 5).numpy()
+    rs_ref.c_encode(d, p, host, S=S)  # consistent codewords (oracle builds the input only)
+    inp = _erase(host, masks, n)
+    want = inp.copy()
+    rc, want_st = rs_ref.c_reconstruct(d, p, want, masks, S=S)
+    t = _dev(inp)
+    st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    enc = fec.New(d, p)
+    enc.reconstruct_batch(t, _masks_to_dev(masks), shard_size=S, status=st)
+    got = t.cpu().numpy()
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(got[:, :, :S], want[:, :, :S])
+    ok = np.array([bin(int(m)).count("1") >= d for m in masks])
+    assert np.array_equal(got[ok][:, :, :S], host[ok][:, :, :S])  # round trip
+
+
+@pytest.mark.parametrize("table_max", ["16", "0"])
+def test_reconstruct_inconsistent_inputs(gpu, table_max, monkeypatch):
+    """Rows that are not a codeword (stale pool tails, ugo/fec.go:84-87): output
+    depends on the survivor choice, which must be klauspost's (first d present).
+    table_max=0 forces the per-group device descriptor path (k_prepare)."""
+    monkeypatch.setenv("UGO_FEC_TABLE_MAX_SHARDS", table_max)
+    d, p, n, S, pitch = 10, 3, 13, 1350, 1360
+    G = 4096
+    rng = np.random.default_rng(9)
+    host = _rand(G, n, pitch, 9).numpy()
+    masks = rng.integers(0, 1 << n, G).astype(np.uint64)
+    masks[:64] = (1 << n) - 1  # nothing to do
+    want = host.copy()
+    rc, want_st = rs_ref.c_reconstruct(d, p, want, masks, S=S)
+    t = _dev(host)
+    st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    enc = fec.New(d, p)
+    enc.reconstruct_batch(t, _masks_to_dev(masks), shard_size=S, status=st)
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(t.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("d,p,S,pitch", [(4, 2, 100, 112), (5, 5, 64, 64), (12, 4, 333, 336),
+                                         (20, 4, 200, 208), (32, 8, 9000, 9008), (3, 1, 50, 50),
+                                         (40, 6, 70, 80), (1, 1, 7, 16), (7, 0, 32, 32)])
+def test_generic_geometries(gpu, d, p, S, pitch):
+    n = d + p
+    G = 300
+    host = _rand(G, n, pitch, d * 100 + p).numpy()
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    enc = fec.New(d, p)
+    t = _dev(host)
+    enc.encode_batch(t, shard_size=S)
+    got = t.cpu().numpy()
+    assert np.array_equal(got, want)
+    if p == 0:
+        return
+    rng = np.random.default_rng(d + p)
+    masks = np.zeros(G, np.uint64)
+    for g in range(G):
+        e = int(rng.integers(0, p + 2))  # includes too-few-shards groups
+        er = rng.choice(n, size=min(e, n), replace=False)
+        m = (1 << n) - 1
+        for r in er:
+            m &= ~(1 << int(r))
+        masks[g] = m
+    inp = _erase(got, masks, n)
+    want2 = inp.copy()
+    rc, want_st = rs_ref.c_reconstruct(d, p, want2, masks, S=S)
+    for data_only in (False, True):
+        want3 = inp.copy()
+        rs_ref.c_reconstruct(d, p, want3, masks, S=S, data_only=data_only)
+        t = _dev(inp)
+        st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+        enc.reconstruct_batch(t, _masks_to_dev(masks), shard_size=S, data_only=data_only, status=st)
+        assert np.array_equal(st.cpu().numpy(), want_st)
+        assert np.array_equal(t.cpu().numpy(), want3), (d, p, data_only)
+
+
+def test_full_size_round_trip_and_linearity(gpu):
+    """BASELINE configs[1]/[2] size: 65536 groups (10+3)x1350, 2 random erasures."""
+    d, p, n, S, pitch, G = 10, 3, 13, 1350, 1360, 65536
+    enc = fec.New(d, p)
+    a = torch.randint(0, 256, (G, n, pitch), dtype=torch.uint8, device="cuda")
+    b = torch.randint(0, 256, (G, n, pitch), dtype=torch.uint8, device="cuda")
+    ab = a ^ b
+    for x in (a, b, ab):
+        enc.encode_batch(x, shard_size=S)
+    assert torch.equal((a ^ b)[:, :, :S], ab[:, :, :S])  # GF linearity
+    ref = a.clone()
+    gen = torch.Generator(device="cpu").manual_seed(2)
+    e1 = torch.randint(0, n, (G,), generator=gen)
+    e2 = (e1 + torch.randint(1, n, (G,), generator=gen)) % n
+    masks = ((1 << n) - 1) ^ (1 << e1) ^ (1 << e2)
+    masks = masks.to(torch.int64).cuda()
+    gi = torch.arange(G, device="cuda")
+    a[gi, e1.cuda()] = 0
+    a[gi, e2.cuda()] = 0
+    enc.reconstruct_batch(a, masks, shard_size=S)
+    assert torch.equal(a[:, :, :S], ref[:, :, :S])
+    # spot-check a sample against the oracle too
+    idx = torch.randint(0, G, (64,), generator=gen)
+    sample = ref[idx.cuda()].cpu().numpy().copy()
+    want = sample.copy()
+    want[:, d:] = 0
+    rs_ref.c_encode(d, p, want, S=S)
+    assert np.array_equal(sample[:, :, :S], want[:, :, :S])
+
+
+def test_go_shaped_api(gpu):
+    enc = fec.New(10, 3)
+    rng = np.random.default_rng(4)
+    shards = [bytearray(rng.integers(0, 256, 1350, dtype=np.uint8).tobytes()) for _ in range(10)] + \
+             [bytearray(1350) for _ in range(3)]
+    enc.Encode(shards)
+    ref = [bytes(s) for s in shards]
+    want = np.array([list(s) for s in ref], np.uint8)[None].copy()
+    w2 = want.copy()
+    w2[:, 10:] = 0
+    rs_ref.c_encode(10, 3, w2)
+    assert np.array_equal(w2, want)
+    lost = list(shards)
+    lost[2] = None
+    lost[11] = bytearray()
+    enc.Reconstruct(lost)
+    assert [bytes(s) for s in lost] == ref
+    lost = list(ref)
+    lost = [bytearray(s) for s in lost]
+    lost[0] = lost[1] = lost[12] = None
+    enc.ReconstructData(lost)
+    assert bytes(lost[0]) == ref[0] and bytes(lost[1]) == ref[1] and lost[12] is None
+    with pytest.raises(fec.ErrTooFewShards):
+        enc.Reconstruct([None] * 4 + [bytearray(ref[i]) for i in range(4, 13)])
+    with pytest.raises(fec.ErrTooFewShards):
+        enc.Encode(shards[:12])
+    with pytest.raises(fec.ErrShardSize):
+        enc.Encode(shards[:12] + [bytearray(10)])
+    with pytest.raises(fec.ErrShardNoData):
+        enc.Reconstruct([None] * 13)
+
+
+def test_host_api_pipelined(gpu):
+    """Host buffers staged through the engine's H2D -> kernel -> D2H pipeline,
+    several chunks (jumbo groups: ~180 groups per 64 MiB staging buffer)."""
+    d, p, n, S, pitch, G = 32, 8, 40, 9000, 9008, 600
+    host = _rand(G, n, pitch, 77).numpy()
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    enc = fec.New(d, p)
+    got = host.copy()
+    enc.encode_host(got, S)
+    assert np.array_equal(got, want)
+    rng = np.random.default_rng(5)
+    masks = np.array([((1 << n) - 1) & ~int(sum(1 << int(r) for r in rng.choice(n, int(rng.integers(0, 9)),
+                                                                                 replace=False)))
+                      for _ in range(G)], dtype=np.uint64)
+    inp = _erase(want, masks, n)
+    st = np.full(G, -1, np.int8)
+    out = inp.copy()
+    assert enc.reconstruct_host(out, masks, S, status=st) == 0
+    assert (st == 0).all()
+    assert np.array_equal(out, want)
+    # pinned buffer variant
+    buf = fec.host_alloc(G * n * pitch)
+    try:
+        arr = buf.reshape(G, n, pitch)
+        arr[:] = inp
+        assert enc.reconstruct_host(arr, masks, S) == 0
+        assert np.array_equal(arr, want)
+    finally:
+        fec.host_free(buf)

@@ -1,0 +1,493 @@
+// fec_kernels.hip -- gfx950 (CDNA4) kernels for batched GF(2^8) Reed-Solomon
+// encode / erasure recovery: the arithmetic below reedsolomon.Encoder.Encode
+// (ugo/fec.go:238) and .Reconstruct (ugo/fec.go:202).
+//
+// Work decomposition: a batch is shards[g][row][pitch].  One
+// work item = one 16-byte column chunk of one group: the lane loads that chunk
+// of each input row (global_load_dwordx4; consecutive lanes take consecutive
+// chunks, so a wave's load of one row is 1 KiB contiguous), computes every
+// output row's chunk in registers and stores it.  Each input byte is read from
+// HBM exactly once and each output byte written once: the kernels are
+// HBM-bound byte-field codecs, no MFMA, no LDS on the streaming path.
+//
+// GF(2^8) multiply-accumulate on 4 packed bytes per dword uses Horner's rule
+// over the coefficient bits (bit 7 first):
+//     y = (((T7 * 2) ^ T6) * 2 ^ ...) ^ T0,   Tb = XOR_{k : bit b of c_k} x_k
+// so every output needs 7 "xtime" doublings regardless of the number of
+// inputs, and the inputs enter only through XORs.  xtime on 4 bytes:
+//     mask = v_perm_b32(y << 8, y, 0x090b080a)   (0xff in bytes whose bit 7 is
+//            set: the sign-replicate selectors 8..11 read bytes 1,3 of y and of
+//            y << 8)
+//     xt   = ((y & 0x7f7f7f7f) << 1) ^ (mask & 0x1d1d1d1d)
+//
+//  * k_encode_c<D,P>: coefficients are compile-time (gf::Code<D,P>), so the
+//    XOR network is fixed at compile time -- used for the (10,3) headline and
+//    the (32,8) jumbo geometry.
+//  * k_apply<DMAX,MODE>: coefficients come from a *descriptor* (input rows,
+//    output rows, e x d coefficient matrix).  MODE 0: one descriptor for all
+//    groups (generic encode); MODE 1: descriptor table indexed by the group's
+//    presence mask (d+p <= 16, built on the host at create time); MODE 2: one
+//    descriptor per group written by k_prepare (larger codes).  A coefficient
+//    bit becomes a lane mask with v_bfe_i32 and enters through v_bitop3
+//    (y ^ (x & m)); the mask is reused for all 4 dwords of the chunk.
+//  * k_apply_bytes<MODE>: any pitch / alignment / d, 4 columns per lane with
+//    byte loads -- the correctness path for layouts the fast path rejects.
+//  * k_prepare: per-group decode descriptor on device (first d present rows
+//    -> d x d sub-matrix -> Gauss-Jordan in LDS -> reconstruct coefficients).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "fec_kernels.hpp"
+#include "gf256.hpp"
+
+namespace ugo {
+namespace kern {
+
+// ---------------------------------------------------------------- helpers
+struct V4 {
+  uint32_t v[4];
+};
+
+__device__ __forceinline__ uint32_t xt1(uint32_t y) {
+  const uint32_t s8 = y << 8;
+  const uint32_t m = __builtin_amdgcn_perm(s8, y, 0x090b080au);
+  return ((y & 0x7f7f7f7fu) << 1) ^ (m & 0x1d1d1d1du);
+}
+
+__device__ __forceinline__ void xt4(V4& y) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y.v[j] = xt1(y.v[j]);
+}
+
+__device__ __forceinline__ void xor4(V4& y, const V4& x) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y.v[j] ^= x.v[j];
+}
+
+// v_bitop3_b32 truth tables (bit index = a*4 + b*2 + c)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c
+}
+__device__ __forceinline__ uint32_t xor_and(uint32_t y, uint32_t x, uint32_t m) {
+  return __builtin_amdgcn_bitop3_b32(y, x, m, 0x78);  // y ^ (x & m)
+}
+
+__device__ __forceinline__ void xor4_2(V4& y, const V4& a, const V4& b) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y.v[j] = xor3(y.v[j], a.v[j], b.v[j]);
+}
+
+__device__ __forceinline__ V4 load16(const uint8_t* p) {
+  const uint4 q = *reinterpret_cast<const uint4*>(p);
+  V4 r;
+  r.v[0] = q.x;
+  r.v[1] = q.y;
+  r.v[2] = q.z;
+  r.v[3] = q.w;
+  return r;
+}
+
+// store the first nb (1..16) bytes of a chunk
+__device__ __forceinline__ void store16(uint8_t* p, const V4& y, uint32_t nb) {
+  if (nb >= 16) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
+    return;
+  }
+  // tail chunk of a row whose length is not a multiple of 16: rare lanes
+  uint32_t j = 0;
+  for (; j + 4 <= nb; j += 4) *reinterpret_cast<uint32_t*>(p + j) = y.v[j >> 2];
+  uint32_t w = y.v[j >> 2];
+  for (; j < nb; ++j) {
+    p[j] = static_cast<uint8_t>(w);
+    w >>= 8;
+  }
+}
+
+// ------------------------------------------------ compile-time coefficients
+template <int D, int P, int I, int B, int K>
+__device__ __forceinline__ constexpr bool cbit() {
+  return ((gf::Code<D, P>::M.at(D + I, K) >> B) & 1) != 0;
+}
+
+template <int D, int P, int I, int B, int... K>
+__device__ __forceinline__ constexpr bool any_bit(std::integer_sequence<int, K...>) {
+  return (cbit<D, P, I, B, K>() || ...);
+}
+
+template <int D, int P, int I, int B>
+__device__ __forceinline__ constexpr bool any_bit_at_or_above() {
+  if constexpr (B > 7) {
+    return false;
+  } else {
+    return any_bit<D, P, I, B>(std::make_integer_sequence<int, D>{}) ||
+           any_bit_at_or_above<D, P, I, B + 1>();
+  }
+}
+
+// The inputs whose coefficient has bit B set, for output I, as a compile-time list.
+template <int D, int P, int I, int B>
+struct Terms {
+  struct List {
+    int n;
+    int k[D];
+  };
+  static constexpr List make() {
+    List l{};
+    for (int k = 0; k < D; ++k)
+      if ((gf::Code<D, P>::M.at(D + I, k) >> B) & 1) l.k[l.n++] = k;
+    return l;
+  }
+  static constexpr List L = make();
+};
+
+// y ^= x[terms J..], two terms per v_bitop3 (3-input XOR)
+template <int D, int P, int I, int B, int J>
+__device__ __forceinline__ void cterms(V4& y, const V4* x) {
+  constexpr int n = Terms<D, P, I, B>::L.n;
+  if constexpr (J + 1 < n) {
+    constexpr int k0 = Terms<D, P, I, B>::L.k[J];
+    constexpr int k1 = Terms<D, P, I, B>::L.k[J + 1];
+    xor4_2(y, x[k0], x[k1]);
+    cterms<D, P, I, B, J + 2>(y, x);
+  } else if constexpr (J < n) {
+    constexpr int k0 = Terms<D, P, I, B>::L.k[J];
+    xor4(y, x[k0]);
+  }
+}
+
+// Horner step for bit B of output I (called for B = 7 .. 0)
+template <int D, int P, int I, int B>
+__device__ __forceinline__ void chorner(V4& y, const V4* x) {
+  constexpr int n = Terms<D, P, I, B>::L.n;
+  if constexpr (any_bit_at_or_above<D, P, I, B + 1>()) {
+    xt4(y);  // y *= 2
+    cterms<D, P, I, B, 0>(y, x);
+  } else if constexpr (n > 0) {
+    constexpr int k0 = Terms<D, P, I, B>::L.k[0];
+    y = x[k0];  // first non-zero bit plane: y was 0
+    cterms<D, P, I, B, 1>(y, x);
+  }
+  if constexpr (B > 0) chorner<D, P, I, B - 1>(y, x);
+}
+
+template <int D, int P, int I>
+__device__ __forceinline__ V4 cparity(const V4* x) {
+  V4 y{{0u, 0u, 0u, 0u}};
+  chorner<D, P, I, 7>(y, x);
+  return y;
+}
+
+// compute and store parity rows one at a time (short live ranges)
+template <int D, int P, int... I>
+__device__ __forceinline__ void cparity_store(uint8_t* gp, uint64_t pitch, uint32_t nb, const V4* x,
+                                              std::integer_sequence<int, I...>) {
+  ((store16(gp + static_cast<uint64_t>(D + I) * pitch, cparity<D, P, I>(x), nb)), ...);
+}
+
+template <int D, int P>
+__global__ __launch_bounds__(256) void k_encode_c(Batch a) {
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t gl = item / a.chunks;
+  const uint32_t c = item - gl * a.chunks;
+  uint8_t* gp = a.base + (a.g0 + gl) * a.group_bytes + static_cast<uint64_t>(c) * 16u;
+  V4 x[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) x[k] = load16(gp + static_cast<uint64_t>(k) * a.pitch);
+  const uint32_t nb = a.S - c * 16u;
+  cparity_store<D, P>(gp, a.pitch, nb, x, std::make_integer_sequence<int, P>{});
+}
+
+// ----------------------------------------------- descriptor-driven kernels
+// Descriptor, byte offsets:
+//   [0] e_total  [1] e_data  [2] status  [3] reserved
+//   [4, 4+dpad)            input rows (survivors / data rows)
+//   [4+dpad, 4+dpad+epad)  output rows: erased data rows, then erased parity
+//   [4+dpad+epad + i*dpad] coefficient row i (d bytes, zero padded)
+template <int MODE>
+__device__ __forceinline__ const uint8_t* desc_for(const Batch& a, uint64_t g) {
+  if constexpr (MODE == 0) {
+    return a.desc;
+  } else if constexpr (MODE == 1) {
+    const uint64_t m = a.present[g] & a.nmask;
+    return a.desc + m * a.desc_stride;
+  } else {
+    return a.desc + (g - a.g_desc0) * a.desc_stride;
+  }
+}
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
+  return *reinterpret_cast<const uint32_t*>(p);
+}
+
+template <int DMAX, int MODE>
+__global__ __launch_bounds__(256) void k_apply(Batch a) {
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t gl = item / a.chunks;
+  const uint32_t c = item - gl * a.chunks;
+  const uint64_t g = a.g0 + gl;
+  const uint8_t* desc = desc_for<MODE>(a, g);
+  const uint32_t hdr = ld32(desc);
+  const uint32_t st = (hdr >> 16) & 0xffu;
+  if (MODE != 0 && a.status != nullptr && c == 0) a.status[g] = static_cast<int8_t>(st);
+  const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
+  if (st != 0 || e == 0) return;
+
+  uint8_t* gp = a.base + g * a.group_bytes + static_cast<uint64_t>(c) * 16u;
+  constexpr int NW = (DMAX + 3) / 4;
+  uint32_t rows[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) rows[w] = ld32(desc + 4 + 4 * w);
+  V4 x[DMAX];
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    if (k < static_cast<int>(a.d)) {
+      const uint32_t r = (rows[k >> 2] >> (8 * (k & 3))) & 0xffu;
+      x[k] = load16(gp + static_cast<uint64_t>(r) * a.pitch);
+    } else {
+      x[k] = V4{{0u, 0u, 0u, 0u}};
+    }
+  }
+  const uint32_t nb = a.S - c * 16u;
+  const uint8_t* orow = desc + 4 + a.dpad;
+  const uint8_t* coef = orow + a.epad;
+  for (uint32_t i = 0; i < e; ++i) {
+    uint32_t cw[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) cw[w] = ld32(coef + i * a.dpad + 4 * w);
+    V4 y{{0u, 0u, 0u, 0u}};
+#pragma unroll
+    for (int b = 7; b >= 0; --b) {
+      if (b != 7) xt4(y);
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) {
+        // sign-extended 1-bit field = 0 or 0xffffffff  (v_bfe_i32)
+        const uint32_t m = static_cast<uint32_t>(
+            static_cast<int32_t>(cw[k >> 2] << (31 - (8 * (k & 3) + b))) >> 31);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y.v[j] = xor_and(y.v[j], x[k].v[j], m);
+      }
+    }
+    const uint32_t r = orow[i];
+    store16(gp + static_cast<uint64_t>(r) * a.pitch, y, nb);
+  }
+}
+
+// generic: any alignment / pitch / d (<= 255); 4 columns per lane, byte I/O
+__device__ __forceinline__ uint32_t gfmul_var(uint32_t cbyte, uint32_t x) {
+  uint32_t t = 0;
+#pragma unroll
+  for (int b = 7; b >= 0; --b) {
+    t = xt1(t);
+    const uint32_t m = static_cast<uint32_t>(-static_cast<int32_t>((cbyte >> b) & 1u));
+    t = xor_and(t, x, m);
+  }
+  return t;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_apply_bytes(Batch a) {
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t gl = item / a.chunks;  // chunks = ceil(S / 4) here
+  const uint32_t c = item - gl * a.chunks;
+  const uint64_t g = a.g0 + gl;
+  const uint8_t* desc = desc_for<MODE>(a, g);
+  const uint32_t hdr = ld32(desc);
+  const uint32_t st = (hdr >> 16) & 0xffu;
+  if (MODE != 0 && a.status != nullptr && c == 0) a.status[g] = static_cast<int8_t>(st);
+  const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
+  if (st != 0 || e == 0) return;
+  uint8_t* gp = a.base + g * a.group_bytes + static_cast<uint64_t>(c) * 4u;
+  const uint32_t nb = min(4u, a.S - c * 4u);
+  const uint8_t* irow = desc + 4;
+  const uint8_t* orow = desc + 4 + a.dpad;
+  const uint8_t* coef = orow + a.epad;
+  for (uint32_t i = 0; i < e; ++i) {
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < a.d; ++k) {
+      const uint8_t* src = gp + static_cast<uint64_t>(irow[k]) * a.pitch;
+      uint32_t x = 0;
+      for (uint32_t j = 0; j < nb; ++j) x |= static_cast<uint32_t>(src[j]) << (8 * j);
+      acc ^= gfmul_var(coef[i * a.dpad + k], x);
+    }
+    uint8_t* dst = gp + static_cast<uint64_t>(orow[i]) * a.pitch;
+    for (uint32_t j = 0; j < nb; ++j) dst[j] = static_cast<uint8_t>(acc >> (8 * j));
+  }
+}
+
+// ------------------------------------------------------------- k_prepare
+// One 64-lane wave per group builds that group's decode descriptor:
+// survivors = first d present rows (index order), A = M[survivors], Gauss-Jordan
+// over GF(2^8) in LDS, then coefficient rows: Dinv[r] for an erased data row r,
+// M[r] * Dinv for an erased parity row r.  d + p <= 64, so d <= 63 rows fit
+// the wave's lanes one row per lane.
+__device__ __forceinline__ uint8_t lmul(const uint8_t* lg, const uint8_t* ex, uint32_t a,
+                                        uint32_t b) {
+  return (a && b) ? ex[lg[a] + lg[b]] : 0;
+}
+
+__global__ __launch_bounds__(64) void k_prepare(Prep a) {
+  __shared__ uint8_t ex[512];
+  __shared__ uint8_t lg[256];
+  __shared__ uint8_t A[63 * 126];
+  __shared__ uint8_t fcol[64];
+  __shared__ uint8_t surv[64];
+  __shared__ uint8_t outr[64];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t g = a.g0 + blockIdx.x;
+  const uint32_t d = a.d, n = a.n, w = 2 * d;
+  for (uint32_t i = lane; i < 512; i += 64) ex[i] = a.gf_exp[i];
+  for (uint32_t i = lane; i < 256; i += 64) lg[i] = a.gf_log[i];
+  const uint64_t mask = a.present[g] & a.nmask;
+  uint8_t* desc = a.desc + (g - a.g_desc0) * a.desc_stride;
+  const uint32_t np = __popcll(mask);
+  if (np == n || np < d) {
+    if (lane == 0) {
+      const uint32_t st = np < d ? 3u : 0u;
+      *reinterpret_cast<uint32_t*>(desc) = st << 16;
+    }
+    return;
+  }
+  // survivors and erased rows (one candidate row per lane, n <= 64)
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  if (lane < n) {
+    if ((mask >> lane) & 1ull) {
+      const uint32_t rank = __popcll(mask & below);
+      if (rank < d) surv[rank] = static_cast<uint8_t>(lane);
+    } else {
+      const uint32_t er = __popcll(~mask & a.nmask & below);
+      outr[er] = static_cast<uint8_t>(lane);
+    }
+  }
+  __syncthreads();
+  const uint32_t e = n - np;
+  const uint32_t e_data = __popcll(~mask & ((d >= 64) ? ~0ull : ((1ull << d) - 1)));
+  // A = [M[surv] | I]
+  for (uint32_t idx = lane; idx < d * w; idx += 64) {
+    const uint32_t r = idx / w, col = idx - r * w;
+    A[idx] = col < d ? a.M[surv[r] * d + col] : static_cast<uint8_t>(col - d == r ? 1 : 0);
+  }
+  __syncthreads();
+  for (uint32_t r = 0; r < d; ++r) {
+    if (A[r * w + r] == 0) {  // uniform: every lane reads the same LDS byte
+      const bool cand = lane > r && lane < d && A[lane * w + r] != 0;
+      const uint64_t bal = __ballot(cand);
+      if (bal == 0) {  // singular: cannot happen for an MDS code
+        if (lane == 0) *reinterpret_cast<uint32_t*>(desc) = 7u << 16;
+        return;
+      }
+      const uint32_t b = __ffsll(static_cast<long long>(bal)) - 1;
+      for (uint32_t col = lane; col < w; col += 64) {
+        const uint8_t t = A[r * w + col];
+        A[r * w + col] = A[b * w + col];
+        A[b * w + col] = t;
+      }
+      __syncthreads();
+    }
+    const uint32_t piv = A[r * w + r];
+    const uint32_t s = ex[255 - lg[piv]];  // 1 / piv  (piv != 0)
+    __syncthreads();
+    for (uint32_t col = lane; col < w; col += 64) A[r * w + col] = lmul(lg, ex, s, A[r * w + col]);
+    if (lane < d) fcol[lane] = A[lane * w + r];
+    __syncthreads();
+    for (uint32_t idx = lane; idx < d * w; idx += 64) {
+      const uint32_t o = idx / w, col = idx - o * w;
+      if (o != r) A[idx] ^= lmul(lg, ex, fcol[o], A[r * w + col]);
+    }
+    __syncthreads();
+  }
+  // header + rows
+  const uint32_t dpad = a.dpad, epad = a.epad;
+  if (lane == 0) *reinterpret_cast<uint32_t*>(desc) = (e & 0xffu) | (e_data << 8);
+  for (uint32_t i = lane; i < dpad; i += 64) desc[4 + i] = i < d ? surv[i] : 0;
+  for (uint32_t i = lane; i < epad; i += 64) desc[4 + dpad + i] = i < e ? outr[i] : 0;
+  uint8_t* coef = desc + 4 + dpad + epad;
+  for (uint32_t idx = lane; idx < e * dpad; idx += 64) {
+    const uint32_t i = idx / dpad, k = idx - i * dpad;
+    uint8_t v = 0;
+    if (k < d) {
+      const uint32_t r = outr[i];
+      if (r < d) {
+        v = A[r * w + d + k];
+      } else {
+        for (uint32_t j = 0; j < d; ++j) v ^= lmul(lg, ex, a.M[r * d + j], A[j * w + d + k]);
+      }
+    }
+    coef[idx] = v;
+  }
+}
+
+// ------------------------------------------------------------- launchers
+static inline uint32_t blocks_for(uint32_t items, uint32_t bs) { return (items + bs - 1) / bs; }
+
+template <int MODE>
+static hipError_t launch_apply_mode(int dmax, const Batch& a, hipStream_t s) {
+  const dim3 grid(blocks_for(a.items, 256)), block(256);
+  switch (dmax) {
+    case 4: hipLaunchKernelGGL((k_apply<4, MODE>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_apply<8, MODE>), grid, block, 0, s, a); break;
+    case 10: hipLaunchKernelGGL((k_apply<10, MODE>), grid, block, 0, s, a); break;
+    case 12: hipLaunchKernelGGL((k_apply<12, MODE>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_apply<16, MODE>), grid, block, 0, s, a); break;
+    case 24: hipLaunchKernelGGL((k_apply<24, MODE>), grid, block, 0, s, a); break;
+    case 32: hipLaunchKernelGGL((k_apply<32, MODE>), grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+int apply_dmax(int d) {
+  if (d <= 4) return 4;
+  if (d <= 8) return 8;
+  if (d <= 10) return 10;
+  if (d <= 12) return 12;
+  if (d <= 16) return 16;
+  if (d <= 24) return 24;
+  if (d <= 32) return 32;
+  return 0;
+}
+
+bool has_const_encode(int d, int p) { return (d == 10 && p == 3) || (d == 32 && p == 8); }
+
+hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
+  const dim3 grid(blocks_for(a.items, 256)), block(256);
+  if (d == 10 && p == 3)
+    hipLaunchKernelGGL((k_encode_c<10, 3>), grid, block, 0, s, a);
+  else if (d == 32 && p == 8)
+    hipLaunchKernelGGL((k_encode_c<32, 8>), grid, block, 0, s, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s) {
+  switch (mode) {
+    case 0: return launch_apply_mode<0>(dmax, a, s);
+    case 1: return launch_apply_mode<1>(dmax, a, s);
+    case 2: return launch_apply_mode<2>(dmax, a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s) {
+  const dim3 grid(blocks_for(a.items, 256)), block(256);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((k_apply_bytes<0>), grid, block, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_apply_bytes<1>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_apply_bytes<2>), grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s) {
+  hipLaunchKernelGGL(k_prepare, dim3(groups), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace kern
+}  // namespace ugo

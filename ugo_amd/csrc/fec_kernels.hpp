@@ -1,0 +1,56 @@
+// fec_kernels.hpp -- internal interface between the C-ABI (ugo_fec.cpp) and
+// the gfx950 kernels (fec_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace ugo {
+namespace kern {
+
+// One launch covers groups [g0, g0 + items / chunks) of the batch.
+struct Batch {
+  uint8_t* base;            // shards[g][row][pitch] (device)
+  const uint8_t* desc;      // descriptor (MODE 0), table (MODE 1), workspace (MODE 2)
+  const uint64_t* present;  // device presence masks (MODE 1)
+  int8_t* status;           // device per-group status, nullable
+  uint64_t g0;              // first group of this launch
+  uint64_t g_desc0;         // group whose descriptor sits at desc (MODE 2)
+  uint64_t group_bytes;     // (d + p) * pitch
+  uint64_t nmask;           // (1 << (d+p)) - 1
+  uint32_t pitch;
+  uint32_t S;               // shard size in bytes
+  uint32_t chunks;          // column chunks per group (16 B, or 4 B for the byte kernel)
+  uint32_t items;           // groups_in_launch * chunks
+  uint32_t desc_stride;
+  uint32_t d;
+  uint32_t dpad;
+  uint32_t epad;
+  uint32_t data_only;
+};
+
+struct Prep {
+  uint8_t* desc;            // workspace: one descriptor per group
+  const uint64_t* present;
+  const uint8_t* M;         // (d+p) x d encoding matrix (device)
+  const uint8_t* gf_exp;    // 512 B
+  const uint8_t* gf_log;    // 256 B
+  uint64_t g0;
+  uint64_t g_desc0;
+  uint64_t nmask;
+  uint32_t desc_stride;
+  uint32_t d;
+  uint32_t n;
+  uint32_t dpad;
+  uint32_t epad;
+};
+
+int apply_dmax(int d);  // register-array bucket for k_apply, 0 if d > 32
+bool has_const_encode(int d, int p);
+hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s);
+hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s);
+hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s);
+hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s);
+
+}  // namespace kern
+}  // namespace ugo

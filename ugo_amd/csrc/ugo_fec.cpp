@@ -1,0 +1,495 @@
+// ugo_fec.cpp -- C-ABI (include/ugo_fec.h) of the MI355X FEC engine.
+//
+// Host-side control plane only: geometry validation (reedsolomon.New as called
+// at ugo/fec.go:59), the code matrix, the decode-descriptor table (the analogue
+// of klauspost's inversion-tree cache, built once per context instead of per
+// erasure pattern on first use), argument checks mirroring checkShards, and
+// launch selection.  All byte arithmetic runs in the gfx950 kernels of
+// fec_kernels.hip; there is no CPU compute path for shard bytes.
+#include "../../include/ugo_fec.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "fec_kernels.hpp"
+#include "gf256.hpp"
+
+namespace {
+
+constexpr int kStreams = 3;
+constexpr size_t kStageBytes = size_t(64) << 20;  // per host-path staging buffer
+constexpr uint32_t kMaxItems = 0x7fffffffu;
+
+inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+struct ugo_fec {
+  int device = 0;
+  int d = 0, p = 0, n = 0;
+  std::vector<uint8_t> M;  // n x d
+  uint32_t dpad = 0, epad = 0, desc_stride = 0;
+  int table_max = 16;       // d+p <= table_max -> host-built pattern table (MODE 1)
+  uint8_t* d_M = nullptr;
+  uint8_t* d_gf = nullptr;  // exp[512] | log[256]
+  uint8_t* d_encdesc = nullptr;
+  uint8_t* d_table = nullptr;
+  uint8_t* d_work = nullptr;  // MODE 2 per-group descriptors
+  size_t work_groups = 0;
+  // host-path staging
+  hipStream_t streams[kStreams] = {};
+  uint8_t* d_stage[kStreams] = {};
+  uint64_t* d_mask[kStreams] = {};
+  int8_t* d_status[kStreams] = {};
+  size_t stage_groups = 0;  // groups per staging buffer
+  size_t stage_pitch = 0;
+};
+
+namespace {
+
+// Decode descriptor for one presence mask (layout: fec_kernels.hip).
+// Survivors = first d present rows in index order (klauspost Reconstruct),
+// outputs = erased data rows then erased parity rows, coefficients
+// Dinv[r] (data row r) or M[r] * Dinv (parity row r).
+int build_desc(const ugo_fec* c, uint64_t mask, uint8_t* out) {
+  const int d = c->d, n = c->n;
+  std::memset(out, 0, c->desc_stride);
+  int np = 0;
+  for (int r = 0; r < n; ++r) np += (mask >> r) & 1;
+  if (np == n) return UGO_FEC_OK;  // e = 0: nothing to rebuild
+  if (np < d) {
+    out[2] = UGO_FEC_ERR_TOO_FEW_SHARDS;
+    return UGO_FEC_OK;
+  }
+  std::vector<uint8_t> sub(size_t(d) * d), inv(size_t(d) * d), work(size_t(2) * d * d);
+  std::vector<int> surv, outr;
+  for (int r = 0; r < n; ++r) {
+    if ((mask >> r) & 1) {
+      if (int(surv.size()) < d) surv.push_back(r);
+    } else {
+      outr.push_back(r);
+    }
+  }
+  for (int i = 0; i < d; ++i) std::memcpy(&sub[size_t(i) * d], &c->M[size_t(surv[i]) * d], d);
+  if (!ugo::gf::invert(d, sub.data(), inv.data(), work.data())) {
+    out[2] = UGO_FEC_ERR_SINGULAR;
+    return UGO_FEC_ERR_SINGULAR;
+  }
+  int e_data = 0;
+  for (int r : outr) e_data += r < d;
+  out[0] = static_cast<uint8_t>(outr.size());
+  out[1] = static_cast<uint8_t>(e_data);
+  for (int i = 0; i < d; ++i) out[4 + i] = static_cast<uint8_t>(surv[i]);
+  for (size_t i = 0; i < outr.size(); ++i) out[4 + c->dpad + i] = static_cast<uint8_t>(outr[i]);
+  uint8_t* coef = out + 4 + c->dpad + c->epad;
+  for (size_t i = 0; i < outr.size(); ++i) {
+    const int r = outr[i];
+    for (int k = 0; k < d; ++k) {
+      uint8_t v;
+      if (r < d) {
+        v = inv[size_t(r) * d + k];
+      } else {
+        v = 0;
+        for (int j = 0; j < d; ++j) v ^= ugo::gf::mul(c->M[size_t(r) * d + j], inv[size_t(j) * d + k]);
+      }
+      coef[i * c->dpad + k] = v;
+    }
+  }
+  return UGO_FEC_OK;
+}
+
+int hip_status(hipError_t e) { return e == hipSuccess ? UGO_FEC_OK : UGO_FEC_ERR_HIP; }
+
+void free_ctx(ugo_fec* c) {
+  if (!c) return;
+  DeviceGuard g(c->device);
+  (void)hipFree(c->d_M);
+  (void)hipFree(c->d_gf);
+  (void)hipFree(c->d_encdesc);
+  (void)hipFree(c->d_table);
+  (void)hipFree(c->d_work);
+  for (int i = 0; i < kStreams; ++i) {
+    (void)hipFree(c->d_stage[i]);
+    (void)hipFree(c->d_mask[i]);
+    (void)hipFree(c->d_status[i]);
+    if (c->streams[i]) (void)hipStreamDestroy(c->streams[i]);
+  }
+  delete c;
+}
+
+bool fast_layout(const ugo_fec* c, const uint8_t* shards, size_t pitch) {
+  return (reinterpret_cast<uintptr_t>(shards) % 16 == 0) && (pitch % 16 == 0) &&
+         ugo::kern::apply_dmax(c->d) != 0 && pitch <= 0xffffffffu;
+}
+
+ugo::kern::Batch base_batch(const ugo_fec* c, uint8_t* shards, size_t S, size_t pitch) {
+  ugo::kern::Batch a{};
+  a.base = shards;
+  a.group_bytes = uint64_t(c->n) * pitch;
+  a.nmask = c->n >= 64 ? ~0ull : ((1ull << c->n) - 1);
+  a.pitch = static_cast<uint32_t>(pitch);
+  a.S = static_cast<uint32_t>(S);
+  a.desc_stride = c->desc_stride;
+  a.d = static_cast<uint32_t>(c->d);
+  a.dpad = c->dpad;
+  a.epad = c->epad;
+  return a;
+}
+
+int check_batch(const ugo_fec* c, const void* shards, size_t groups, size_t S, size_t pitch) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;  // checkShards: all shards empty
+  if (pitch < S || S > 0xffffffffu || pitch > 0xffffffffu) return UGO_FEC_ERR_INVALID_ARG;
+  if (groups && !shards) return UGO_FEC_ERR_INVALID_ARG;
+  return UGO_FEC_OK;
+}
+
+int encode_dev(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch, hipStream_t s) {
+  if (c->p == 0 || groups == 0) return UGO_FEC_OK;
+  const bool fast = fast_layout(c, shards, pitch);
+  ugo::kern::Batch a = base_batch(c, shards, S, pitch);
+  a.desc = c->d_encdesc;
+  a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
+  const size_t per = std::max<size_t>(1, kMaxItems / a.chunks);
+  for (size_t g0 = 0; g0 < groups; g0 += per) {
+    const size_t gn = std::min(per, groups - g0);
+    a.g0 = g0;
+    a.items = static_cast<uint32_t>(gn * a.chunks);
+    hipError_t e;
+    if (fast && ugo::kern::has_const_encode(c->d, c->p))
+      e = ugo::kern::launch_encode_const(c->d, c->p, a, s);
+    else if (fast)
+      e = ugo::kern::launch_apply(0, ugo::kern::apply_dmax(c->d), a, s);
+    else
+      e = ugo::kern::launch_apply_bytes(0, a, s);
+    if (e != hipSuccess) return UGO_FEC_ERR_HIP;
+  }
+  return UGO_FEC_OK;
+}
+
+int ensure_work(ugo_fec* c, size_t groups) {
+  if (c->work_groups >= groups) return UGO_FEC_OK;
+  (void)hipFree(c->d_work);
+  c->d_work = nullptr;
+  c->work_groups = 0;
+  if (hipMalloc(&c->d_work, groups * c->desc_stride + 64) != hipSuccess) return UGO_FEC_ERR_HIP;
+  c->work_groups = groups;
+  return UGO_FEC_OK;
+}
+
+int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
+                    size_t pitch, unsigned flags, int8_t* status, hipStream_t s) {
+  if (groups == 0) return UGO_FEC_OK;
+  if (!present) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->n > 64) return UGO_FEC_ERR_INVALID_ARG;  // 64-bit presence masks
+  const bool fast = fast_layout(c, shards, pitch);
+  const int mode = c->d_table ? 1 : 2;
+  ugo::kern::Batch a = base_batch(c, shards, S, pitch);
+  a.present = present;
+  a.status = status;
+  a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
+  a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
+  size_t per = std::max<size_t>(1, kMaxItems / a.chunks);
+  if (mode == 2) {
+    // per-group descriptors, bounded workspace (<= 64 Ki groups per slice)
+    per = std::min<size_t>(per, 65536);
+    const int st = ensure_work(c, std::min(per, groups));
+    if (st) return st;
+  }
+  for (size_t g0 = 0; g0 < groups; g0 += per) {
+    const size_t gn = std::min(per, groups - g0);
+    a.g0 = g0;
+    a.items = static_cast<uint32_t>(gn * a.chunks);
+    if (mode == 1) {
+      a.desc = c->d_table;
+    } else {
+      ugo::kern::Prep pr{};
+      pr.desc = c->d_work;
+      pr.present = present;
+      pr.M = c->d_M;
+      pr.gf_exp = c->d_gf;
+      pr.gf_log = c->d_gf + 512;
+      pr.g0 = g0;
+      pr.g_desc0 = g0;
+      pr.nmask = a.nmask;
+      pr.desc_stride = c->desc_stride;
+      pr.d = static_cast<uint32_t>(c->d);
+      pr.n = static_cast<uint32_t>(c->n);
+      pr.dpad = c->dpad;
+      pr.epad = c->epad;
+      if (ugo::kern::launch_prepare(pr, static_cast<uint32_t>(gn), s) != hipSuccess) return UGO_FEC_ERR_HIP;
+      a.desc = c->d_work;
+      a.g_desc0 = g0;
+    }
+    hipError_t e = fast ? ugo::kern::launch_apply(mode, ugo::kern::apply_dmax(c->d), a, s)
+                        : ugo::kern::launch_apply_bytes(mode, a, s);
+    if (e != hipSuccess) return UGO_FEC_ERR_HIP;
+  }
+  return UGO_FEC_OK;
+}
+
+int ensure_stage(ugo_fec* c, size_t pitch) {
+  const size_t gbytes = size_t(c->n) * pitch;
+  const size_t want = std::max<size_t>(1, kStageBytes / gbytes);
+  if (c->stage_groups >= want && c->stage_pitch == pitch && c->streams[0]) return UGO_FEC_OK;
+  for (int i = 0; i < kStreams; ++i) {
+    (void)hipFree(c->d_stage[i]);
+    (void)hipFree(c->d_mask[i]);
+    (void)hipFree(c->d_status[i]);
+    c->d_stage[i] = nullptr;
+    c->d_mask[i] = nullptr;
+    c->d_status[i] = nullptr;
+  }
+  c->stage_groups = 0;
+  for (int i = 0; i < kStreams; ++i) {
+    if (!c->streams[i] && hipStreamCreateWithFlags(&c->streams[i], hipStreamNonBlocking) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
+    if (hipMalloc(&c->d_stage[i], want * gbytes + 16) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (hipMalloc(&c->d_mask[i], want * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (hipMalloc(&c->d_status[i], want) != hipSuccess) return UGO_FEC_ERR_HIP;
+  }
+  c->stage_groups = want;
+  c->stage_pitch = pitch;
+  return UGO_FEC_OK;
+}
+
+// Host path: chunks of stage_groups groups round-robin over kStreams streams:
+// H2D(chunk) -> kernel -> D2H(chunk) on one stream, chunks on different
+// streams overlap (copy engines in both directions + compute).
+int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
+              size_t pitch, bool recon, unsigned flags, int8_t* status) {
+  int st = ensure_stage(c, pitch);
+  if (st) return st;
+  const size_t gbytes = size_t(c->n) * pitch;
+  const size_t per = c->stage_groups;
+  std::vector<int8_t> tmp_status;
+  if (recon && !status) {
+    tmp_status.resize(groups);
+    status = tmp_status.data();
+  }
+  size_t chunk = 0;
+  for (size_t g0 = 0; g0 < groups; g0 += per, ++chunk) {
+    const int si = static_cast<int>(chunk % kStreams);
+    hipStream_t s = c->streams[si];
+    const size_t gn = std::min(per, groups - g0);
+    uint8_t* host = shards + g0 * gbytes;
+    uint8_t* dev = c->d_stage[si];
+    hipError_t e;
+    if (!recon) {
+      // data rows in, parity rows out
+      e = hipMemcpy2DAsync(dev, gbytes, host, gbytes, size_t(c->d) * pitch, gn, hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) return UGO_FEC_ERR_HIP;
+      st = encode_dev(c, dev, gn, S, pitch, s);
+      if (st) return st;
+      e = hipMemcpy2DAsync(host + size_t(c->d) * pitch, gbytes, dev + size_t(c->d) * pitch, gbytes,
+                           size_t(c->p) * pitch, gn, hipMemcpyDeviceToHost, s);
+      if (e != hipSuccess) return UGO_FEC_ERR_HIP;
+    } else {
+      e = hipMemcpyAsync(dev, host, gn * gbytes, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(c->d_mask[si], present + g0, gn * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) return UGO_FEC_ERR_HIP;
+      st = reconstruct_dev(c, dev, c->d_mask[si], gn, S, pitch, flags, c->d_status[si], s);
+      if (st) return st;
+      e = hipMemcpyAsync(host, dev, gn * gbytes, hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(status + g0, c->d_status[si], gn, hipMemcpyDeviceToHost, s);
+      if (e != hipSuccess) return UGO_FEC_ERR_HIP;
+    }
+  }
+  for (int i = 0; i < kStreams; ++i)
+    if (hipStreamSynchronize(c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
+  if (recon)
+    for (size_t g = 0; g < groups; ++g)
+      if (status[g]) return status[g];
+  return UGO_FEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ugo_fec_abi_version(void) { return UGO_FEC_ABI_VERSION; }
+
+const char* ugo_fec_strerror(int s) {
+  switch (s) {
+    case UGO_FEC_OK: return "ok";
+    case UGO_FEC_ERR_INV_SHARD_NUM:
+      return "cannot create Encoder with less than one data shard or less than zero parity shards";
+    case UGO_FEC_ERR_MAX_SHARD_NUM: return "cannot create Encoder with more than 256 data+parity shards";
+    case UGO_FEC_ERR_TOO_FEW_SHARDS: return "too few shards given";
+    case UGO_FEC_ERR_SHARD_NO_DATA: return "no shard data";
+    case UGO_FEC_ERR_SHARD_SIZE: return "shard sizes do not match";
+    case UGO_FEC_ERR_INVALID_ARG: return "invalid argument";
+    case UGO_FEC_ERR_SINGULAR: return "matrix is singular";
+    case UGO_FEC_ERR_HIP: return "HIP runtime error";
+    case UGO_FEC_ERR_NO_DEVICE: return "no usable gfx950 device";
+    default: return "unknown status";
+  }
+}
+
+int ugo_fec_check_shards(int n, const size_t* lens, int nil_ok, size_t* shard_size) {
+  if (n <= 0 || !lens) return UGO_FEC_ERR_INVALID_ARG;
+  size_t size = 0;
+  for (int i = 0; i < n; ++i)
+    if (lens[i]) {
+      size = lens[i];
+      break;
+    }
+  if (shard_size) *shard_size = size;
+  if (size == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
+  for (int i = 0; i < n; ++i)
+    if (lens[i] != size && (lens[i] != 0 || !nil_ok)) return UGO_FEC_ERR_SHARD_SIZE;
+  return UGO_FEC_OK;
+}
+
+int ugo_fec_create(int device, int data_shards, int parity_shards, ugo_fec** out) {
+  if (!out) return UGO_FEC_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (data_shards <= 0 || parity_shards < 0) return UGO_FEC_ERR_INV_SHARD_NUM;
+  if (data_shards + parity_shards > 256) return UGO_FEC_ERR_MAX_SHARD_NUM;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return UGO_FEC_ERR_NO_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return UGO_FEC_ERR_NO_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return UGO_FEC_ERR_NO_DEVICE;
+  DeviceGuard guard(device);
+  if (!guard.ok) return UGO_FEC_ERR_NO_DEVICE;
+
+  ugo_fec* c = new (std::nothrow) ugo_fec();
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  c->device = device;
+  c->d = data_shards;
+  c->p = parity_shards;
+  c->n = data_shards + parity_shards;
+  if (const char* env = std::getenv("UGO_FEC_TABLE_MAX_SHARDS")) c->table_max = std::atoi(env);
+  const int d = c->d, p = c->p, n = c->n;
+  c->M.resize(size_t(n) * d);
+  std::vector<uint8_t> scratch(size_t(n) * d + 3 * size_t(d) * d);
+  if (!ugo::gf::build_matrix(d, p, c->M.data(), scratch.data())) {
+    delete c;
+    return UGO_FEC_ERR_SINGULAR;
+  }
+  const int dmax = ugo::kern::apply_dmax(d);
+  c->dpad = static_cast<uint32_t>(round_up(std::max(d, dmax), 4));
+  c->epad = static_cast<uint32_t>(round_up(std::max(p, 1), 4));
+  c->desc_stride = static_cast<uint32_t>(round_up(4 + c->dpad + c->epad + size_t(p) * c->dpad, 16));
+
+  int st = UGO_FEC_OK;
+  auto fail = [&](int code) {
+    free_ctx(c);
+    return code;
+  };
+  if (hipMalloc(&c->d_M, c->M.size()) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
+  if (hipMemcpy(c->d_M, c->M.data(), c->M.size(), hipMemcpyHostToDevice) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
+  {
+    std::vector<uint8_t> gf(768);
+    std::memcpy(gf.data(), ugo::gf::kTables.exp, 512);
+    std::memcpy(gf.data() + 512, ugo::gf::kTables.log, 256);
+    if (hipMalloc(&c->d_gf, gf.size()) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
+    if (hipMemcpy(c->d_gf, gf.data(), gf.size(), hipMemcpyHostToDevice) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
+  }
+  {
+    // MODE 0 encode descriptor: inputs = data rows, outputs = parity rows
+    std::vector<uint8_t> ed(c->desc_stride + 64, 0);
+    ed[0] = static_cast<uint8_t>(p);
+    ed[1] = 0;
+    for (int i = 0; i < d; ++i) ed[4 + i] = static_cast<uint8_t>(i);
+    for (int i = 0; i < p; ++i) ed[4 + c->dpad + i] = static_cast<uint8_t>(d + i);
+    for (int i = 0; i < p; ++i)
+      for (int k = 0; k < d; ++k) ed[4 + c->dpad + c->epad + size_t(i) * c->dpad + k] = c->M[size_t(d + i) * d + k];
+    if (hipMalloc(&c->d_encdesc, ed.size()) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
+    if (hipMemcpy(c->d_encdesc, ed.data(), ed.size(), hipMemcpyHostToDevice) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
+  }
+  if (n <= c->table_max && n <= 20) {
+    const size_t entries = size_t(1) << n;
+    std::vector<uint8_t> tab(entries * c->desc_stride + 64, 0);
+    for (size_t m = 0; m < entries; ++m) {
+      st = build_desc(c, m, &tab[m * c->desc_stride]);
+      if (st) return fail(st);
+    }
+    if (hipMalloc(&c->d_table, tab.size()) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
+    if (hipMemcpy(c->d_table, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
+  }
+  *out = c;
+  return UGO_FEC_OK;
+}
+
+void ugo_fec_destroy(ugo_fec* c) { free_ctx(c); }
+
+int ugo_fec_geometry(const ugo_fec* c, int* d, int* p, int* device) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (d) *d = c->d;
+  if (p) *p = c->p;
+  if (device) *device = c->device;
+  return UGO_FEC_OK;
+}
+
+int ugo_fec_matrix(const ugo_fec* c, uint8_t* out) {
+  if (!c || !out) return UGO_FEC_ERR_INVALID_ARG;
+  std::memcpy(out, c->M.data(), c->M.size());
+  return UGO_FEC_OK;
+}
+
+int ugo_fec_encode(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch, void* stream) {
+  int st = check_batch(c, shards, groups, S, pitch);
+  if (st) return st;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  return encode_dev(c, shards, groups, S, pitch, static_cast<hipStream_t>(stream));
+}
+
+int ugo_fec_reconstruct(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
+                        size_t pitch, unsigned flags, int8_t* status, void* stream) {
+  int st = check_batch(c, shards, groups, S, pitch);
+  if (st) return st;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  return reconstruct_dev(c, shards, present, groups, S, pitch, flags, status, static_cast<hipStream_t>(stream));
+}
+
+int ugo_fec_encode_host(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch) {
+  int st = check_batch(c, shards, groups, S, pitch);
+  if (st || groups == 0 || c->p == 0) return st;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  return host_path(c, shards, nullptr, groups, S, pitch, false, 0, nullptr);
+}
+
+int ugo_fec_reconstruct_host(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
+                             size_t pitch, unsigned flags, int8_t* status) {
+  int st = check_batch(c, shards, groups, S, pitch);
+  if (st || groups == 0) return st;
+  if (!present) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->n > 64) return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  return host_path(c, shards, present, groups, S, pitch, true, flags, status);
+}
+
+int ugo_fec_host_alloc(size_t bytes, void** out) {
+  if (!out) return UGO_FEC_ERR_INVALID_ARG;
+  *out = nullptr;
+  return hip_status(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+}
+
+int ugo_fec_host_free(void* p) { return hip_status(hipHostFree(p)); }
+
+}  // extern "C"

@@ -1,0 +1,287 @@
+"""Python host mirror of the reedsolomon.Encoder subset used by jflyup/ugo.
+
+ugo/fec.go drives klauspost/reedsolomon through three calls:
+  reedsolomon.New(dataShards, parityShards)   ugo/fec.go:59
+  enc.Reconstruct(shards)                     ugo/fec.go:202
+  enc.Encode(shards)                          ugo/fec.go:238
+This module exposes the same names and argument meaning over the C-ABI in
+include/ugo_fec.h (libugofec.so, gfx950 kernels):
+
+* ``New(d, p, device=0)`` -> ``Encoder`` (raises ``ErrInvShardNum`` /
+  ``ErrMaxShardNum`` like upstream ``New``).
+* ``Encoder.Encode(shards)`` / ``Encoder.Reconstruct(shards)`` /
+  ``Encoder.ReconstructData(shards)``: Go-shaped, one group per call, shards
+  are a list of ``bytearray`` (``None`` or empty = missing), same error
+  behaviour (``ErrTooFewShards``, ``ErrShardNoData``, ``ErrShardSize``).
+* ``Encoder.encode_batch`` / ``reconstruct_batch``: the device-resident batch
+  form (torch uint8 tensors on the GPU, shape [groups, d+p, pitch]).
+* ``Encoder.encode_host`` / ``reconstruct_host``: host numpy batches, staged
+  through the engine's pipelined H2D -> kernel -> D2H path.
+
+There is no CPU fallback: if libugofec.so is missing the import fails, and
+every compute call needs a gfx950 device.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+try:  # load torch first so libugofec.so binds torch's libamdhip64.so.7 (same soname)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the host-only paths
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libugofec.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ugo_fec.h")
+
+OK = 0
+RECONSTRUCT_DATA_ONLY = 1
+
+
+class FecError(Exception):
+    code = -1
+
+
+class ErrInvShardNum(FecError):
+    code = 1
+
+
+class ErrMaxShardNum(FecError):
+    code = 2
+
+
+class ErrTooFewShards(FecError):
+    code = 3
+
+
+class ErrShardNoData(FecError):
+    code = 4
+
+
+class ErrShardSize(FecError):
+    code = 5
+
+
+class ErrInvalidArg(FecError):
+    code = 6
+
+
+class ErrSingular(FecError):
+    code = 7
+
+
+class ErrHip(FecError):
+    code = 8
+
+
+class ErrNoDevice(FecError):
+    code = 9
+
+
+_ERRORS = {c.code: c for c in (ErrInvShardNum, ErrMaxShardNum, ErrTooFewShards, ErrShardNoData,
+                                ErrShardSize, ErrInvalidArg, ErrSingular, ErrHip, ErrNoDevice)}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libugofec.so.  Raises loudly if it was not built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built: run `make -C ugo_amd/csrc` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    sz, vp, i, u = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint
+    lib.ugo_fec_create.argtypes = [i, i, i, ctypes.POINTER(vp)]
+    lib.ugo_fec_destroy.argtypes = [vp]
+    lib.ugo_fec_destroy.restype = None
+    lib.ugo_fec_geometry.argtypes = [vp, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i)]
+    lib.ugo_fec_matrix.argtypes = [vp, vp]
+    lib.ugo_fec_encode.argtypes = [vp, vp, sz, sz, sz, vp]
+    lib.ugo_fec_reconstruct.argtypes = [vp, vp, vp, sz, sz, sz, u, vp, vp]
+    lib.ugo_fec_encode_host.argtypes = [vp, vp, sz, sz, sz]
+    lib.ugo_fec_reconstruct_host.argtypes = [vp, vp, vp, sz, sz, sz, u, vp]
+    lib.ugo_fec_check_shards.argtypes = [i, vp, i, ctypes.POINTER(sz)]
+    lib.ugo_fec_host_alloc.argtypes = [sz, ctypes.POINTER(vp)]
+    lib.ugo_fec_host_free.argtypes = [vp]
+    lib.ugo_fec_strerror.argtypes = [i]
+    lib.ugo_fec_strerror.restype = ctypes.c_char_p
+    lib.ugo_fec_abi_version.argtypes = []
+    _lib = lib
+    return lib
+
+
+def header_symbols(path: str = HEADER_PATH) -> List[str]:
+    """Every entry point declared in include/ugo_fec.h."""
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ugo_fec_[a-z0-9_]+)\s*\(", src)))
+
+
+def strerror(code: int) -> str:
+    return load_library().ugo_fec_strerror(code).decode()
+
+
+def _raise(code: int):
+    if code != OK:
+        raise _ERRORS.get(code, FecError)(f"{strerror(code)} (status {code})")
+
+
+def check_shards(lens: Sequence[int], nil_ok: bool) -> int:
+    """klauspost checkShards over shard lengths; returns the shard size."""
+    lib = load_library()
+    arr = (ctypes.c_size_t * len(lens))(*lens)
+    out = ctypes.c_size_t(0)
+    _raise(lib.ugo_fec_check_shards(len(lens), ctypes.cast(arr, ctypes.c_void_p), int(nil_ok),
+                                    ctypes.byref(out)))
+    return out.value
+
+
+def _stream_handle(stream) -> Optional[int]:
+    if stream is None and torch is not None and torch.cuda.is_available():
+        stream = torch.cuda.current_stream()
+    if stream is None:
+        return None
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+class Encoder:
+    """A (d, p) code bound to one GPU (reedsolomon.Encoder equivalent)."""
+
+    def __init__(self, data_shards: int, parity_shards: int, device: int = 0):
+        lib = load_library()
+        h = ctypes.c_void_p()
+        _raise(lib.ugo_fec_create(device, data_shards, parity_shards, ctypes.byref(h)))
+        self._h = h
+        self.DataShards = data_shards
+        self.ParityShards = parity_shards
+        self.Shards = data_shards + parity_shards
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().ugo_fec_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def matrix(self) -> np.ndarray:
+        out = np.zeros((self.Shards, self.DataShards), np.uint8)
+        _raise(load_library().ugo_fec_matrix(self._h, out.ctypes.data))
+        return out
+
+    # -------------------------------------------------- device-resident batch
+    def encode_batch(self, shards, shard_size: Optional[int] = None, stream=None):
+        """shards: torch.uint8 CUDA tensor [G, d+p, pitch] (row-contiguous)."""
+        G, n, pitch = shards.shape
+        assert n == self.Shards and shards.stride(2) == 1 and shards.stride(1) == pitch \
+            and shards.stride(0) == n * pitch, "shards must be a contiguous [G, d+p, pitch] tensor"
+        S = pitch if shard_size is None else shard_size
+        _raise(load_library().ugo_fec_encode(self._h, shards.data_ptr(), G, S, pitch, _stream_handle(stream)))
+
+    def reconstruct_batch(self, shards, present, shard_size: Optional[int] = None, data_only=False,
+                          status=None, stream=None):
+        """present: torch.int64/uint64 CUDA tensor [G] of presence bitmasks;
+        status: optional torch.int8 CUDA tensor [G]."""
+        G, n, pitch = shards.shape
+        assert n == self.Shards and shards.is_contiguous()
+        assert present.is_contiguous() and present.numel() == G and present.element_size() == 8
+        S = pitch if shard_size is None else shard_size
+        st = 0 if status is None else status.data_ptr()
+        _raise(load_library().ugo_fec_reconstruct(self._h, shards.data_ptr(), present.data_ptr(), G, S, pitch,
+                                                  RECONSTRUCT_DATA_ONLY if data_only else 0, st or None,
+                                                  _stream_handle(stream)))
+
+    # ------------------------------------------------------ host-buffer batch
+    def encode_host(self, shards: np.ndarray, shard_size: Optional[int] = None):
+        assert shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"] and shards.ndim == 3
+        G, n, pitch = shards.shape
+        assert n == self.Shards
+        S = pitch if shard_size is None else shard_size
+        _raise(load_library().ugo_fec_encode_host(self._h, shards.ctypes.data, G, S, pitch))
+
+    def reconstruct_host(self, shards: np.ndarray, present: np.ndarray, shard_size: Optional[int] = None,
+                         data_only=False, status: Optional[np.ndarray] = None) -> int:
+        """Returns the aggregate status (0 or the first failing group's code);
+        per-group codes go to `status` when given.  Does not raise for
+        ErrTooFewShards groups (they are reported and left untouched)."""
+        assert shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"] and shards.ndim == 3
+        G, n, pitch = shards.shape
+        assert n == self.Shards
+        present = np.ascontiguousarray(present, dtype=np.uint64)
+        S = pitch if shard_size is None else shard_size
+        st = None if status is None else status.ctypes.data
+        if status is not None:
+            assert status.dtype == np.int8 and status.size == G
+        rc = load_library().ugo_fec_reconstruct_host(self._h, shards.ctypes.data, present.ctypes.data, G, S, pitch,
+                                                     RECONSTRUCT_DATA_ONLY if data_only else 0, st)
+        if rc not in (OK, ErrTooFewShards.code, ErrSingular.code):
+            _raise(rc)
+        return rc
+
+    # ------------------------------------------- Go-shaped, one group per call
+    def Encode(self, shards: List[bytearray]) -> None:
+        """reedsolomon Encode: parity shards written in place (ugo/fec.go:238)."""
+        if len(shards) != self.Shards:
+            raise ErrTooFewShards(strerror(ErrTooFewShards.code))
+        S = check_shards([len(s) for s in shards], nil_ok=False)
+        buf = np.zeros((1, self.Shards, S), np.uint8)
+        for k in range(self.DataShards):
+            buf[0, k] = np.frombuffer(bytes(shards[k]), np.uint8)
+        self.encode_host(buf, S)
+        for k in range(self.DataShards, self.Shards):
+            shards[k][:] = buf[0, k].tobytes()
+
+    def _reconstruct(self, shards: list, data_only: bool) -> None:
+        if len(shards) != self.Shards:
+            raise ErrTooFewShards(strerror(ErrTooFewShards.code))
+        lens = [0 if s is None else len(s) for s in shards]
+        S = check_shards(lens, nil_ok=True)
+        mask = 0
+        buf = np.zeros((1, self.Shards, S), np.uint8)
+        for r, s in enumerate(shards):
+            if lens[r]:
+                mask |= 1 << r
+                buf[0, r] = np.frombuffer(bytes(s), np.uint8)
+        status = np.zeros(1, np.int8)
+        rc = self.reconstruct_host(buf, np.array([mask], np.uint64), S, data_only, status)
+        _raise(rc)
+        limit = self.DataShards if data_only else self.Shards
+        for r in range(limit):
+            if not lens[r]:
+                shards[r] = bytearray(buf[0, r].tobytes())
+
+    def Reconstruct(self, shards: list) -> None:
+        """reedsolomon Reconstruct (ugo/fec.go:202): fills every missing shard."""
+        self._reconstruct(shards, data_only=False)
+
+    def ReconstructData(self, shards: list) -> None:
+        self._reconstruct(shards, data_only=True)
+
+
+def New(data_shards: int, parity_shards: int, device: int = 0) -> Encoder:
+    """reedsolomon.New as called at ugo/fec.go:59."""
+    return Encoder(data_shards, parity_shards, device)
+
+
+def host_alloc(nbytes: int) -> np.ndarray:
+    """Pinned host buffer (uint8 numpy view); free with host_free(arr)."""
+    lib = load_library()
+    p = ctypes.c_void_p()
+    _raise(lib.ugo_fec_host_alloc(nbytes, ctypes.byref(p)))
+    arr = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(nbytes,))
+    return arr
+
+
+def host_free(arr: np.ndarray) -> None:
+    _raise(load_library().ugo_fec_host_free(ctypes.c_void_p(arr.ctypes.data)))
