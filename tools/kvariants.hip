@@ -1,0 +1,158 @@
+// kvariants.hip -- interleaved A/B timing of kernel variants (one process,
+// N rounds x M variants, median reported: cdna_hip_programming.md §5.4 rule 24).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/kvariants tools/kvariants.hip
+// Not product code: it includes the kernel TU to instantiate variants.
+#include "../ugo_amd/csrc/fec_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+using namespace ugo;
+using namespace ugo::kern;
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));   \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+static void build_table(int d, int p, uint32_t dpad, uint32_t epad, uint32_t stride, std::vector<uint8_t>& tab) {
+  const int n = d + p;
+  std::vector<uint8_t> M(n * d), scratch(n * d + 3 * d * d);
+  gf::build_matrix(d, p, M.data(), scratch.data());
+  tab.assign((size_t(1) << n) * stride + 64, 0);
+  for (uint64_t m = 0; m < (1ull << n); ++m) {
+    uint8_t* out = &tab[m * stride];
+    int np = __builtin_popcountll(m);
+    if (np == n) continue;
+    if (np < d) { out[2] = 3; continue; }
+    std::vector<int> surv, outr;
+    for (int r = 0; r < n; ++r) {
+      if ((m >> r) & 1) { if ((int)surv.size() < d) surv.push_back(r); } else outr.push_back(r);
+    }
+    std::vector<uint8_t> sub(d * d), inv(d * d), work(2 * d * d);
+    for (int i = 0; i < d; ++i) memcpy(&sub[i * d], &M[surv[i] * d], d);
+    gf::invert(d, sub.data(), inv.data(), work.data());
+    int ed = 0;
+    for (int r : outr) ed += r < d;
+    out[0] = outr.size(); out[1] = ed;
+    for (int i = 0; i < d; ++i) out[4 + i] = surv[i];
+    for (size_t i = 0; i < outr.size(); ++i) out[4 + dpad + i] = outr[i];
+    uint8_t* coef = out + 4 + dpad + epad;
+    for (size_t i = 0; i < outr.size(); ++i)
+      for (int k = 0; k < d; ++k) {
+        int r = outr[i];
+        uint8_t v = 0;
+        if (r < d) v = inv[r * d + k];
+        else for (int j = 0; j < d; ++j) v ^= gf::mul(M[r * d + j], inv[j * d + k]);
+        coef[i * dpad + k] = v;
+      }
+  }
+}
+
+int main(int argc, char** argv) {
+  const int d = 10, p = 3, n = 13;
+  const uint32_t S = 1350, pitch = 1360;
+  const uint64_t G = argc > 1 ? atoll(argv[1]) : 65536;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 15;
+  uint8_t* buf;
+  uint64_t* masks;
+  CK(hipMalloc(&buf, G * n * pitch));
+  CK(hipMalloc(&masks, G * 8));
+  std::vector<uint8_t> h(G * n * pitch);
+  uint64_t st = 0x5EED;
+  for (auto& b : h) { st = st * 6364136223846793005ull + 1442695040888963407ull; b = st >> 56; }
+  CK(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
+  std::vector<uint64_t> hm(G);
+  for (uint64_t g = 0; g < G; ++g) {
+    st = st * 6364136223846793005ull + 1442695040888963407ull;
+    int a = (st >> 33) % n, b = (a + 1 + (st >> 40) % (n - 1)) % n;
+    hm[g] = ((1ull << n) - 1) & ~(1ull << a) & ~(1ull << b);
+  }
+  CK(hipMemcpy(masks, hm.data(), G * 8, hipMemcpyHostToDevice));
+  const uint32_t dpad = 12, epad = 4, stride = 64;
+  std::vector<uint8_t> tab;
+  build_table(d, p, dpad, epad, stride, tab);
+  uint8_t* dtab;
+  CK(hipMalloc(&dtab, tab.size()));
+  CK(hipMemcpy(dtab, tab.data(), tab.size(), hipMemcpyHostToDevice));
+
+  Batch a{};
+  a.base = buf; a.group_bytes = n * pitch; a.nmask = (1ull << n) - 1; a.pitch = pitch; a.S = S;
+  a.chunks = 85; a.items = G * 85; a.desc = dtab; a.present = masks; a.desc_stride = stride; a.d = d;
+  a.dpad = dpad; a.epad = epad;
+  const double enc_bytes = double(G) * n * S, dec_bytes = double(G) * 12 * S;
+
+  struct Var { std::string name; double bytes; std::function<void()> go; std::vector<float> t; };
+  std::vector<Var> vars;
+  auto enc = [&](auto kern, int cpt, const char* nm) {
+    vars.push_back({nm, enc_bytes, [=]() {
+      Batch b = a; b.pass = (b.items + cpt - 1) / cpt;
+      hipLaunchKernelGGL(kern, dim3((b.pass + 255) / 256), dim3(256), 0, 0, b);
+    }, {}});
+  };
+  enc(k_encode_c<10, 3, 1, 0>, 1, "enc cpt1 nt0");
+  enc(k_encode_c<10, 3, 1, 1>, 1, "enc cpt1 nt1");
+  enc(k_encode_c<10, 3, 1, 2>, 1, "enc cpt1 nt2");
+  enc(k_encode_c<10, 3, 1, 3>, 1, "enc cpt1 nt3");
+  enc(k_encode_c<10, 3, 2, 0>, 2, "enc cpt2 nt0");
+  enc(k_encode_c<10, 3, 2, 3>, 2, "enc cpt2 nt3");
+  enc(k_encode_c<10, 3, 4, 0>, 4, "enc cpt4 nt0");
+  auto dec = [&](auto kern, const char* nm) {
+    vars.push_back({nm, dec_bytes, [=]() {
+      Batch b = a; b.pass = b.items;
+      hipLaunchKernelGGL(kern, dim3((b.items + 255) / 256), dim3(256), 0, 0, b);
+    }, {}});
+  };
+  {
+    // planar layout [13][G][pitch]: group stride = pitch, row stride = G * pitch
+    Batch pl = a;
+    pl.group_bytes = pitch;
+    pl.pitch = G * pitch;
+    vars.push_back({"enc planar cpt1 nt0", enc_bytes, [=]() {
+      Batch b = pl; b.pass = b.items;
+      hipLaunchKernelGGL((k_encode_c<10, 3, 1, 0>), dim3((b.pass + 255) / 256), dim3(256), 0, 0, b);
+    }, {}});
+    vars.push_back({"enc planar cpt1 nt3", enc_bytes, [=]() {
+      Batch b = pl; b.pass = b.items;
+      hipLaunchKernelGGL((k_encode_c<10, 3, 1, 3>), dim3((b.pass + 255) / 256), dim3(256), 0, 0, b);
+    }, {}});
+    vars.push_back({"dec planar mode1 nt0", dec_bytes, [=]() {
+      Batch b = pl; b.pass = b.items;
+      hipLaunchKernelGGL((k_apply<10, 1, 0>), dim3((b.items + 255) / 256), dim3(256), 0, 0, b);
+    }, {}});
+  }
+  dec(k_apply<10, 1, 0>, "dec mode1 nt0");
+  dec(k_apply<10, 1, 1>, "dec mode1 nt1");
+  dec(k_apply<10, 1, 3>, "dec mode1 nt3");
+
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (auto& v : vars) { v.go(); }
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < rounds; ++r)
+    for (auto& v : vars) {
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < 5; ++i) v.go();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.t.push_back(ms / 5);
+    }
+  for (auto& v : vars) {
+    std::sort(v.t.begin(), v.t.end());
+    float med = v.t[v.t.size() / 2], mn = v.t[0];
+    printf("{\"variant\":\"%s\",\"median_us\":%.2f,\"min_us\":%.2f,\"GBps\":%.1f}\n", v.name.c_str(), med * 1e3,
+           mn * 1e3, v.bytes / (med * 1e-3) / 1e9);
+  }
+  return 0;
+}

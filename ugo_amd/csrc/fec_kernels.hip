@@ -79,20 +79,32 @@ __device__ __forceinline__ void xor4_2(V4& y, const V4& a, const V4& b) {
   for (int j = 0; j < 4; ++j) y.v[j] = xor3(y.v[j], a.v[j], b.v[j]);
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// NT policy bits: 1 = nontemporal loads, 2 = nontemporal stores (streaming
+// data touched once; keeps it from displacing L2 / Infinity-Cache lines)
+template <int NT>
 __device__ __forceinline__ V4 load16(const uint8_t* p) {
-  const uint4 q = *reinterpret_cast<const uint4*>(p);
-  V4 r;
-  r.v[0] = q.x;
-  r.v[1] = q.y;
-  r.v[2] = q.z;
-  r.v[3] = q.w;
-  return r;
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  u32x4 v;
+  if constexpr (NT & 1) {
+    v = __builtin_nontemporal_load(q);
+  } else {
+    v = *q;
+  }
+  return V4{{v.x, v.y, v.z, v.w}};
 }
 
 // store the first nb (1..16) bytes of a chunk
+template <int NT>
 __device__ __forceinline__ void store16(uint8_t* p, const V4& y, uint32_t nb) {
   if (nb >= 16) {
-    *reinterpret_cast<uint4*>(p) = make_uint4(y.v[0], y.v[1], y.v[2], y.v[3]);
+    const u32x4 v = {y.v[0], y.v[1], y.v[2], y.v[3]};
+    if constexpr (NT & 2) {
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    } else {
+      *reinterpret_cast<u32x4*>(p) = v;
+    }
     return;
   }
   // tail chunk of a row whose length is not a multiple of 16: rare lanes
@@ -180,24 +192,37 @@ __device__ __forceinline__ V4 cparity(const V4* x) {
 }
 
 // compute and store parity rows one at a time (short live ranges)
-template <int D, int P, int... I>
+template <int D, int P, int NT, int... I>
 __device__ __forceinline__ void cparity_store(uint8_t* gp, uint64_t pitch, uint32_t nb, const V4* x,
                                               std::integer_sequence<int, I...>) {
-  ((store16(gp + static_cast<uint64_t>(D + I) * pitch, cparity<D, P, I>(x), nb)), ...);
+  ((store16<NT>(gp + static_cast<uint64_t>(D + I) * pitch, cparity<D, P, I>(x), nb)), ...);
 }
 
-template <int D, int P>
+// CPT column chunks per thread, `a.pass` items apart (so each pass is still a
+// coalesced 1 KiB-per-row wave access); all CPT*D loads are issued before any
+// arithmetic for more bytes in flight per wave.
+template <int D, int P, int CPT, int NT>
 __global__ __launch_bounds__(256) void k_encode_c(Batch a) {
-  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
-  if (item >= a.items) return;
-  const uint32_t gl = item / a.chunks;
-  const uint32_t c = item - gl * a.chunks;
-  uint8_t* gp = a.base + (a.g0 + gl) * a.group_bytes + static_cast<uint64_t>(c) * 16u;
-  V4 x[D];
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  V4 x[CPT][D];
+  uint8_t* gp[CPT];
+  uint32_t nb[CPT];
 #pragma unroll
-  for (int k = 0; k < D; ++k) x[k] = load16(gp + static_cast<uint64_t>(k) * a.pitch);
-  const uint32_t nb = a.S - c * 16u;
-  cparity_store<D, P>(gp, a.pitch, nb, x, std::make_integer_sequence<int, P>{});
+  for (int j = 0; j < CPT; ++j) {
+    const uint32_t item = t + j * a.pass;
+    gp[j] = nullptr;
+    if (item < a.items) {
+      const uint32_t gl = item / a.chunks;
+      const uint32_t c = item - gl * a.chunks;
+      gp[j] = a.base + (a.g0 + gl) * a.group_bytes + static_cast<uint64_t>(c) * 16u;
+      nb[j] = a.S - c * 16u;
+#pragma unroll
+      for (int k = 0; k < D; ++k) x[j][k] = load16<NT>(gp[j] + static_cast<uint64_t>(k) * a.pitch);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPT; ++j)
+    if (gp[j]) cparity_store<D, P, NT>(gp[j], a.pitch, nb[j], x[j], std::make_integer_sequence<int, P>{});
 }
 
 // ----------------------------------------------- descriptor-driven kernels
@@ -222,7 +247,7 @@ __device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
   return *reinterpret_cast<const uint32_t*>(p);
 }
 
-template <int DMAX, int MODE>
+template <int DMAX, int MODE, int NT = 0>
 __global__ __launch_bounds__(256) void k_apply(Batch a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
   if (item >= a.items) return;
@@ -246,7 +271,7 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
   for (int k = 0; k < DMAX; ++k) {
     if (k < static_cast<int>(a.d)) {
       const uint32_t r = (rows[k >> 2] >> (8 * (k & 3))) & 0xffu;
-      x[k] = load16(gp + static_cast<uint64_t>(r) * a.pitch);
+      x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.pitch);
     } else {
       x[k] = V4{{0u, 0u, 0u, 0u}};
     }
@@ -272,7 +297,7 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
       }
     }
     const uint32_t r = orow[i];
-    store16(gp + static_cast<uint64_t>(r) * a.pitch, y, nb);
+    store16<NT>(gp + static_cast<uint64_t>(r) * a.pitch, y, nb);
   }
 }
 
@@ -453,12 +478,19 @@ int apply_dmax(int d) {
 
 bool has_const_encode(int d, int p) { return (d == 10 && p == 3) || (d == 32 && p == 8); }
 
-hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
-  const dim3 grid(blocks_for(a.items, 256)), block(256);
+// Tuned launch policy for the compile-time encode kernels (tools/kvariants.hip)
+constexpr int kEncCPT = 1;
+constexpr int kEncNT = 0;
+
+hipError_t launch_encode_const(int d, int p, const Batch& a0, hipStream_t s) {
+  Batch a = a0;
+  a.pass = (a.items + kEncCPT - 1) / kEncCPT;
+  const dim3 grid(blocks_for(a.pass, 256)), block(256);
   if (d == 10 && p == 3)
-    hipLaunchKernelGGL((k_encode_c<10, 3>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_encode_c<10, 3, kEncCPT, kEncNT>), grid, block, 0, s, a);
   else if (d == 32 && p == 8)
-    hipLaunchKernelGGL((k_encode_c<32, 8>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_encode_c<32, 8, 1, kEncNT>), dim3(blocks_for(a.items, 256)), block, 0, s,
+                       [&] { Batch b = a0; b.pass = b.items; return b; }());
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -18,10 +18,11 @@ struct Batch {
   uint64_t g_desc0;         // group whose descriptor sits at desc (MODE 2)
   uint64_t group_bytes;     // (d + p) * pitch
   uint64_t nmask;           // (1 << (d+p)) - 1
-  uint32_t pitch;
+  uint64_t pitch;           // row stride in bytes (rows of one group are `pitch` apart)
   uint32_t S;               // shard size in bytes
   uint32_t chunks;          // column chunks per group (16 B, or 4 B for the byte kernel)
   uint32_t items;           // groups_in_launch * chunks
+  uint32_t pass;            // items handled per "pass" of the grid (= items / chunks-per-thread)
   uint32_t desc_stride;
   uint32_t d;
   uint32_t dpad;

@@ -299,8 +299,15 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
       st = encode_dev(c, dev, gn, S, pitch, s);
       if (st) return st;
-      e = hipMemcpy2DAsync(host + size_t(c->d) * pitch, gbytes, dev + size_t(c->d) * pitch, gbytes,
-                           size_t(c->p) * pitch, gn, hipMemcpyDeviceToHost, s);
+      // parity rows out, bytes [0, S) only: padding bytes of the caller's rows are never written
+      hipMemcpy3DParms cp{};
+      cp.srcPtr = make_hipPitchedPtr(dev, pitch, pitch, c->n);
+      cp.srcPos = make_hipPos(0, c->d, 0);
+      cp.dstPtr = make_hipPitchedPtr(host, pitch, pitch, c->n);
+      cp.dstPos = make_hipPos(0, c->d, 0);
+      cp.extent = make_hipExtent(S, c->p, gn);
+      cp.kind = hipMemcpyDeviceToHost;
+      e = hipMemcpy3DAsync(&cp, s);
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
     } else {
       e = hipMemcpyAsync(dev, host, gn * gbytes, hipMemcpyHostToDevice, s);
@@ -309,6 +316,8 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
       st = reconstruct_dev(c, dev, c->d_mask[si], gn, S, pitch, flags, c->d_status[si], s);
       if (st) return st;
+      // all rows back: present rows and padding come back byte-identical (they
+      // were copied in above and the kernels write only erased rows' [0, S))
       e = hipMemcpyAsync(host, dev, gn * gbytes, hipMemcpyDeviceToHost, s);
       if (e == hipSuccess) e = hipMemcpyAsync(status + g0, c->d_status[si], gn, hipMemcpyDeviceToHost, s);
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
