@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--shard-size", type=int, default=1350)
     ap.add_argument("--pitch", type=int, default=0, help="row pitch in HBM (default: shard size rounded to 16)")
     ap.add_argument("--erasures", type=int, default=2)
+    ap.add_argument("--layout", choices=["planar", "interleaved"], default="planar",
+                    help="planar = shard-major [d+p][G][pitch] batch; interleaved = [G][d+p][pitch]")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=1)
@@ -125,17 +127,19 @@ def main():
 
     enc = fec.New(d, p, device=local_rank)
     gen = torch.Generator(device=dev).manual_seed(args.seed + rank)
-    shards = torch.randint(0, 256, (G, n, pitch), dtype=torch.uint8, device=dev, generator=gen)
+    planar = args.layout == "planar"
+    shape = (n, G, pitch) if planar else (G, n, pitch)
+    shards = torch.randint(0, 256, shape, dtype=torch.uint8, device=dev, generator=gen)
     masks, erased = make_masks(G, n, e, args.seed + 1000 + rank, dev)
     stream = torch.cuda.current_stream()
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        enc.encode_batch(shards, shard_size=S, stream=stream)
+        enc.encode_batch(shards, shard_size=S, stream=stream, shard_major=planar)
         if ev is not None:
             ev[1].record(stream)
-        enc.reconstruct_batch(shards, masks, shard_size=S, stream=stream)
+        enc.reconstruct_batch(shards, masks, shard_size=S, stream=stream, shard_major=planar)
         if ev is not None:
             ev[2].record(stream)
 
@@ -171,16 +175,17 @@ def main():
     # bit-exactness at full size (outside the timed region): erase, reconstruct, compare
     verify = None
     if not args.no_verify:
-        ref = shards.clone()
+        view = shards.transpose(0, 1) if planar else shards  # [G, n, pitch] view either way
+        ref = view.clone()
         gi = torch.arange(G, device=dev)
         for j in range(e):
-            shards[gi, erased[:, j].to(dev)] = 0
-        enc.reconstruct_batch(shards, masks, shard_size=S, stream=stream)
-        ok_rt = bool(torch.equal(shards[:, :, :S], ref[:, :, :S]))
+            view[gi, erased[:, j].to(dev)] = 0
+        enc.reconstruct_batch(shards, masks, shard_size=S, stream=stream, shard_major=planar)
+        ok_rt = bool(torch.equal(view[:, :, :S], ref[:, :, :S]))
         par = ref[:, d:, :S].clone()
-        shards[:, d:, :] = 0
-        enc.encode_batch(shards, shard_size=S, stream=stream)
-        ok_idem = bool(torch.equal(shards[:, d:, :S], par))
+        view[:, d:, :] = 0
+        enc.encode_batch(shards, shard_size=S, stream=stream, shard_major=planar)
+        ok_idem = bool(torch.equal(view[:, d:, :S], par))
         del ref, par
         verify = {"round_trip_full_size": ok_rt, "encode_idempotent": ok_idem}
         okt = torch.tensor([int(ok_rt and ok_idem)], device=dev)
@@ -217,6 +222,7 @@ def main():
             "config": {"workload": f"({d}+{p})x{S}B groups, encode + {e}-erasure reconstruct, device-resident, "
                                    f"{G} groups/GPU", "groups_per_gpu": G, "total_groups": total_groups,
                        "data_shards": d, "parity_shards": p, "shard_size": S, "pitch": pitch, "erasures": e,
+                       "layout": "shard-major [d+p][G][pitch]" if planar else "group-major [G][d+p][pitch]",
                        "parallelism": f"dp{world} (independent packet groups, no collective)"},
             "pct_hbm_roofline": round(step_bytes_all / world * args.steps / elapsed / (HBM_PEAK_GBS * 1e9), 4),
             "roofline": roof, "kernels": kern, "verify": verify,

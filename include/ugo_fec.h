@@ -80,6 +80,16 @@ int ugo_fec_matrix(const ugo_fec* ctx, uint8_t* out /* (d+p)*d bytes */);
 int ugo_fec_encode(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_size,
                    size_t pitch, void* stream);
 
+/* Strided form of ugo_fec_encode: row r of group g is at
+ *     shards + g * group_stride + r * row_stride.
+ * ugo_fec_encode(pitch) == strided(row_stride = pitch, group_stride = (d+p)*pitch).
+ * The shard-major ("planar") batch layout [d+p][groups][pitch] -- row_stride =
+ * groups*pitch, group_stride = pitch -- turns every shard index into one
+ * sequential HBM stream and is the fastest layout on MI355X.
+ * Fast path: shards, row_stride and group_stride all multiples of 16. */
+int ugo_fec_encode_strided(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_size,
+                           size_t row_stride, size_t group_stride, void* stream);
+
 /* Encoder.Reconstruct(shards) (ugo/fec.go:202) for every group.  `present`
  * (device, u64 per group) marks the non-empty shards.  Survivors are the first
  * d present rows in index order (upstream rule), every erased row is written.
@@ -89,6 +99,11 @@ int ugo_fec_encode(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_si
 int ugo_fec_reconstruct(ugo_fec* ctx, uint8_t* shards, const uint64_t* present, size_t groups,
                         size_t shard_size, size_t pitch, unsigned flags, int8_t* status,
                         void* stream);
+
+/* Strided form of ugo_fec_reconstruct (layout as ugo_fec_encode_strided). */
+int ugo_fec_reconstruct_strided(ugo_fec* ctx, uint8_t* shards, const uint64_t* present, size_t groups,
+                                size_t shard_size, size_t row_stride, size_t group_stride,
+                                unsigned flags, int8_t* status, void* stream);
 
 /* ---- host-buffer batch (synchronous) ------------------------------------
  * Same contracts with HOST pointers: the engine stages through its own device

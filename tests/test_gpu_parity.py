@@ -278,3 +278,29 @@ def test_host_api_pipelined(gpu):
         assert np.array_equal(arr[:, :, :S], want[:, :, :S])
     finally:
         fec.host_free(buf)
+
+
+@pytest.mark.parametrize("d,p,S,pitch", [(10, 3, 1350, 1360), (32, 8, 9000, 9008), (6, 2, 77, 80)])
+def test_shard_major_layout(gpu, d, p, S, pitch):
+    """Planar [d+p][G][pitch] batches (ugo_fec_*_strided) give the same bytes."""
+    n, G = d + p, 513
+    host = _rand(G, n, pitch, 31 + d).numpy()
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    enc = fec.New(d, p)
+    t = _dev(np.ascontiguousarray(host.transpose(1, 0, 2)))
+    enc.encode_batch(t, shard_size=S, shard_major=True)
+    got = t.cpu().numpy().transpose(1, 0, 2)
+    assert np.array_equal(got, want)
+    rng = np.random.default_rng(3)
+    masks = np.array([((1 << n) - 1) & ~int(sum(1 << int(r) for r in rng.choice(n, int(rng.integers(0, p + 2)),
+                                                                                 replace=False)))
+                      for _ in range(G)], dtype=np.uint64)
+    inp = _erase(want, masks, n)
+    want2 = inp.copy()
+    rc, want_st = rs_ref.c_reconstruct(d, p, want2, masks, S=S)
+    t = _dev(np.ascontiguousarray(inp.transpose(1, 0, 2)))
+    st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    enc.reconstruct_batch(t, _masks_to_dev(masks), shard_size=S, status=st, shard_major=True)
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(t.cpu().numpy().transpose(1, 0, 2), want2)

@@ -85,53 +85,58 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dtab, tab.data(), tab.size(), hipMemcpyHostToDevice));
 
   Batch a{};
-  a.base = buf; a.group_bytes = n * pitch; a.nmask = (1ull << n) - 1; a.pitch = pitch; a.S = S;
+  a.base = buf; a.gstride = n * pitch; a.rstride = pitch; a.nmask = (1ull << n) - 1; a.S = S;
   a.chunks = 85; a.items = G * 85; a.desc = dtab; a.present = masks; a.desc_stride = stride; a.d = d;
   a.dpad = dpad; a.epad = epad;
+  Batch pl = a;  // planar [13][G][pitch]
+  pl.gstride = pitch;
+  pl.rstride = G * pitch;
   const double enc_bytes = double(G) * n * S, dec_bytes = double(G) * 12 * S;
 
   struct Var { std::string name; double bytes; std::function<void()> go; std::vector<float> t; };
   std::vector<Var> vars;
-  auto enc = [&](auto kern, int cpt, const char* nm) {
-    vars.push_back({nm, enc_bytes, [=]() {
-      Batch b = a; b.pass = (b.items + cpt - 1) / cpt;
-      hipLaunchKernelGGL(kern, dim3((b.pass + 255) / 256), dim3(256), 0, 0, b);
-    }, {}});
+  auto enc = [&](auto kern, const Batch& b, uint32_t gridmax, std::string nm) {
+    const uint32_t grid = std::min<uint32_t>((b.items + 255) / 256, gridmax);
+    vars.push_back({nm, enc_bytes, [=]() { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, b); }, {}});
   };
-  enc(k_encode_c<10, 3, 1, 0>, 1, "enc cpt1 nt0");
-  enc(k_encode_c<10, 3, 1, 1>, 1, "enc cpt1 nt1");
-  enc(k_encode_c<10, 3, 1, 2>, 1, "enc cpt1 nt2");
-  enc(k_encode_c<10, 3, 1, 3>, 1, "enc cpt1 nt3");
-  enc(k_encode_c<10, 3, 2, 0>, 2, "enc cpt2 nt0");
-  enc(k_encode_c<10, 3, 2, 3>, 2, "enc cpt2 nt3");
-  enc(k_encode_c<10, 3, 4, 0>, 4, "enc cpt4 nt0");
-  auto dec = [&](auto kern, const char* nm) {
+  for (int lay = 0; lay < 2; ++lay) {
+    const Batch& b = lay ? pl : a;
+    const std::string L = lay ? "planar" : "interl";
+    enc(k_encode_c<10, 3, 0>, b, 1u << 30, "enc " + L + " nt0 grid=full");
+    enc(k_encode_c<10, 3, 3>, b, 1u << 30, "enc " + L + " nt3 grid=full");
+    enc(k_encode_c<10, 3, 0>, b, 2048, "enc " + L + " nt0 grid=2048");
+    enc(k_encode_c<10, 3, 3>, b, 2048, "enc " + L + " nt3 grid=2048");
+    enc(k_encode_c<10, 3, 3>, b, 1024, "enc " + L + " nt3 grid=1024");
+    enc(k_encode_c<10, 3, 1>, b, 2048, "enc " + L + " nt1 grid=2048");
+  }
+  auto dec_simple = [&](auto kern, const Batch& b0, std::string nm) {
+    Batch b = b0;
     vars.push_back({nm, dec_bytes, [=]() {
-      Batch b = a; b.pass = b.items;
       hipLaunchKernelGGL(kern, dim3((b.items + 255) / 256), dim3(256), 0, 0, b);
     }, {}});
   };
-  {
-    // planar layout [13][G][pitch]: group stride = pitch, row stride = G * pitch
-    Batch pl = a;
-    pl.group_bytes = pitch;
-    pl.pitch = G * pitch;
-    vars.push_back({"enc planar cpt1 nt0", enc_bytes, [=]() {
-      Batch b = pl; b.pass = b.items;
-      hipLaunchKernelGGL((k_encode_c<10, 3, 1, 0>), dim3((b.pass + 255) / 256), dim3(256), 0, 0, b);
-    }, {}});
-    vars.push_back({"enc planar cpt1 nt3", enc_bytes, [=]() {
-      Batch b = pl; b.pass = b.items;
-      hipLaunchKernelGGL((k_encode_c<10, 3, 1, 3>), dim3((b.pass + 255) / 256), dim3(256), 0, 0, b);
-    }, {}});
-    vars.push_back({"dec planar mode1 nt0", dec_bytes, [=]() {
-      Batch b = pl; b.pass = b.items;
-      hipLaunchKernelGGL((k_apply<10, 1, 0>), dim3((b.items + 255) / 256), dim3(256), 0, 0, b);
-    }, {}});
+  auto dec_tiled = [&](auto kern, const Batch& b0, uint32_t tg, uint32_t gridmax, std::string nm) {
+    Batch b = b0;
+    b.tile_groups = tg;
+    const uint32_t ntiles = (G + tg - 1) / tg;
+    const uint32_t grid = std::min(ntiles, gridmax);
+    const size_t lds = size_t(tg) * b.desc_stride;
+    vars.push_back({nm, dec_bytes, [=]() { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, 0, b); }, {}});
+  };
+  for (int lay = 0; lay < 2; ++lay) {
+    const Batch& b = lay ? pl : a;
+    const std::string L = lay ? "planar" : "interl";
+    dec_simple(k_apply<10, 1, 0>, b, "dec " + L + " simple nt0");
+    dec_simple(k_apply<10, 1, 3>, b, "dec " + L + " simple nt3");
+    dec_tiled(k_apply_t<10, 1, 0, true, 4>, b, 36, 2048, "dec " + L + " tiled pipe o4 tg36 nt0");
+    dec_tiled(k_apply_t<10, 1, 3, true, 4>, b, 36, 2048, "dec " + L + " tiled pipe o4 tg36 nt3");
+    dec_tiled(k_apply_t<10, 1, 3, true, 3>, b, 36, 2048, "dec " + L + " tiled pipe o3 tg36 nt3");
+    dec_tiled(k_apply_t<10, 1, 3, false, 4>, b, 36, 2048, "dec " + L + " tiled nopipe o4 tg36 nt3");
+    dec_tiled(k_apply_t<10, 1, 3, false, 6>, b, 36, 2048, "dec " + L + " tiled nopipe o6 tg36 nt3");
+    dec_tiled(k_apply_t<10, 1, 3, true, 4>, b, 36, 1024, "dec " + L + " tiled pipe o4 tg36 nt3 g1024");
+    dec_tiled(k_apply_t<10, 1, 3, true, 4>, b, 18, 4096, "dec " + L + " tiled pipe o4 tg18 nt3");
+    dec_tiled(k_apply_t<10, 1, 3, true, 4>, b, 72, 2048, "dec " + L + " tiled pipe o4 tg72 nt3");
   }
-  dec(k_apply<10, 1, 0>, "dec mode1 nt0");
-  dec(k_apply<10, 1, 1>, "dec mode1 nt1");
-  dec(k_apply<10, 1, 3>, "dec mode1 nt3");
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));

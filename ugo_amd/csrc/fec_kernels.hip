@@ -36,6 +36,7 @@
 //    -> d x d sub-matrix -> Gauss-Jordan in LDS -> reconstruct coefficients).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <utility>
 
@@ -107,13 +108,19 @@ __device__ __forceinline__ void store16(uint8_t* p, const V4& y, uint32_t nb) {
     }
     return;
   }
-  // tail chunk of a row whose length is not a multiple of 16: rare lanes
-  uint32_t j = 0;
-  for (; j + 4 <= nb; j += 4) *reinterpret_cast<uint32_t*>(p + j) = y.v[j >> 2];
-  uint32_t w = y.v[j >> 2];
-  for (; j < nb; ++j) {
-    p[j] = static_cast<uint8_t>(w);
-    w >>= 8;
+  // tail chunk of a row whose length is not a multiple of 16 (rare lanes).
+  // No runtime indexing into y: that would demote it to scratch / LDS.
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t lo = 4u * j;
+    if (nb >= lo + 4) {
+      *reinterpret_cast<uint32_t*>(p + lo) = y.v[j];
+    } else if (nb > lo) {
+      const uint32_t w = y.v[j], rem = nb - lo;
+      p[lo] = static_cast<uint8_t>(w);
+      if (rem >= 2) p[lo + 1] = static_cast<uint8_t>(w >> 8);
+      if (rem >= 3) p[lo + 2] = static_cast<uint8_t>(w >> 16);
+    }
   }
 }
 
@@ -198,31 +205,67 @@ __device__ __forceinline__ void cparity_store(uint8_t* gp, uint64_t pitch, uint3
   ((store16<NT>(gp + static_cast<uint64_t>(D + I) * pitch, cparity<D, P, I>(x), nb)), ...);
 }
 
-// CPT column chunks per thread, `a.pass` items apart (so each pass is still a
-// coalesced 1 KiB-per-row wave access); all CPT*D loads are issued before any
-// arithmetic for more bytes in flight per wave.
-template <int D, int P, int CPT, int NT>
-__global__ __launch_bounds__(256) void k_encode_c(Batch a) {
-  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-  V4 x[CPT][D];
-  uint8_t* gp[CPT];
-  uint32_t nb[CPT];
+// Location of work item `item` (group-local index gl, 16-byte chunk c).
+struct Loc {
+  uint8_t* gp;   // row 0, chunk c of the group
+  uint32_t nb;   // valid bytes in the chunk (1..16)
+};
+
+__device__ __forceinline__ Loc locate(const Batch& a, uint32_t item) {
+  const uint32_t gl = item / a.chunks;
+  const uint32_t c = item - gl * a.chunks;
+  return Loc{a.base + (a.g0 + gl) * a.gstride + static_cast<uint64_t>(c) * 16u, a.S - c * 16u};
+}
+
+template <int D, int NT>
+__device__ __forceinline__ void load_rows(V4* x, const uint8_t* gp, uint64_t rstride) {
 #pragma unroll
-  for (int j = 0; j < CPT; ++j) {
-    const uint32_t item = t + j * a.pass;
-    gp[j] = nullptr;
-    if (item < a.items) {
-      const uint32_t gl = item / a.chunks;
-      const uint32_t c = item - gl * a.chunks;
-      gp[j] = a.base + (a.g0 + gl) * a.group_bytes + static_cast<uint64_t>(c) * 16u;
-      nb[j] = a.S - c * 16u;
-#pragma unroll
-      for (int k = 0; k < D; ++k) x[j][k] = load16<NT>(gp[j] + static_cast<uint64_t>(k) * a.pitch);
+  for (int k = 0; k < D; ++k) x[k] = load16<NT>(gp + static_cast<uint64_t>(k) * rstride);
+}
+
+// Persistent, software-pipelined: each thread walks items t, t+T, t+2T, ...
+// (T = threads in the grid; consecutive lanes = consecutive 16-B chunks, so a
+// wave's access to one row is 1 KiB contiguous) and issues the loads of its
+// next item before computing the current one, so every wave keeps D loads in
+// flight while its VALU works.
+// PIPE (small D): two register sets in ping-pong, so no array copies and the
+// compiler keeps everything in VGPRs; 4 waves/SIMD (<= 128 VGPRs).  Large D
+// (jumbo codes) cannot afford two sets and runs one item at a time.
+template <int D, int P, int NT, bool PIPE = (D <= 16)>
+__global__ __launch_bounds__(256, PIPE ? 4 : 1) void k_encode_c(Batch a) {
+  const uint32_t T = gridDim.x * 256u;
+  uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  if constexpr (!PIPE) {
+    for (; item < a.items; item += T) {
+      V4 x[D];
+      const Loc l = locate(a, item);
+      load_rows<D, NT>(x, l.gp, a.rstride);
+      cparity_store<D, P, NT>(l.gp, a.rstride, l.nb, x, std::make_integer_sequence<int, P>{});
+    }
+  } else {
+    V4 xa[D], xb[D];
+    Loc la = locate(a, item), lb{nullptr, 0};
+    load_rows<D, NT>(xa, la.gp, a.rstride);
+    for (;;) {
+      item += T;
+      const bool mb = item < a.items;
+      if (mb) {
+        lb = locate(a, item);
+        load_rows<D, NT>(xb, lb.gp, a.rstride);
+      }
+      cparity_store<D, P, NT>(la.gp, a.rstride, la.nb, xa, std::make_integer_sequence<int, P>{});
+      if (!mb) break;
+      item += T;
+      const bool ma = item < a.items;
+      if (ma) {
+        la = locate(a, item);
+        load_rows<D, NT>(xa, la.gp, a.rstride);
+      }
+      cparity_store<D, P, NT>(lb.gp, a.rstride, lb.nb, xb, std::make_integer_sequence<int, P>{});
+      if (!ma) break;
     }
   }
-#pragma unroll
-  for (int j = 0; j < CPT; ++j)
-    if (gp[j]) cparity_store<D, P, NT>(gp[j], a.pitch, nb[j], x[j], std::make_integer_sequence<int, P>{});
 }
 
 // ----------------------------------------------- descriptor-driven kernels
@@ -247,6 +290,46 @@ __device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
   return *reinterpret_cast<const uint32_t*>(p);
 }
 
+// y = sum_k c_k * x_k over GF(2^8) with per-lane coefficients: Horner over the
+// coefficient bits; bit b of c_k becomes a lane mask (v_bfe_i32) that enters
+// the 4 dwords of the chunk through v_bitop3 y ^ (x & m).  The mask and its
+// four uses are one asm unit: left to itself the compiler computes all 8*DMAX
+// masks once, keeps them live to share across the 4 dwords, and runs out of
+// VGPRs (124 -> 60 for DMAX = 10).
+template <int POS>
+__device__ __forceinline__ void mxor4(V4& y, const V4& x, uint32_t cw) {
+  uint32_t m;
+  asm("v_bfe_i32 %4, %5, %6, 1\n\t"
+      "v_bitop3_b32 %0, %0, %7, %4 bitop3:0x78\n\t"
+      "v_bitop3_b32 %1, %1, %8, %4 bitop3:0x78\n\t"
+      "v_bitop3_b32 %2, %2, %9, %4 bitop3:0x78\n\t"
+      "v_bitop3_b32 %3, %3, %10, %4 bitop3:0x78"
+      : "+v"(y.v[0]), "+v"(y.v[1]), "+v"(y.v[2]), "+v"(y.v[3]), "=&v"(m)
+      : "v"(cw), "i"(POS), "v"(x.v[0]), "v"(x.v[1]), "v"(x.v[2]), "v"(x.v[3]));
+}
+
+template <int DMAX, int B, int K>
+__device__ __forceinline__ void hv_terms(V4& y, const V4* x, const uint32_t* cw) {
+  mxor4<8 * (K & 3) + B>(y, x[K], cw[K >> 2]);
+  if constexpr (K + 1 < DMAX) hv_terms<DMAX, B, K + 1>(y, x, cw);
+}
+
+template <int DMAX, int B>
+__device__ __forceinline__ void hv_bits(V4& y, const V4* x, const uint32_t* cw) {
+  if constexpr (B != 7) xt4(y);
+  hv_terms<DMAX, B, 0>(y, x, cw);
+  if constexpr (B > 0) hv_bits<DMAX, B - 1>(y, x, cw);
+}
+
+template <int DMAX>
+__device__ __forceinline__ V4 horner_var(const V4* x, const uint32_t* cw) {
+  V4 y{{0u, 0u, 0u, 0u}};
+  hv_bits<DMAX, 7>(y, x, cw);
+  return y;
+}
+
+// Simple form: one item per thread, descriptor read from global memory
+// (kept for A/B against the tiled form below; tools/kvariants.hip).
 template <int DMAX, int MODE, int NT = 0>
 __global__ __launch_bounds__(256) void k_apply(Batch a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
@@ -260,8 +343,7 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
   if (MODE != 0 && a.status != nullptr && c == 0) a.status[g] = static_cast<int8_t>(st);
   const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
   if (st != 0 || e == 0) return;
-
-  uint8_t* gp = a.base + g * a.group_bytes + static_cast<uint64_t>(c) * 16u;
+  uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
   constexpr int NW = (DMAX + 3) / 4;
   uint32_t rows[NW];
 #pragma unroll
@@ -271,7 +353,7 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
   for (int k = 0; k < DMAX; ++k) {
     if (k < static_cast<int>(a.d)) {
       const uint32_t r = (rows[k >> 2] >> (8 * (k & 3))) & 0xffu;
-      x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.pitch);
+      x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
     } else {
       x[k] = V4{{0u, 0u, 0u, 0u}};
     }
@@ -283,25 +365,116 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
     uint32_t cw[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) cw[w] = ld32(coef + i * a.dpad + 4 * w);
-    V4 y{{0u, 0u, 0u, 0u}};
-#pragma unroll
-    for (int b = 7; b >= 0; --b) {
-      if (b != 7) xt4(y);
-#pragma unroll
-      for (int k = 0; k < DMAX; ++k) {
-        // sign-extended 1-bit field = 0 or 0xffffffff  (v_bfe_i32)
-        const uint32_t m = static_cast<uint32_t>(
-            static_cast<int32_t>(cw[k >> 2] << (31 - (8 * (k & 3) + b))) >> 31);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) y.v[j] = xor_and(y.v[j], x[k].v[j], m);
-      }
-    }
-    const uint32_t r = orow[i];
-    store16<NT>(gp + static_cast<uint64_t>(r) * a.pitch, y, nb);
+    const V4 y = horner_var<DMAX>(x, cw);
+    store16<NT>(gp + static_cast<uint64_t>(orow[i]) * a.rstride, y, nb);
   }
 }
 
-// generic: any alignment / pitch / d (<= 255); 4 columns per lane, byte I/O
+// Tiled form (production): a workgroup owns tiles of `tile_groups` groups.
+// Per tile it first stages every group's descriptor into LDS (one coalesced
+// pass: the presence-mask -> table lookup and the descriptor fetch happen once
+// per group per tile instead of once per 16-B item), then its 256 threads walk
+// the tile's items software-pipelined: the survivor-row loads of the next item
+// are in flight while the current item's outputs are computed.
+template <int DMAX>
+struct Item {
+  V4 x[DMAX];
+  uint8_t* gp;
+  const uint8_t* desc;  // LDS
+  uint32_t nb;
+  uint32_t e;           // outputs to produce (0: nothing / error)
+};
+
+template <int DMAX, int NT>
+__device__ __forceinline__ void item_issue(Item<DMAX>& it, const Batch& a, const uint8_t* sdesc, uint64_t tg0,
+                                           uint32_t li) {
+  const uint32_t gl = li / a.chunks;
+  const uint32_t c = li - gl * a.chunks;
+  it.desc = sdesc + gl * a.desc_stride;
+  const uint32_t hdr = *reinterpret_cast<const uint32_t*>(it.desc);
+  const uint32_t st = (hdr >> 16) & 0xffu;
+  const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
+  it.e = st ? 0u : e;
+  it.gp = a.base + (a.g0 + tg0 + gl) * a.gstride + static_cast<uint64_t>(c) * 16u;
+  it.nb = a.S - c * 16u;
+  if (it.e == 0) return;
+  constexpr int NW = (DMAX + 3) / 4;
+  uint32_t rows[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) rows[w] = *reinterpret_cast<const uint32_t*>(it.desc + 4 + 4 * w);
+  // rows k >= d are zero-padded (row 0, coefficient 0): load them anyway,
+  // cheaper than a per-k branch (DMAX == d for the common geometries)
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    const uint32_t r = (rows[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    it.x[k] = load16<NT>(it.gp + static_cast<uint64_t>(r) * a.rstride);
+  }
+}
+
+template <int DMAX, int NT>
+__device__ __forceinline__ void item_finish(const Item<DMAX>& it, const Batch& a) {
+  constexpr int NW = (DMAX + 3) / 4;
+  const uint8_t* orow = it.desc + 4 + a.dpad;
+  const uint8_t* coef = orow + a.epad;
+  for (uint32_t i = 0; i < it.e; ++i) {
+    uint32_t cw[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) cw[w] = *reinterpret_cast<const uint32_t*>(coef + i * a.dpad + 4 * w);
+    const V4 y = horner_var<DMAX>(it.x, cw);
+    store16<NT>(it.gp + static_cast<uint64_t>(orow[i]) * a.rstride, y, it.nb);
+  }
+}
+
+template <int DMAX, int MODE, int NT, bool PIPE = (DMAX <= 12), int OCC = (DMAX <= 16 ? 4 : 2)>
+__global__ __launch_bounds__(256, OCC) void k_apply_t(Batch a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sdesc[];
+  const uint32_t TG = a.tile_groups;
+  const uint64_t ngroups = a.items / a.chunks;
+  const uint64_t ntiles = (ngroups + TG - 1) / TG;
+  const uint32_t dq = a.desc_stride / 16;  // 16-B pieces per descriptor
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t tg0 = tile * TG;
+    const uint32_t tgn = static_cast<uint32_t>(min<uint64_t>(TG, ngroups - tg0));
+    for (uint32_t i = threadIdx.x; i < tgn * dq; i += 256u) {
+      const uint32_t gl = i / dq, q = i - gl * dq;
+      const uint8_t* src = desc_for<MODE>(a, a.g0 + tg0 + gl);
+      *reinterpret_cast<u32x4*>(sdesc + gl * a.desc_stride + q * 16) =
+          *reinterpret_cast<const u32x4*>(src + q * 16);
+    }
+    __syncthreads();
+    if (MODE != 0 && a.status != nullptr)
+      for (uint32_t i = threadIdx.x; i < tgn; i += 256u)
+        a.status[a.g0 + tg0 + i] = static_cast<int8_t>(sdesc[i * a.desc_stride + 2]);
+    const uint32_t titems = tgn * a.chunks;
+    uint32_t li = threadIdx.x;
+    if constexpr (!PIPE) {
+      for (; li < titems; li += 256u) {
+        Item<DMAX> A;
+        item_issue<DMAX, NT>(A, a, sdesc, tg0, li);
+        item_finish<DMAX, NT>(A, a);
+      }
+    } else if (li < titems) {
+      // ping-pong register sets: issue item li+256's loads, then finish li
+      Item<DMAX> A, B;
+      item_issue<DMAX, NT>(A, a, sdesc, tg0, li);
+      for (;;) {
+        li += 256u;
+        const bool mb = li < titems;
+        if (mb) item_issue<DMAX, NT>(B, a, sdesc, tg0, li);
+        item_finish<DMAX, NT>(A, a);
+        if (!mb) break;
+        li += 256u;
+        const bool ma = li < titems;
+        if (ma) item_issue<DMAX, NT>(A, a, sdesc, tg0, li);
+        item_finish<DMAX, NT>(B, a);
+        if (!ma) break;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// generic: any alignment / stride / d (<= 255); 4 columns per lane, byte I/O
 __device__ __forceinline__ uint32_t gfmul_var(uint32_t cbyte, uint32_t x) {
   uint32_t t = 0;
 #pragma unroll
@@ -326,7 +499,7 @@ __global__ __launch_bounds__(256) void k_apply_bytes(Batch a) {
   if (MODE != 0 && a.status != nullptr && c == 0) a.status[g] = static_cast<int8_t>(st);
   const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
   if (st != 0 || e == 0) return;
-  uint8_t* gp = a.base + g * a.group_bytes + static_cast<uint64_t>(c) * 4u;
+  uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 4u;
   const uint32_t nb = min(4u, a.S - c * 4u);
   const uint8_t* irow = desc + 4;
   const uint8_t* orow = desc + 4 + a.dpad;
@@ -334,12 +507,12 @@ __global__ __launch_bounds__(256) void k_apply_bytes(Batch a) {
   for (uint32_t i = 0; i < e; ++i) {
     uint32_t acc = 0;
     for (uint32_t k = 0; k < a.d; ++k) {
-      const uint8_t* src = gp + static_cast<uint64_t>(irow[k]) * a.pitch;
+      const uint8_t* src = gp + static_cast<uint64_t>(irow[k]) * a.rstride;
       uint32_t x = 0;
       for (uint32_t j = 0; j < nb; ++j) x |= static_cast<uint32_t>(src[j]) << (8 * j);
       acc ^= gfmul_var(coef[i * a.dpad + k], x);
     }
-    uint8_t* dst = gp + static_cast<uint64_t>(orow[i]) * a.pitch;
+    uint8_t* dst = gp + static_cast<uint64_t>(orow[i]) * a.rstride;
     for (uint32_t j = 0; j < nb; ++j) dst[j] = static_cast<uint8_t>(acc >> (8 * j));
   }
 }
@@ -447,23 +620,16 @@ __global__ __launch_bounds__(64) void k_prepare(Prep a) {
 }
 
 // ------------------------------------------------------------- launchers
-static inline uint32_t blocks_for(uint32_t items, uint32_t bs) { return (items + bs - 1) / bs; }
-
-template <int MODE>
-static hipError_t launch_apply_mode(int dmax, const Batch& a, hipStream_t s) {
-  const dim3 grid(blocks_for(a.items, 256)), block(256);
-  switch (dmax) {
-    case 4: hipLaunchKernelGGL((k_apply<4, MODE>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_apply<8, MODE>), grid, block, 0, s, a); break;
-    case 10: hipLaunchKernelGGL((k_apply<10, MODE>), grid, block, 0, s, a); break;
-    case 12: hipLaunchKernelGGL((k_apply<12, MODE>), grid, block, 0, s, a); break;
-    case 16: hipLaunchKernelGGL((k_apply<16, MODE>), grid, block, 0, s, a); break;
-    case 24: hipLaunchKernelGGL((k_apply<24, MODE>), grid, block, 0, s, a); break;
-    case 32: hipLaunchKernelGGL((k_apply<32, MODE>), grid, block, 0, s, a); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
+static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
+  return static_cast<uint32_t>((items + bs - 1) / bs);
 }
+
+// Launch policy (tuned with tools/kvariants.hip on MI355X)
+constexpr uint32_t kEncGridMax = 2048;     // persistent grid: 8 workgroups per CU
+constexpr int kEncNT = 3;                  // nontemporal loads + stores
+constexpr uint32_t kApplyGridMax = 2048;
+constexpr int kApplyNT = 3;
+constexpr uint32_t kApplyItemsPerThread = 12;
 
 int apply_dmax(int d) {
   if (d <= 4) return 4;
@@ -478,21 +644,39 @@ int apply_dmax(int d) {
 
 bool has_const_encode(int d, int p) { return (d == 10 && p == 3) || (d == 32 && p == 8); }
 
-// Tuned launch policy for the compile-time encode kernels (tools/kvariants.hip)
-constexpr int kEncCPT = 1;
-constexpr int kEncNT = 0;
-
-hipError_t launch_encode_const(int d, int p, const Batch& a0, hipStream_t s) {
-  Batch a = a0;
-  a.pass = (a.items + kEncCPT - 1) / kEncCPT;
-  const dim3 grid(blocks_for(a.pass, 256)), block(256);
+hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
+  const dim3 grid(std::min(blocks_for(a.items, 256), kEncGridMax)), block(256);
   if (d == 10 && p == 3)
-    hipLaunchKernelGGL((k_encode_c<10, 3, kEncCPT, kEncNT>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_encode_c<10, 3, kEncNT>), grid, block, 0, s, a);
   else if (d == 32 && p == 8)
-    hipLaunchKernelGGL((k_encode_c<32, 8, 1, kEncNT>), dim3(blocks_for(a.items, 256)), block, 0, s,
-                       [&] { Batch b = a0; b.pass = b.items; return b; }());
+    hipLaunchKernelGGL((k_encode_c<32, 8, kEncNT>), grid, block, 0, s, a);
   else
     return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+uint32_t apply_tile_groups(uint32_t chunks) {
+  return std::max<uint32_t>(1, (256u * kApplyItemsPerThread + chunks / 2) / chunks);
+}
+
+template <int MODE>
+static hipError_t launch_apply_mode(int dmax, const Batch& a0, hipStream_t s) {
+  Batch a = a0;
+  a.tile_groups = apply_tile_groups(a.chunks);
+  const uint64_t ngroups = a.items / a.chunks;
+  const uint64_t ntiles = (ngroups + a.tile_groups - 1) / a.tile_groups;
+  const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(ntiles, kApplyGridMax))), block(256);
+  const size_t lds = size_t(a.tile_groups) * a.desc_stride;
+  switch (dmax) {
+    case 4: hipLaunchKernelGGL((k_apply_t<4, MODE, kApplyNT>), grid, block, lds, s, a); break;
+    case 8: hipLaunchKernelGGL((k_apply_t<8, MODE, kApplyNT>), grid, block, lds, s, a); break;
+    case 10: hipLaunchKernelGGL((k_apply_t<10, MODE, kApplyNT>), grid, block, lds, s, a); break;
+    case 12: hipLaunchKernelGGL((k_apply_t<12, MODE, kApplyNT>), grid, block, lds, s, a); break;
+    case 16: hipLaunchKernelGGL((k_apply_t<16, MODE, kApplyNT>), grid, block, lds, s, a); break;
+    case 24: hipLaunchKernelGGL((k_apply_t<24, MODE, kApplyNT>), grid, block, lds, s, a); break;
+    case 32: hipLaunchKernelGGL((k_apply_t<32, MODE, kApplyNT>), grid, block, lds, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -10,19 +10,19 @@ namespace kern {
 
 // One launch covers groups [g0, g0 + items / chunks) of the batch.
 struct Batch {
-  uint8_t* base;            // shards[g][row][pitch] (device)
+  uint8_t* base;            // row r of group g at base + g*gstride + r*rstride (device)
   const uint8_t* desc;      // descriptor (MODE 0), table (MODE 1), workspace (MODE 2)
-  const uint64_t* present;  // device presence masks (MODE 1)
+  const uint64_t* present;  // device presence masks (MODE 1/2)
   int8_t* status;           // device per-group status, nullable
   uint64_t g0;              // first group of this launch
   uint64_t g_desc0;         // group whose descriptor sits at desc (MODE 2)
-  uint64_t group_bytes;     // (d + p) * pitch
+  uint64_t gstride;         // bytes between consecutive groups
+  uint64_t rstride;         // bytes between consecutive rows of one group
   uint64_t nmask;           // (1 << (d+p)) - 1
-  uint64_t pitch;           // row stride in bytes (rows of one group are `pitch` apart)
   uint32_t S;               // shard size in bytes
   uint32_t chunks;          // column chunks per group (16 B, or 4 B for the byte kernel)
   uint32_t items;           // groups_in_launch * chunks
-  uint32_t pass;            // items handled per "pass" of the grid (= items / chunks-per-thread)
+  uint32_t tile_groups;     // groups per LDS descriptor tile (k_apply_t)
   uint32_t desc_stride;
   uint32_t d;
   uint32_t dpad;
@@ -46,7 +46,8 @@ struct Prep {
   uint32_t epad;
 };
 
-int apply_dmax(int d);  // register-array bucket for k_apply, 0 if d > 32
+int apply_dmax(int d);  // register-array bucket for k_apply_t, 0 if d > 32
+uint32_t apply_tile_groups(uint32_t chunks);
 bool has_const_encode(int d, int p);
 hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s);
 hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s);

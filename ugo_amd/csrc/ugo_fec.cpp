@@ -135,17 +135,24 @@ void free_ctx(ugo_fec* c) {
   delete c;
 }
 
-bool fast_layout(const ugo_fec* c, const uint8_t* shards, size_t pitch) {
-  return (reinterpret_cast<uintptr_t>(shards) % 16 == 0) && (pitch % 16 == 0) &&
-         ugo::kern::apply_dmax(c->d) != 0 && pitch <= 0xffffffffu;
+struct Layout {
+  uint64_t rstride;  // bytes between rows of one group
+  uint64_t gstride;  // bytes between groups
+};
+
+Layout interleaved(const ugo_fec* c, size_t pitch) { return Layout{pitch, uint64_t(c->n) * pitch}; }
+
+bool fast_layout(const ugo_fec* c, const uint8_t* shards, const Layout& L) {
+  return (reinterpret_cast<uintptr_t>(shards) % 16 == 0) && (L.rstride % 16 == 0) && (L.gstride % 16 == 0) &&
+         ugo::kern::apply_dmax(c->d) != 0;
 }
 
-ugo::kern::Batch base_batch(const ugo_fec* c, uint8_t* shards, size_t S, size_t pitch) {
+ugo::kern::Batch base_batch(const ugo_fec* c, uint8_t* shards, size_t S, const Layout& L) {
   ugo::kern::Batch a{};
   a.base = shards;
-  a.group_bytes = uint64_t(c->n) * pitch;
+  a.gstride = L.gstride;
+  a.rstride = L.rstride;
   a.nmask = c->n >= 64 ? ~0ull : ((1ull << c->n) - 1);
-  a.pitch = static_cast<uint32_t>(pitch);
   a.S = static_cast<uint32_t>(S);
   a.desc_stride = c->desc_stride;
   a.d = static_cast<uint32_t>(c->d);
@@ -154,18 +161,20 @@ ugo::kern::Batch base_batch(const ugo_fec* c, uint8_t* shards, size_t S, size_t 
   return a;
 }
 
-int check_batch(const ugo_fec* c, const void* shards, size_t groups, size_t S, size_t pitch) {
+int check_batch(const ugo_fec* c, const void* shards, size_t groups, size_t S, const Layout& L) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;  // checkShards: all shards empty
-  if (pitch < S || S > 0xffffffffu || pitch > 0xffffffffu) return UGO_FEC_ERR_INVALID_ARG;
+  if (S > 0xffffffffu) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->n > 1 && L.rstride < S) return UGO_FEC_ERR_INVALID_ARG;   // rows would overlap
+  if (groups > 1 && L.gstride < S) return UGO_FEC_ERR_INVALID_ARG;
   if (groups && !shards) return UGO_FEC_ERR_INVALID_ARG;
   return UGO_FEC_OK;
 }
 
-int encode_dev(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch, hipStream_t s) {
+int encode_dev(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, const Layout& L, hipStream_t s) {
   if (c->p == 0 || groups == 0) return UGO_FEC_OK;
-  const bool fast = fast_layout(c, shards, pitch);
-  ugo::kern::Batch a = base_batch(c, shards, S, pitch);
+  const bool fast = fast_layout(c, shards, L);
+  ugo::kern::Batch a = base_batch(c, shards, S, L);
   a.desc = c->d_encdesc;
   a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
   const size_t per = std::max<size_t>(1, kMaxItems / a.chunks);
@@ -196,13 +205,13 @@ int ensure_work(ugo_fec* c, size_t groups) {
 }
 
 int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
-                    size_t pitch, unsigned flags, int8_t* status, hipStream_t s) {
+                    const Layout& L, unsigned flags, int8_t* status, hipStream_t s) {
   if (groups == 0) return UGO_FEC_OK;
   if (!present) return UGO_FEC_ERR_INVALID_ARG;
   if (c->n > 64) return UGO_FEC_ERR_INVALID_ARG;  // 64-bit presence masks
-  const bool fast = fast_layout(c, shards, pitch);
+  const bool fast = fast_layout(c, shards, L);
   const int mode = c->d_table ? 1 : 2;
-  ugo::kern::Batch a = base_batch(c, shards, S, pitch);
+  ugo::kern::Batch a = base_batch(c, shards, S, L);
   a.present = present;
   a.status = status;
   a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
@@ -297,7 +306,7 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
       // data rows in, parity rows out
       e = hipMemcpy2DAsync(dev, gbytes, host, gbytes, size_t(c->d) * pitch, gn, hipMemcpyHostToDevice, s);
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
-      st = encode_dev(c, dev, gn, S, pitch, s);
+      st = encode_dev(c, dev, gn, S, interleaved(c, pitch), s);
       if (st) return st;
       // parity rows out, bytes [0, S) only: padding bytes of the caller's rows are never written
       hipMemcpy3DParms cp{};
@@ -314,7 +323,7 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
       if (e == hipSuccess)
         e = hipMemcpyAsync(c->d_mask[si], present + g0, gn * sizeof(uint64_t), hipMemcpyHostToDevice, s);
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
-      st = reconstruct_dev(c, dev, c->d_mask[si], gn, S, pitch, flags, c->d_status[si], s);
+      st = reconstruct_dev(c, dev, c->d_mask[si], gn, S, interleaved(c, pitch), flags, c->d_status[si], s);
       if (st) return st;
       // all rows back: present rows and padding come back byte-identical (they
       // were copied in above and the kernels write only erased rows' [0, S))
@@ -457,25 +466,45 @@ int ugo_fec_matrix(const ugo_fec* c, uint8_t* out) {
   return UGO_FEC_OK;
 }
 
-int ugo_fec_encode(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch, void* stream) {
-  int st = check_batch(c, shards, groups, S, pitch);
+int ugo_fec_encode_strided(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t row_stride,
+                           size_t group_stride, void* stream) {
+  const Layout L{row_stride, group_stride};
+  int st = check_batch(c, shards, groups, S, L);
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
-  return encode_dev(c, shards, groups, S, pitch, static_cast<hipStream_t>(stream));
+  return encode_dev(c, shards, groups, S, L, static_cast<hipStream_t>(stream));
+}
+
+int ugo_fec_encode(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch, void* stream) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (pitch < S) return S == 0 ? UGO_FEC_ERR_SHARD_NO_DATA : UGO_FEC_ERR_INVALID_ARG;
+  return ugo_fec_encode_strided(c, shards, groups, S, pitch, size_t(c->n) * pitch, stream);
+}
+
+int ugo_fec_reconstruct_strided(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
+                                size_t row_stride, size_t group_stride, unsigned flags, int8_t* status,
+                                void* stream) {
+  const Layout L{row_stride, group_stride};
+  int st = check_batch(c, shards, groups, S, L);
+  if (st) return st;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  return reconstruct_dev(c, shards, present, groups, S, L, flags, status, static_cast<hipStream_t>(stream));
 }
 
 int ugo_fec_reconstruct(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
                         size_t pitch, unsigned flags, int8_t* status, void* stream) {
-  int st = check_batch(c, shards, groups, S, pitch);
-  if (st) return st;
-  DeviceGuard g(c->device);
-  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
-  return reconstruct_dev(c, shards, present, groups, S, pitch, flags, status, static_cast<hipStream_t>(stream));
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (pitch < S) return S == 0 ? UGO_FEC_ERR_SHARD_NO_DATA : UGO_FEC_ERR_INVALID_ARG;
+  return ugo_fec_reconstruct_strided(c, shards, present, groups, S, pitch, size_t(c->n) * pitch, flags, status,
+                                     stream);
 }
 
 int ugo_fec_encode_host(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch) {
-  int st = check_batch(c, shards, groups, S, pitch);
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (pitch < S) return S == 0 ? UGO_FEC_ERR_SHARD_NO_DATA : UGO_FEC_ERR_INVALID_ARG;
+  int st = check_batch(c, shards, groups, S, interleaved(c, pitch));
   if (st || groups == 0 || c->p == 0) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
@@ -484,7 +513,9 @@ int ugo_fec_encode_host(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, si
 
 int ugo_fec_reconstruct_host(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
                              size_t pitch, unsigned flags, int8_t* status) {
-  int st = check_batch(c, shards, groups, S, pitch);
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (pitch < S) return S == 0 ? UGO_FEC_ERR_SHARD_NO_DATA : UGO_FEC_ERR_INVALID_ARG;
+  int st = check_batch(c, shards, groups, S, interleaved(c, pitch));
   if (st || groups == 0) return st;
   if (!present) return UGO_FEC_ERR_INVALID_ARG;
   if (c->n > 64) return UGO_FEC_ERR_INVALID_ARG;

@@ -105,6 +105,8 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_matrix.argtypes = [vp, vp]
     lib.ugo_fec_encode.argtypes = [vp, vp, sz, sz, sz, vp]
     lib.ugo_fec_reconstruct.argtypes = [vp, vp, vp, sz, sz, sz, u, vp, vp]
+    lib.ugo_fec_encode_strided.argtypes = [vp, vp, sz, sz, sz, sz, vp]
+    lib.ugo_fec_reconstruct_strided.argtypes = [vp, vp, vp, sz, sz, sz, sz, u, vp, vp]
     lib.ugo_fec_encode_host.argtypes = [vp, vp, sz, sz, sz]
     lib.ugo_fec_reconstruct_host.argtypes = [vp, vp, vp, sz, sz, sz, u, vp]
     lib.ugo_fec_check_shards.argtypes = [i, vp, i, ctypes.POINTER(sz)]
@@ -181,26 +183,38 @@ class Encoder:
         return out
 
     # -------------------------------------------------- device-resident batch
-    def encode_batch(self, shards, shard_size: Optional[int] = None, stream=None):
-        """shards: torch.uint8 CUDA tensor [G, d+p, pitch] (row-contiguous)."""
-        G, n, pitch = shards.shape
-        assert n == self.Shards and shards.stride(2) == 1 and shards.stride(1) == pitch \
-            and shards.stride(0) == n * pitch, "shards must be a contiguous [G, d+p, pitch] tensor"
+    def _geom(self, shards, shard_major: bool):
+        """(groups, pitch, row_stride, group_stride) of a contiguous uint8 tensor:
+        group-major [G, d+p, pitch] or shard-major [d+p, G, pitch] (planar)."""
+        assert shards.is_contiguous() and shards.dim() == 3 and shards.element_size() == 1
+        if shard_major:
+            n, G, pitch = shards.shape
+            rs, gs = G * pitch, pitch
+        else:
+            G, n, pitch = shards.shape
+            rs, gs = pitch, n * pitch
+        assert n == self.Shards, f"expected {self.Shards} rows per group, got {n}"
+        return G, pitch, rs, gs
+
+    def encode_batch(self, shards, shard_size: Optional[int] = None, stream=None, shard_major: bool = False):
+        """Encode every group of a device tensor: [G, d+p, pitch] (default) or,
+        with shard_major=True, the planar [d+p, G, pitch] layout."""
+        G, pitch, rs, gs = self._geom(shards, shard_major)
         S = pitch if shard_size is None else shard_size
-        _raise(load_library().ugo_fec_encode(self._h, shards.data_ptr(), G, S, pitch, _stream_handle(stream)))
+        _raise(load_library().ugo_fec_encode_strided(self._h, shards.data_ptr(), G, S, rs, gs,
+                                                     _stream_handle(stream)))
 
     def reconstruct_batch(self, shards, present, shard_size: Optional[int] = None, data_only=False,
-                          status=None, stream=None):
-        """present: torch.int64/uint64 CUDA tensor [G] of presence bitmasks;
-        status: optional torch.int8 CUDA tensor [G]."""
-        G, n, pitch = shards.shape
-        assert n == self.Shards and shards.is_contiguous()
+                          status=None, stream=None, shard_major: bool = False):
+        """present: int64/uint64 CUDA tensor [G] of presence bitmasks (bit r = shard r
+        non-empty); status: optional int8 CUDA tensor [G]."""
+        G, pitch, rs, gs = self._geom(shards, shard_major)
         assert present.is_contiguous() and present.numel() == G and present.element_size() == 8
         S = pitch if shard_size is None else shard_size
-        st = 0 if status is None else status.data_ptr()
-        _raise(load_library().ugo_fec_reconstruct(self._h, shards.data_ptr(), present.data_ptr(), G, S, pitch,
-                                                  RECONSTRUCT_DATA_ONLY if data_only else 0, st or None,
-                                                  _stream_handle(stream)))
+        st = None if status is None else status.data_ptr()
+        _raise(load_library().ugo_fec_reconstruct_strided(self._h, shards.data_ptr(), present.data_ptr(), G, S, rs,
+                                                          gs, RECONSTRUCT_DATA_ONLY if data_only else 0, st,
+                                                          _stream_handle(stream)))
 
     # ------------------------------------------------------ host-buffer batch
     def encode_host(self, shards: np.ndarray, shard_size: Optional[int] = None):
