@@ -223,49 +223,18 @@ __device__ __forceinline__ void load_rows(V4* x, const uint8_t* gp, uint64_t rst
   for (int k = 0; k < D; ++k) x[k] = load16<NT>(gp + static_cast<uint64_t>(k) * rstride);
 }
 
-// Persistent, software-pipelined: each thread walks items t, t+T, t+2T, ...
-// (T = threads in the grid; consecutive lanes = consecutive 16-B chunks, so a
-// wave's access to one row is 1 KiB contiguous) and issues the loads of its
-// next item before computing the current one, so every wave keeps D loads in
-// flight while its VALU works.
-// PIPE (small D): two register sets in ping-pong, so no array copies and the
-// compiler keeps everything in VGPRs; 4 waves/SIMD (<= 128 VGPRs).  Large D
-// (jumbo codes) cannot afford two sets and runs one item at a time.
-template <int D, int P, int NT, bool PIPE = (D <= 16)>
-__global__ __launch_bounds__(256, PIPE ? 4 : 1) void k_encode_c(Batch a) {
-  const uint32_t T = gridDim.x * 256u;
-  uint32_t item = blockIdx.x * 256u + threadIdx.x;
+// One 16-byte column chunk per thread over a full grid (items / 256 blocks).
+// Measured on MI355X (tools/kvariants.hip): a full grid at
+// 8 waves/SIMD (62 VGPRs) beats persistent grids and software-pipelined
+// (ping-pong) forms, whose second register set halves occupancy.
+template <int D, int P, int NT>
+__global__ __launch_bounds__(256) void k_encode_c(Batch a) {
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
   if (item >= a.items) return;
-  if constexpr (!PIPE) {
-    for (; item < a.items; item += T) {
-      V4 x[D];
-      const Loc l = locate(a, item);
-      load_rows<D, NT>(x, l.gp, a.rstride);
-      cparity_store<D, P, NT>(l.gp, a.rstride, l.nb, x, std::make_integer_sequence<int, P>{});
-    }
-  } else {
-    V4 xa[D], xb[D];
-    Loc la = locate(a, item), lb{nullptr, 0};
-    load_rows<D, NT>(xa, la.gp, a.rstride);
-    for (;;) {
-      item += T;
-      const bool mb = item < a.items;
-      if (mb) {
-        lb = locate(a, item);
-        load_rows<D, NT>(xb, lb.gp, a.rstride);
-      }
-      cparity_store<D, P, NT>(la.gp, a.rstride, la.nb, xa, std::make_integer_sequence<int, P>{});
-      if (!mb) break;
-      item += T;
-      const bool ma = item < a.items;
-      if (ma) {
-        la = locate(a, item);
-        load_rows<D, NT>(xa, la.gp, a.rstride);
-      }
-      cparity_store<D, P, NT>(lb.gp, a.rstride, lb.nb, xb, std::make_integer_sequence<int, P>{});
-      if (!ma) break;
-    }
-  }
+  const Loc l = locate(a, item);
+  V4 x[D];
+  load_rows<D, NT>(x, l.gp, a.rstride);
+  cparity_store<D, P, NT>(l.gp, a.rstride, l.nb, x, std::make_integer_sequence<int, P>{});
 }
 
 // ----------------------------------------------- descriptor-driven kernels
@@ -328,9 +297,11 @@ __device__ __forceinline__ V4 horner_var(const V4* x, const uint32_t* cw) {
   return y;
 }
 
-// Simple form: one item per thread, descriptor read from global memory
-// (kept for A/B against the tiled form below; tools/kvariants.hip).
-template <int DMAX, int MODE, int NT = 0>
+// One 16-byte chunk per thread over a full grid; the descriptor (presence
+// mask -> table entry, or the group's workspace entry) is read per thread from
+// L2.  Staging descriptors per tile in LDS and software-pipelining the next
+// item measured slower (fewer waves per SIMD), see DESIGN.md §4.
+template <int DMAX, int MODE, int NT>
 __global__ __launch_bounds__(256) void k_apply(Batch a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
   if (item >= a.items) return;
@@ -367,110 +338,6 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
     for (int w = 0; w < NW; ++w) cw[w] = ld32(coef + i * a.dpad + 4 * w);
     const V4 y = horner_var<DMAX>(x, cw);
     store16<NT>(gp + static_cast<uint64_t>(orow[i]) * a.rstride, y, nb);
-  }
-}
-
-// Tiled form (production): a workgroup owns tiles of `tile_groups` groups.
-// Per tile it first stages every group's descriptor into LDS (one coalesced
-// pass: the presence-mask -> table lookup and the descriptor fetch happen once
-// per group per tile instead of once per 16-B item), then its 256 threads walk
-// the tile's items software-pipelined: the survivor-row loads of the next item
-// are in flight while the current item's outputs are computed.
-template <int DMAX>
-struct Item {
-  V4 x[DMAX];
-  uint8_t* gp;
-  const uint8_t* desc;  // LDS
-  uint32_t nb;
-  uint32_t e;           // outputs to produce (0: nothing / error)
-};
-
-template <int DMAX, int NT>
-__device__ __forceinline__ void item_issue(Item<DMAX>& it, const Batch& a, const uint8_t* sdesc, uint64_t tg0,
-                                           uint32_t li) {
-  const uint32_t gl = li / a.chunks;
-  const uint32_t c = li - gl * a.chunks;
-  it.desc = sdesc + gl * a.desc_stride;
-  const uint32_t hdr = *reinterpret_cast<const uint32_t*>(it.desc);
-  const uint32_t st = (hdr >> 16) & 0xffu;
-  const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
-  it.e = st ? 0u : e;
-  it.gp = a.base + (a.g0 + tg0 + gl) * a.gstride + static_cast<uint64_t>(c) * 16u;
-  it.nb = a.S - c * 16u;
-  if (it.e == 0) return;
-  constexpr int NW = (DMAX + 3) / 4;
-  uint32_t rows[NW];
-#pragma unroll
-  for (int w = 0; w < NW; ++w) rows[w] = *reinterpret_cast<const uint32_t*>(it.desc + 4 + 4 * w);
-  // rows k >= d are zero-padded (row 0, coefficient 0): load them anyway,
-  // cheaper than a per-k branch (DMAX == d for the common geometries)
-#pragma unroll
-  for (int k = 0; k < DMAX; ++k) {
-    const uint32_t r = (rows[k >> 2] >> (8 * (k & 3))) & 0xffu;
-    it.x[k] = load16<NT>(it.gp + static_cast<uint64_t>(r) * a.rstride);
-  }
-}
-
-template <int DMAX, int NT>
-__device__ __forceinline__ void item_finish(const Item<DMAX>& it, const Batch& a) {
-  constexpr int NW = (DMAX + 3) / 4;
-  const uint8_t* orow = it.desc + 4 + a.dpad;
-  const uint8_t* coef = orow + a.epad;
-  for (uint32_t i = 0; i < it.e; ++i) {
-    uint32_t cw[NW];
-#pragma unroll
-    for (int w = 0; w < NW; ++w) cw[w] = *reinterpret_cast<const uint32_t*>(coef + i * a.dpad + 4 * w);
-    const V4 y = horner_var<DMAX>(it.x, cw);
-    store16<NT>(it.gp + static_cast<uint64_t>(orow[i]) * a.rstride, y, it.nb);
-  }
-}
-
-template <int DMAX, int MODE, int NT, bool PIPE = (DMAX <= 12), int OCC = (DMAX <= 16 ? 4 : 2)>
-__global__ __launch_bounds__(256, OCC) void k_apply_t(Batch a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sdesc[];
-  const uint32_t TG = a.tile_groups;
-  const uint64_t ngroups = a.items / a.chunks;
-  const uint64_t ntiles = (ngroups + TG - 1) / TG;
-  const uint32_t dq = a.desc_stride / 16;  // 16-B pieces per descriptor
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t tg0 = tile * TG;
-    const uint32_t tgn = static_cast<uint32_t>(min<uint64_t>(TG, ngroups - tg0));
-    for (uint32_t i = threadIdx.x; i < tgn * dq; i += 256u) {
-      const uint32_t gl = i / dq, q = i - gl * dq;
-      const uint8_t* src = desc_for<MODE>(a, a.g0 + tg0 + gl);
-      *reinterpret_cast<u32x4*>(sdesc + gl * a.desc_stride + q * 16) =
-          *reinterpret_cast<const u32x4*>(src + q * 16);
-    }
-    __syncthreads();
-    if (MODE != 0 && a.status != nullptr)
-      for (uint32_t i = threadIdx.x; i < tgn; i += 256u)
-        a.status[a.g0 + tg0 + i] = static_cast<int8_t>(sdesc[i * a.desc_stride + 2]);
-    const uint32_t titems = tgn * a.chunks;
-    uint32_t li = threadIdx.x;
-    if constexpr (!PIPE) {
-      for (; li < titems; li += 256u) {
-        Item<DMAX> A;
-        item_issue<DMAX, NT>(A, a, sdesc, tg0, li);
-        item_finish<DMAX, NT>(A, a);
-      }
-    } else if (li < titems) {
-      // ping-pong register sets: issue item li+256's loads, then finish li
-      Item<DMAX> A, B;
-      item_issue<DMAX, NT>(A, a, sdesc, tg0, li);
-      for (;;) {
-        li += 256u;
-        const bool mb = li < titems;
-        if (mb) item_issue<DMAX, NT>(B, a, sdesc, tg0, li);
-        item_finish<DMAX, NT>(A, a);
-        if (!mb) break;
-        li += 256u;
-        const bool ma = li < titems;
-        if (ma) item_issue<DMAX, NT>(A, a, sdesc, tg0, li);
-        item_finish<DMAX, NT>(B, a);
-        if (!ma) break;
-      }
-    }
-    __syncthreads();
   }
 }
 
@@ -625,11 +492,8 @@ static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
 }
 
 // Launch policy (tuned with tools/kvariants.hip on MI355X)
-constexpr uint32_t kEncGridMax = 2048;     // persistent grid: 8 workgroups per CU
-constexpr int kEncNT = 3;                  // nontemporal loads + stores
-constexpr uint32_t kApplyGridMax = 2048;
-constexpr int kApplyNT = 3;
-constexpr uint32_t kApplyItemsPerThread = 12;
+constexpr int kEncNT = 1;    // nontemporal loads, plain stores
+constexpr int kApplyNT = 3;  // nontemporal loads and stores
 
 int apply_dmax(int d) {
   if (d <= 4) return 4;
@@ -645,7 +509,7 @@ int apply_dmax(int d) {
 bool has_const_encode(int d, int p) { return (d == 10 && p == 3) || (d == 32 && p == 8); }
 
 hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
-  const dim3 grid(std::min(blocks_for(a.items, 256), kEncGridMax)), block(256);
+  const dim3 grid(blocks_for(a.items, 256)), block(256);
   if (d == 10 && p == 3)
     hipLaunchKernelGGL((k_encode_c<10, 3, kEncNT>), grid, block, 0, s, a);
   else if (d == 32 && p == 8)
@@ -655,26 +519,17 @@ hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-uint32_t apply_tile_groups(uint32_t chunks) {
-  return std::max<uint32_t>(1, (256u * kApplyItemsPerThread + chunks / 2) / chunks);
-}
-
 template <int MODE>
-static hipError_t launch_apply_mode(int dmax, const Batch& a0, hipStream_t s) {
-  Batch a = a0;
-  a.tile_groups = apply_tile_groups(a.chunks);
-  const uint64_t ngroups = a.items / a.chunks;
-  const uint64_t ntiles = (ngroups + a.tile_groups - 1) / a.tile_groups;
-  const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>(ntiles, kApplyGridMax))), block(256);
-  const size_t lds = size_t(a.tile_groups) * a.desc_stride;
+static hipError_t launch_apply_mode(int dmax, const Batch& a, hipStream_t s) {
+  const dim3 grid(blocks_for(a.items, 256)), block(256);
   switch (dmax) {
-    case 4: hipLaunchKernelGGL((k_apply_t<4, MODE, kApplyNT>), grid, block, lds, s, a); break;
-    case 8: hipLaunchKernelGGL((k_apply_t<8, MODE, kApplyNT>), grid, block, lds, s, a); break;
-    case 10: hipLaunchKernelGGL((k_apply_t<10, MODE, kApplyNT>), grid, block, lds, s, a); break;
-    case 12: hipLaunchKernelGGL((k_apply_t<12, MODE, kApplyNT>), grid, block, lds, s, a); break;
-    case 16: hipLaunchKernelGGL((k_apply_t<16, MODE, kApplyNT>), grid, block, lds, s, a); break;
-    case 24: hipLaunchKernelGGL((k_apply_t<24, MODE, kApplyNT>), grid, block, lds, s, a); break;
-    case 32: hipLaunchKernelGGL((k_apply_t<32, MODE, kApplyNT>), grid, block, lds, s, a); break;
+    case 4: hipLaunchKernelGGL((k_apply<4, MODE, kApplyNT>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_apply<8, MODE, kApplyNT>), grid, block, 0, s, a); break;
+    case 10: hipLaunchKernelGGL((k_apply<10, MODE, kApplyNT>), grid, block, 0, s, a); break;
+    case 12: hipLaunchKernelGGL((k_apply<12, MODE, kApplyNT>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_apply<16, MODE, kApplyNT>), grid, block, 0, s, a); break;
+    case 24: hipLaunchKernelGGL((k_apply<24, MODE, kApplyNT>), grid, block, 0, s, a); break;
+    case 32: hipLaunchKernelGGL((k_apply<32, MODE, kApplyNT>), grid, block, 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

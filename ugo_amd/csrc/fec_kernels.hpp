@@ -22,7 +22,6 @@ struct Batch {
   uint32_t S;               // shard size in bytes
   uint32_t chunks;          // column chunks per group (16 B, or 4 B for the byte kernel)
   uint32_t items;           // groups_in_launch * chunks
-  uint32_t tile_groups;     // groups per LDS descriptor tile (k_apply_t)
   uint32_t desc_stride;
   uint32_t d;
   uint32_t dpad;
@@ -46,8 +45,7 @@ struct Prep {
   uint32_t epad;
 };
 
-int apply_dmax(int d);  // register-array bucket for k_apply_t, 0 if d > 32
-uint32_t apply_tile_groups(uint32_t chunks);
+int apply_dmax(int d);  // register-array bucket for k_apply, 0 if d > 32
 bool has_const_encode(int d, int p);
 hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s);
 hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s);
