@@ -149,7 +149,8 @@ def test_reconstruct_inconsistent_inputs(gpu, table_max, monkeypatch):
 
 @pytest.mark.parametrize("d,p,S,pitch", [(4, 2, 100, 112), (5, 5, 64, 64), (12, 4, 333, 336),
                                          (20, 4, 200, 208), (32, 8, 9000, 9008), (3, 1, 50, 50),
-                                         (40, 6, 70, 80), (1, 1, 7, 16), (7, 0, 32, 32)])
+                                         (40, 6, 70, 80), (1, 1, 7, 16), (7, 0, 32, 32),
+                                         (5, 3, 1500, 1504), (8, 4, 4096, 4096), (16, 4, 1030, 1040)])
 def test_generic_geometries(gpu, d, p, S, pitch):
     n = d + p
     G = 300

@@ -114,10 +114,30 @@ int main(int argc, char** argv) {
     add(k_apply<10, 1, 0>, b, dec_bytes, "dec " + L + " nt0");
     add(k_apply<10, 1, 1>, b, dec_bytes, "dec " + L + " nt1");
     add(k_apply<10, 1, 3>, b, dec_bytes, "dec " + L + " nt3");
+    add(k_apply_w<10, 1, 3>, b, dec_bytes, "dec " + L + " nt3 wave-scalar-desc");
+    add(k_apply_w<10, 1, 1>, b, dec_bytes, "dec " + L + " nt1 wave-scalar-desc");
     Batch bf = b;
     bf.present = masks_fixed;
     add(k_apply<10, 1, 3>, bf, dec_bytes, "dec " + L + " nt3 fixed-pattern");
+    // same fixed pattern through a uniform (MODE 0) descriptor: no per-lane
+    // mask -> descriptor dependent loads, scalar descriptor reads
+    Batch bu = b;
+    bu.desc = dtab + hf[0] * stride;
+    add(k_apply<10, 0, 3>, bu, dec_bytes, "dec " + L + " nt3 fixed-pattern uniform-desc");
   }
+
+  // encode -> reconstruct back-to-back (the bench step): the encode's store
+  // policy changes what the following reconstruct finds in L2 / MALL
+  auto pair = [&](auto ke, auto kd, const Batch& b, std::string nm) {
+    const uint32_t grid = (b.items + 255) / 256;
+    vars.push_back({nm, enc_bytes + dec_bytes, [=]() {
+      hipLaunchKernelGGL(ke, dim3(grid), dim3(256), 0, 0, b);
+      hipLaunchKernelGGL(kd, dim3(grid), dim3(256), 0, 0, b);
+    }, {}});
+  };
+  pair(k_encode_c<10, 3, 1>, k_apply<10, 1, 3>, pl, "pair planar enc-nt1 dec-nt3");
+  pair(k_encode_c<10, 3, 3>, k_apply<10, 1, 3>, pl, "pair planar enc-nt3 dec-nt3");
+  pair(k_encode_c<10, 3, 1>, k_apply<10, 1, 1>, pl, "pair planar enc-nt1 dec-nt1");
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));

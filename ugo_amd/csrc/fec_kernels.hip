@@ -341,6 +341,71 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
   }
 }
 
+// Wave-scalar form, for rows of >= 64 chunks (S > 1008 B): a 64-lane wave
+// then spans at most two groups, A and B = A + 1.  Both groups' presence masks
+// and descriptors are fetched with scalar loads (wave-uniform addresses), and
+// each lane selects its group's words with v_cndmask.  This removes the
+// per-lane mask -> descriptor -> data dependent vector-load chain of k_apply
+// and the per-lane descriptor loads.
+template <int DMAX, int MODE, int NT>
+__global__ __launch_bounds__(256) void k_apply_w(Batch a) {
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  if (wfirst >= a.items) return;
+  const uint32_t wlast = min(wfirst + 63u, a.items - 1u);
+  const uint32_t gA = wfirst / a.chunks;
+  const uint32_t gB = wlast / a.chunks;  // gA or gA + 1
+  const uint8_t* dA = desc_for<MODE>(a, a.g0 + gA);
+  const uint8_t* dB = desc_for<MODE>(a, a.g0 + gB);
+  constexpr int NW = (DMAX + 3) / 4;
+  const uint32_t hA = ld32(dA), hB = ld32(dB);
+  uint32_t rA[NW], rB[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    rA[w] = ld32(dA + 4 + 4 * w);
+    rB[w] = ld32(dB + 4 + 4 * w);
+  }
+  const uint32_t oA = ld32(dA + 4 + a.dpad), oB = ld32(dB + 4 + a.dpad);  // output rows (e <= 4)
+
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t gl = item / a.chunks;
+  const bool inB = gl != gA;
+  const uint32_t c = item - gl * a.chunks;
+  const uint64_t g = a.g0 + gl;
+  const uint32_t hdr = inB ? hB : hA;
+  const uint32_t st = (hdr >> 16) & 0xffu;
+  if (MODE != 0 && a.status != nullptr && c == 0) a.status[g] = static_cast<int8_t>(st);
+  const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
+  if (st != 0 || e == 0) return;
+  uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
+  V4 x[DMAX];
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    if (k < static_cast<int>(a.d)) {
+      const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
+      const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
+      x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
+    } else {
+      x[k] = V4{{0u, 0u, 0u, 0u}};
+    }
+  }
+  const uint32_t nb = a.S - c * 16u;
+  const uint32_t orows = inB ? oB : oA;
+  const uint32_t cbase = 4 + a.dpad + a.epad;
+  for (uint32_t i = 0; i < e; ++i) {
+    uint32_t cw[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const uint32_t ca = ld32(dA + cbase + i * a.dpad + 4 * w);
+      const uint32_t cb = ld32(dB + cbase + i * a.dpad + 4 * w);
+      cw[w] = inB ? cb : ca;
+    }
+    const V4 y = horner_var<DMAX>(x, cw);
+    const uint32_t r = (orows >> (8 * i)) & 0xffu;
+    store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, y, nb);
+  }
+}
+
 // generic: any alignment / stride / d (<= 255); 4 columns per lane, byte I/O
 __device__ __forceinline__ uint32_t gfmul_var(uint32_t cbyte, uint32_t x) {
   uint32_t t = 0;
@@ -519,17 +584,27 @@ hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// k_apply_w needs a wave to span <= 2 groups (>= 64 chunks per row) and all
+// output rows in one descriptor dword (p <= 4); k_apply covers the rest.
+template <int DMAX, int MODE>
+static void launch_apply_dm(const Batch& a, hipStream_t s) {
+  const dim3 grid(blocks_for(a.items, 256)), block(256);
+  if (a.chunks >= 64 && a.epad == 4)
+    hipLaunchKernelGGL((k_apply_w<DMAX, MODE, kApplyNT>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((k_apply<DMAX, MODE, kApplyNT>), grid, block, 0, s, a);
+}
+
 template <int MODE>
 static hipError_t launch_apply_mode(int dmax, const Batch& a, hipStream_t s) {
-  const dim3 grid(blocks_for(a.items, 256)), block(256);
   switch (dmax) {
-    case 4: hipLaunchKernelGGL((k_apply<4, MODE, kApplyNT>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_apply<8, MODE, kApplyNT>), grid, block, 0, s, a); break;
-    case 10: hipLaunchKernelGGL((k_apply<10, MODE, kApplyNT>), grid, block, 0, s, a); break;
-    case 12: hipLaunchKernelGGL((k_apply<12, MODE, kApplyNT>), grid, block, 0, s, a); break;
-    case 16: hipLaunchKernelGGL((k_apply<16, MODE, kApplyNT>), grid, block, 0, s, a); break;
-    case 24: hipLaunchKernelGGL((k_apply<24, MODE, kApplyNT>), grid, block, 0, s, a); break;
-    case 32: hipLaunchKernelGGL((k_apply<32, MODE, kApplyNT>), grid, block, 0, s, a); break;
+    case 4: launch_apply_dm<4, MODE>(a, s); break;
+    case 8: launch_apply_dm<8, MODE>(a, s); break;
+    case 10: launch_apply_dm<10, MODE>(a, s); break;
+    case 12: launch_apply_dm<12, MODE>(a, s); break;
+    case 16: launch_apply_dm<16, MODE>(a, s); break;
+    case 24: launch_apply_dm<24, MODE>(a, s); break;
+    case 32: launch_apply_dm<32, MODE>(a, s); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
