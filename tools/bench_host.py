@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""Host-buffer (PCIe-inclusive) and jumbo-geometry measurements for DESIGN.md.
+
+BASELINE configs[4]: (32+8)x9000 B groups, mixed erasure patterns
+(e uniform in 0..8, positions uniform among the 40 shards), timed with the
+pinned hipMemcpyAsync H2D/D2H included.  The same host path is also measured
+for the (10+3)x1350 geometry, and the jumbo geometry device-resident.
+
+The host path is ugo_fec_encode_host / ugo_fec_reconstruct_host: the engine
+chunks the batch over 3 internal streams (H2D -> kernel -> D2H per chunk).
+Bytes reported are the algorithmic bytes of BASELINE.md ((d+p)*S encode,
+(d+e)*S reconstruct); "pcie_bytes" counts what actually crosses the link.
+Prints one JSON object per measurement.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from ugo_amd import fec  # noqa: E402
+
+
+def masks_mixed(G, n, emax, rng):
+    m = np.full(G, (1 << n) - 1, np.uint64)
+    es = rng.integers(0, emax + 1, G)
+    for g in range(G):
+        for r in rng.choice(n, int(es[g]), replace=False):
+            m[g] &= ~np.uint64(1 << int(r))
+    return m, es
+
+
+def host_case(d, p, S, G, emax, reps, pinned=True):
+    n = d + p
+    pitch = (S + 15) // 16 * 16
+    enc = fec.New(d, p)
+    nbytes = G * n * pitch
+    rng = np.random.default_rng(7)
+    if pinned:
+        raw = fec.host_alloc(nbytes)
+        arr = raw.reshape(G, n, pitch)
+    else:
+        arr = np.empty((G, n, pitch), np.uint8)
+    arr[:] = rng.integers(0, 256, (G, n, pitch), dtype=np.uint8)
+    masks, es = masks_mixed(G, n, emax, rng)
+    enc.encode_host(arr, S)  # warm up (allocates staging)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        enc.encode_host(arr, S)
+    t_enc = (time.perf_counter() - t0) / reps
+    keep = arr.copy()
+    st = np.zeros(G, np.int8)
+    enc.reconstruct_host(arr, masks, S, status=st)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        enc.reconstruct_host(arr, masks, S, status=st)
+    t_dec = (time.perf_counter() - t0) / reps
+    ok = bool(np.array_equal(arr[:, :, :S], keep[:, :, :S])) and not st.any()
+    alg_enc = G * n * S
+    alg_dec = int(sum(d + int(e) for e in es) * S)
+    out = [
+        {"case": f"host encode ({d}+{p})x{S}", "groups": G, "pinned": pinned, "ms": t_enc * 1e3,
+         "alg_GBps": alg_enc / t_enc / 1e9, "pcie_bytes": G * (d * pitch + p * S),
+         "pcie_GBps": G * (d * pitch + p * S) / t_enc / 1e9},
+        {"case": f"host reconstruct ({d}+{p})x{S} e~U[0,{emax}]", "groups": G, "pinned": pinned,
+         "ms": t_dec * 1e3, "alg_GBps": alg_dec / t_dec / 1e9, "pcie_bytes": 2 * G * n * pitch + 9 * G,
+         "pcie_GBps": (2 * G * n * pitch + 9 * G) / t_dec / 1e9, "round_trip_ok": ok},
+    ]
+    if pinned:
+        fec.host_free(raw)
+    return out
+
+
+def device_case(d, p, S, G, emax, reps):
+    n = d + p
+    pitch = (S + 15) // 16 * 16
+    enc = fec.New(d, p)
+    sh = torch.randint(0, 256, (n, G, pitch), dtype=torch.uint8, device="cuda")
+    rng = np.random.default_rng(9)
+    masks, es = masks_mixed(G, n, emax, rng)
+    dm = torch.as_tensor(masks.view(np.int64)).cuda()
+    s = torch.cuda.current_stream()
+    for _ in range(2):
+        enc.encode_batch(sh, S, shard_major=True)
+        enc.reconstruct_batch(sh, dm, S, shard_major=True)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    e[0].record(s)
+    for _ in range(reps):
+        enc.encode_batch(sh, S, shard_major=True)
+    e[1].record(s)
+    for _ in range(reps):
+        enc.reconstruct_batch(sh, dm, S, shard_major=True)
+    e[2].record(s)
+    torch.cuda.synchronize()
+    te = e[0].elapsed_time(e[1]) / reps * 1e-3
+    td = e[1].elapsed_time(e[2]) / reps * 1e-3
+    alg_dec = int(sum(d + int(x) for x in es) * S)
+    return [{"case": f"device encode ({d}+{p})x{S}", "groups": G, "us": te * 1e6, "alg_GBps": G * n * S / te / 1e9},
+            {"case": f"device reconstruct ({d}+{p})x{S} e~U[0,{emax}]", "groups": G, "us": td * 1e6,
+             "alg_GBps": alg_dec / td / 1e9}]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    res = []
+    res += device_case(32, 8, 9000, 8192, 8, args.reps)
+    res += host_case(32, 8, 9000, 8192, 8, args.reps, pinned=True)
+    res += host_case(10, 3, 1350, 65536, 3, args.reps, pinned=True)
+    res += host_case(10, 3, 1350, 65536, 3, 2, pinned=False)
+    for r in res:
+        print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
+
+
+if __name__ == "__main__":
+    main()
