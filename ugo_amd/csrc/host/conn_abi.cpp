@@ -1,0 +1,111 @@
+// conn_abi.cpp -- C-ABI (include/ugo_fec_conn.h) over the C++ FEC mirror.
+#include "../../../include/ugo_fec_conn.h"
+
+#include <cstring>
+#include <new>
+
+#include "fec.hpp"
+
+struct ugo_fecconn {
+  std::unique_ptr<ugo::FEC> fec;
+};
+
+extern "C" {
+
+int ugo_fecconn_new(int rxlimit, int d, int p, int device, ugo_fecconn** out) {
+  if (!out) return UGO_FEC_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (d <= 0 || p <= 0 || rxlimit < d + p) return UGO_FEC_ERR_INV_SHARD_NUM;  // newFEC -> nil
+  // probe reedsolomon.New's status for a precise error before constructing
+  ugo_fec* probe = nullptr;
+  const int st = ugo_fec_create(device, d, p, &probe);
+  if (st != UGO_FEC_OK) return st;
+  ugo_fec_destroy(probe);
+  auto* c = new (std::nothrow) ugo_fecconn();
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  c->fec = ugo::FEC::newFEC(rxlimit, d, p, device);
+  if (!c->fec) {
+    delete c;
+    return UGO_FEC_ERR_HIP;
+  }
+  *out = c;
+  return UGO_FEC_OK;
+}
+
+void ugo_fecconn_free(ugo_fecconn* f) { delete f; }
+
+int ugo_fecconn_set_clock(ugo_fecconn* f, uint32_t (*clock)(void*), void* user) {
+  if (!f) return UGO_FEC_ERR_INVALID_ARG;
+  if (clock)
+    f->fec->setClock([clock, user]() { return clock(user); });
+  else
+    f->fec->setClock(ugo::currentMs);
+  return UGO_FEC_OK;
+}
+
+int ugo_fecconn_mark_data(ugo_fecconn* f, uint8_t* data) {
+  if (!f || !data) return UGO_FEC_ERR_INVALID_ARG;
+  f->fec->markData(data);
+  return UGO_FEC_OK;
+}
+
+int ugo_fecconn_mark_fec(ugo_fecconn* f, uint8_t* data) {
+  if (!f || !data) return UGO_FEC_ERR_INVALID_ARG;
+  f->fec->markFEC(data);
+  return UGO_FEC_OK;
+}
+
+int ugo_fecconn_get_next(const ugo_fecconn* f, uint32_t* next) {
+  if (!f || !next) return UGO_FEC_ERR_INVALID_ARG;
+  *next = f->fec->next();
+  return UGO_FEC_OK;
+}
+
+int ugo_fecconn_set_next(ugo_fecconn* f, uint32_t next) {
+  if (!f) return UGO_FEC_ERR_INVALID_ARG;
+  f->fec->setNext(next);
+  return UGO_FEC_OK;
+}
+
+int ugo_fecconn_input(ugo_fecconn* f, const uint8_t* wire, size_t len, uint32_t* seqid, uint16_t* flag,
+                      uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len) {
+  if (!f || !wire || len < ugo::fecHeaderSize) return UGO_FEC_ERR_INVALID_ARG;
+  if (nrec) *nrec = 0;
+  if (rec_len) *rec_len = 0;
+  ugo::fecPacket pkt = f->fec->decode(wire, len);
+  if (seqid) *seqid = pkt.seqid;
+  if (flag) *flag = pkt.flag;
+  if (pkt.flag != ugo::typeData && pkt.flag != ugo::typeFEC) {
+    // ugo/conn.go:395: such a packet never reaches input(); its pool buffer
+    // is dropped (never Put back), as in Go
+    f->fec->dropBuffer(pkt.data);
+    return UGO_FEC_OK;
+  }
+  std::vector<ugo::Bytes> rec = f->fec->input(pkt);
+  if (!rec.empty()) {
+    const size_t L = rec[0].size();
+    if (!out || out_cap < rec.size() * ugo::maxPacketSize || L > ugo::maxPacketSize) return UGO_FEC_ERR_INVALID_ARG;
+    for (size_t i = 0; i < rec.size(); ++i) std::memcpy(out + i * ugo::maxPacketSize, rec[i].data(), L);
+    if (nrec) *nrec = static_cast<int>(rec.size());
+    if (rec_len) *rec_len = L;
+  }
+  return f->fec->lastError() == UGO_FEC_ERR_HIP ? UGO_FEC_ERR_HIP : UGO_FEC_OK;
+}
+
+int ugo_fecconn_calc_ecc(ugo_fecconn* f, uint8_t* const* bufs, const size_t* lens, int n, int offset, int maxlen) {
+  if (!f || !bufs || !lens || n < 0) return UGO_FEC_ERR_INVALID_ARG;
+  std::vector<ugo::Bytes> data(n);
+  for (int k = 0; k < n; ++k) data[k].assign(bufs[k], bufs[k] + lens[k]);
+  auto ecc = f->fec->calcECC(data, offset, maxlen);
+  if (ecc.empty()) return f->fec->lastError() ? f->fec->lastError() : UGO_FEC_ERR_INVALID_ARG;
+  for (int k = f->fec->dataShards(); k < n; ++k) std::memcpy(bufs[k], data[k].data(), lens[k]);
+  return UGO_FEC_OK;
+}
+
+int ugo_fecconn_rx_len(const ugo_fecconn* f, size_t* len) {
+  if (!f || !len) return UGO_FEC_ERR_INVALID_ARG;
+  *len = f->fec->rxLen();
+  return UGO_FEC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,188 @@
+// fec.cpp -- see fec.hpp.  Control logic mirrors ugo/fec.go line by line in
+// behaviour; every byte of Reed-Solomon arithmetic runs on the GPU through
+// reedsolomon::Encoder (the C-ABI), none on the CPU.
+#include "fec.hpp"
+
+#include <chrono>
+#include <cstring>
+
+namespace ugo {
+
+uint32_t currentMs() {  // ugo/fec.go:73-75
+  using namespace std::chrono;
+  return static_cast<uint32_t>(duration_cast<milliseconds>(system_clock::now().time_since_epoch()).count());
+}
+
+static inline void putLE32(uint8_t* p, uint32_t v) {
+  p[0] = uint8_t(v); p[1] = uint8_t(v >> 8); p[2] = uint8_t(v >> 16); p[3] = uint8_t(v >> 24);
+}
+static inline void putLE16(uint8_t* p, uint16_t v) { p[0] = uint8_t(v); p[1] = uint8_t(v >> 8); }
+static inline uint32_t getLE32(const uint8_t* p) {
+  return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+static inline uint16_t getLE16(const uint8_t* p) { return uint16_t(p[0] | p[1] << 8); }
+
+std::unique_ptr<FEC> FEC::newFEC(int rxlimit, int dataShards, int parityShards, int device) {
+  if (dataShards <= 0 || parityShards <= 0) return nullptr;  // :46-48
+  if (rxlimit < dataShards + parityShards) return nullptr;  // :49-51
+  std::unique_ptr<FEC> f(new FEC());
+  f->rxlimit_ = rxlimit;
+  f->dataShards_ = dataShards;
+  f->parityShards_ = parityShards;
+  f->shardSize_ = dataShards + parityShards;
+  f->paws_ = (0xffffffffu / uint32_t(f->shardSize_) - 1) * uint32_t(f->shardSize_);  // :58
+  int err = 0;
+  f->enc_ = reedsolomon::New(dataShards, parityShards, &err, device);  // :59
+  if (!f->enc_) return nullptr;  // :60-63 (logged upstream)
+  f->clock_ = currentMs;
+  return f;
+}
+
+Bytes* FEC::poolGet() {
+  if (!poolFree_.empty()) {
+    Bytes* b = poolFree_.back();
+    poolFree_.pop_back();
+    return b;
+  }
+  poolAll_.push_back(std::make_unique<Bytes>(maxPacketSize, 0));
+  return poolAll_.back().get();
+}
+
+void FEC::poolPut(Bytes* b) { poolFree_.push_back(b); }
+
+void FEC::dropBuffer(Bytes* b) {
+  for (size_t i = poolAll_.size(); i-- > 0;)
+    if (poolAll_[i].get() == b) {
+      poolAll_.erase(poolAll_.begin() + static_cast<long>(i));
+      return;
+    }
+}
+
+fecPacket FEC::decode(const uint8_t* data, size_t len) {  // :78-89
+  fecPacket pkt;
+  pkt.seqid = getLE32(data);
+  pkt.flag = getLE16(data + 4);
+  pkt.ts = clock_();
+  Bytes* buf = poolGet();
+  const size_t n = len > fecHeaderSize ? std::min(buf->size(), len - fecHeaderSize) : 0;
+  if (n) std::memcpy(buf->data(), data + fecHeaderSize, n);  // copy(buf, data[6:]); stale tail kept
+  pkt.data = buf;
+  return pkt;
+}
+
+void FEC::markData(uint8_t* data) {  // :91-95
+  putLE32(data, next_);
+  putLE16(data + 4, typeData);
+  next_++;
+}
+
+void FEC::markFEC(uint8_t* data) {  // :97-104
+  putLE32(data, next_);
+  putLE16(data + 4, typeFEC);
+  next_++;
+  if (next_ >= paws_) next_ = 0;
+}
+
+std::vector<Bytes> FEC::input(fecPacket pkt) {  // :107-226
+  std::vector<Bytes> recovered;
+  const uint32_t now = clock_();
+  if (now - lastCheck_ >= fecExpire) {  // expiration :109-121
+    std::vector<fecPacket> keep;
+    for (auto& q : rx_) {
+      if (now - q.ts < fecExpire)
+        keep.push_back(q);
+      else
+        poolPut(q.data);
+    }
+    rx_.swap(keep);
+    lastCheck_ = now;
+  }
+  // insertion :124-143
+  const int n = static_cast<int>(rx_.size()) - 1;
+  int insertIdx = 0;
+  for (int i = n; i >= 0; --i) {
+    if (pkt.seqid == rx_[i].seqid) {  // de-duplicate
+      poolPut(pkt.data);
+      return recovered;
+    } else if (pkt.seqid > rx_[i].seqid) {
+      insertIdx = i + 1;
+      break;
+    }
+  }
+  rx_.insert(rx_.begin() + insertIdx, pkt);
+
+  const uint32_t ss = uint32_t(shardSize_);
+  const uint32_t shardBegin = pkt.seqid - pkt.seqid % ss;  // :145-146
+  const uint32_t shardEnd = shardBegin + ss - 1;
+  int searchBegin = insertIdx - shardSize_;
+  if (searchBegin < 0) searchBegin = 0;
+  int searchEnd = insertIdx + shardSize_;
+  if (searchEnd >= static_cast<int>(rx_.size())) searchEnd = static_cast<int>(rx_.size()) - 1;
+
+  if (static_cast<int>(rx_.size()) >= dataShards_ && shardBegin < shardEnd) {  // :158
+    int numshard = 0, numDataShard = 0, first = -1;
+    size_t maxlen = 0;
+    std::vector<Bytes*> shards(shardSize_, nullptr);
+    std::vector<bool> shardsflag(shardSize_, false);
+    for (int i = searchBegin; i <= searchEnd; ++i) {  // :170-188
+      const uint32_t seqid = rx_[i].seqid;
+      if (seqid > shardEnd) break;
+      if (seqid >= shardBegin) {
+        shards[seqid % ss] = rx_[i].data;
+        shardsflag[seqid % ss] = true;
+        numshard++;
+        if (rx_[i].flag == typeData) numDataShard++;
+        if (numshard == 1) first = i;
+        if (rx_[i].data->size() > maxlen) maxlen = rx_[i].data->size();
+      }
+    }
+    if (numDataShard == dataShards_) {  // no loss :190-195
+      for (int i = first; i < first + numshard; ++i) poolPut(rx_[i].data);
+      rx_.erase(rx_.begin() + first, rx_.begin() + first + numshard);
+    } else if (numshard >= dataShards_) {  // recoverable :196-217
+      std::vector<Bytes> rs(shardSize_);
+      for (int k = 0; k < shardSize_; ++k)
+        if (shards[k]) rs[k].assign(shards[k]->begin(), shards[k]->begin() + maxlen);  // shards[k][:maxlen]
+      const int err = enc_->Reconstruct(rs);  // :202 -> GPU
+      lastError_ = err;
+      if (err == UGO_FEC_OK) {
+        for (int k = 0; k < dataShards_; ++k)
+          if (!shardsflag[k]) recovered.push_back(std::move(rs[k]));
+      }  // else: logged and swallowed upstream (:208-210)
+      for (int i = first; i < first + numshard; ++i) poolPut(rx_[i].data);
+      rx_.erase(rx_.begin() + first, rx_.begin() + first + numshard);
+    }
+  }
+  if (static_cast<int>(rx_.size()) > rxlimit_) {  // keep rxlimit :220-224
+    poolPut(rx_.front().data);
+    rx_.erase(rx_.begin());
+  }
+  return recovered;
+}
+
+std::vector<Bytes*> FEC::calcECC(std::vector<Bytes>& data, int offset, int maxlen) {  // :228-243
+  std::vector<Bytes*> ecc;
+  if (static_cast<int>(data.size()) != shardSize_) {
+    lastError_ = UGO_FEC_ERR_INVALID_ARG;  // "mismatch" logged upstream
+    return ecc;
+  }
+  if (offset < 0 || maxlen < offset) {  // Go: slice bounds panic
+    lastError_ = UGO_FEC_ERR_INVALID_ARG;
+    return ecc;
+  }
+  std::vector<uint8_t*> rows(shardSize_);
+  for (int k = 0; k < shardSize_; ++k) {
+    if (static_cast<int>(data[k].size()) < maxlen) {  // Go: slice bounds panic
+      lastError_ = UGO_FEC_ERR_INVALID_ARG;
+      return ecc;
+    }
+    rows[k] = data[k].data() + offset;
+  }
+  const int err = enc_->EncodeWindows(rows.data(), size_t(maxlen - offset));  // :238 -> GPU
+  lastError_ = err;
+  if (err != UGO_FEC_OK) return ecc;
+  for (int k = dataShards_; k < shardSize_; ++k) ecc.push_back(&data[k]);
+  return ecc;
+}
+
+}  // namespace ugo

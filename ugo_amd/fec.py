@@ -38,6 +38,7 @@ except Exception:  # pragma: no cover - torch is optional for the host-only path
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libugofec.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ugo_fec.h")
+CONN_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ugo_fec_conn.h")
 
 OK = 0
 RECONSTRUCT_DATA_ONLY = 1
@@ -119,11 +120,14 @@ def load_library(path: str = LIB_PATH):
     return lib
 
 
-def header_symbols(path: str = HEADER_PATH) -> List[str]:
-    """Every entry point declared in include/ugo_fec.h."""
-    src = open(path).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(ugo_fec_[a-z0-9_]+)\s*\(", src)))
+def header_symbols(paths=(HEADER_PATH, CONN_HEADER_PATH)) -> List[str]:
+    """Every entry point declared in include/ugo_fec.h and include/ugo_fec_conn.h."""
+    out = set()
+    for path in paths:
+        src = open(path).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        out |= set(re.findall(r"\b(ugo_fec(?:conn)?_[a-z0-9_]+)\s*\(", src))
+    return sorted(out)
 
 
 def strerror(code: int) -> str:
@@ -299,3 +303,104 @@ def host_alloc(nbytes: int) -> np.ndarray:
 
 def host_free(arr: np.ndarray) -> None:
     _raise(load_library().ugo_fec_host_free(ctypes.c_void_p(arr.ctypes.data)))
+
+
+# ---------------------------------------------------------------- FEC object
+UGO_FEC_MAX_PACKET = 1476
+_CLOCK_T = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_void_p)
+
+
+def _bind_conn(lib):
+    if getattr(lib, "_conn_bound", False):
+        return lib
+    vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    lib.ugo_fecconn_new.argtypes = [i, i, i, i, ctypes.POINTER(vp)]
+    lib.ugo_fecconn_free.argtypes = [vp]
+    lib.ugo_fecconn_free.restype = None
+    lib.ugo_fecconn_set_clock.argtypes = [vp, _CLOCK_T, vp]
+    lib.ugo_fecconn_mark_data.argtypes = [vp, vp]
+    lib.ugo_fecconn_mark_fec.argtypes = [vp, vp]
+    lib.ugo_fecconn_get_next.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
+    lib.ugo_fecconn_set_next.argtypes = [vp, ctypes.c_uint32]
+    lib.ugo_fecconn_input.argtypes = [vp, vp, sz, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint16),
+                                      vp, sz, ctypes.POINTER(i), ctypes.POINTER(sz)]
+    lib.ugo_fecconn_calc_ecc.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(sz), i, i, i]
+    lib.ugo_fecconn_rx_len.argtypes = [vp, ctypes.POINTER(sz)]
+    lib._conn_bound = True
+    return lib
+
+
+class FecConn:
+    """ugo's per-connection FEC object (ugo/fec.go:14-27) as implemented by the
+    C++ host mirror (ugo_amd/csrc/host/fec.cpp) behind include/ugo_fec_conn.h."""
+
+    def __init__(self, rxlimit: int, data_shards: int, parity_shards: int, device: int = 0):
+        lib = _bind_conn(load_library())
+        h = ctypes.c_void_p()
+        _raise(lib.ugo_fecconn_new(rxlimit, data_shards, parity_shards, device, ctypes.byref(h)))
+        self._h, self._lib = h, lib
+        self.dataShards, self.parityShards = data_shards, parity_shards
+        self._clock_cb = None
+        self._out = (ctypes.c_uint8 * (data_shards * UGO_FEC_MAX_PACKET))()
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.ugo_fecconn_free(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_clock(self, fn):
+        """fn() -> uint32 milliseconds (replaces currentMs, ugo/fec.go:73)."""
+        self._clock_cb = _CLOCK_T(lambda _u: fn() & 0xFFFFFFFF)
+        _raise(self._lib.ugo_fecconn_set_clock(self._h, self._clock_cb, None))
+
+    def markData(self, buf: bytearray):
+        c = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
+        _raise(self._lib.ugo_fecconn_mark_data(self._h, ctypes.addressof(c)))
+
+    def markFEC(self, buf: bytearray):
+        c = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
+        _raise(self._lib.ugo_fecconn_mark_fec(self._h, ctypes.addressof(c)))
+
+    @property
+    def next(self) -> int:
+        v = ctypes.c_uint32()
+        _raise(self._lib.ugo_fecconn_get_next(self._h, ctypes.byref(v)))
+        return v.value
+
+    @next.setter
+    def next(self, v: int):
+        _raise(self._lib.ugo_fecconn_set_next(self._h, v))
+
+    def input(self, wire: bytes):
+        """decode + input (ugo/conn.go:394-396): returns (seqid, flag, recovered list | None)."""
+        seq, flag = ctypes.c_uint32(), ctypes.c_uint16()
+        nrec, rlen = ctypes.c_int(), ctypes.c_size_t()
+        w = (ctypes.c_uint8 * len(wire)).from_buffer_copy(wire)
+        _raise(self._lib.ugo_fecconn_input(self._h, ctypes.addressof(w), len(wire), ctypes.byref(seq),
+                                           ctypes.byref(flag), ctypes.addressof(self._out), len(self._out),
+                                           ctypes.byref(nrec), ctypes.byref(rlen)))
+        rec = None
+        if nrec.value:
+            raw = bytes(self._out)
+            rec = [bytearray(raw[i * UGO_FEC_MAX_PACKET: i * UGO_FEC_MAX_PACKET + rlen.value])
+                   for i in range(nrec.value)]
+        return seq.value, flag.value, rec
+
+    def calcECC(self, data: List[bytearray], offset: int, maxlen: int):
+        n = len(data)
+        arrs = [(ctypes.c_uint8 * len(b)).from_buffer(b) for b in data]
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.addressof(a) for a in arrs])
+        lens = (ctypes.c_size_t * n)(*[len(b) for b in data])
+        _raise(self._lib.ugo_fecconn_calc_ecc(self._h, ptrs, lens, n, offset, maxlen))
+        return data[self.dataShards:]
+
+    def rx_len(self) -> int:
+        v = ctypes.c_size_t()
+        _raise(self._lib.ugo_fecconn_rx_len(self._h, ctypes.byref(v)))
+        return v.value
