@@ -123,6 +123,31 @@ int ugo_fec_reconstruct_host(ugo_fec* ctx, uint8_t* shards, const uint64_t* pres
  * differs (or an empty one with nil_ok == 0).  Host-only, no device needed. */
 int ugo_fec_check_shards(int n, const size_t* lens, int nil_ok, size_t* shard_size);
 
+/* ---- RX group assembly ----------------------
+ * The batch form of what ugo does per packet before Reconstruct:
+ * Decrypt (ugo/conn.go:390: a fresh RC4 cipher per packet from a fixed key =
+ * XOR with one keystream prefix, `pad`), decode (ugo/fec.go:78-89: LE32 seqid,
+ * LE16 flag, payload data[6:]) and the group/slot choice of input
+ * (ugo/fec.go:145,175: group = seqid / (d+p), slot = seqid % (d+p)).
+ *   wire     device; packet i at wire + i*slot_stride (slot_stride % 16 == 0,
+ *            shards 16-B aligned), lens[i] bytes (device uint16).
+ *   pad      device keystream >= slot_stride bytes, or NULL (no decryption).
+ * A packet whose flag is typeData (0xf1) or typeFEC (0xf2) and whose group is
+ * in [first_group, first_group + groups) is written to row seqid % (d+p) of
+ * group seqid/(d+p) - first_group of the strided batch: its payload bytes
+ * [0, min(len-6, shard_size)) then zeros up to shard_size; bit row of
+ * present[group] is OR-ed (zero `present` before the first call of a batch).
+ * stats (device u32[4], nullable) counts accepted / bad-flag / out-of-window /
+ * too-short packets.  Then ugo_fec_reconstruct_strided recovers the batch. */
+int ugo_fec_rx_assemble(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, const uint16_t* lens,
+                        size_t npackets, const uint8_t* pad, uint64_t first_group, size_t groups,
+                        uint8_t* shards, size_t shard_size, size_t row_stride, size_t group_stride,
+                        uint64_t* present, uint32_t* stats, void* stream);
+
+/* RC4 keystream (crypto/rc4 KSA + PRGA) of a key, host memory: the pad above
+ * for ugo's fixed-key rc4StreamCrypto (ugo/crypto.go:14-39). */
+int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size_t n);
+
 /* ---- helpers ------------------------------------------------------------- */
 int ugo_fec_host_alloc(size_t bytes, void** out);  /* pinned host memory */
 int ugo_fec_host_free(void* p);

@@ -105,11 +105,67 @@ def device_case(d, p, S, G, emax, reps):
              "alg_GBps": alg_dec / td / 1e9}]
 
 
+def rx_case(G, loss, reps, encrypt=True):
+    """RX path device-resident: packets already in HBM (16-B slots of 1488 B),
+    RC4 pad XOR + header decode + planar placement (ugo_fec_rx_assemble), then
+    data-only Reconstruct of the batch.  Synthetic payloads (not codewords:
+    throughput only; parity is covered by tests/test_rx_batch.py)."""
+    d, p, n, S, pitch, slot = 10, 3, 13, 1470, 1472, 1488
+    enc = fec.New(d, p)
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    seq = torch.arange(G * n, device="cuda", dtype=torch.int64)
+    keep = torch.rand(G * n, device="cuda", generator=gen) >= loss
+    seq = seq[keep]
+    seq = seq[torch.randperm(seq.numel(), device="cuda", generator=gen)]
+    npk = seq.numel()
+    wire = torch.randint(0, 256, (npk, slot), dtype=torch.uint8, device="cuda", generator=gen)
+    hdr = torch.zeros((npk, 6), dtype=torch.uint8, device="cuda")
+    for b in range(4):
+        hdr[:, b] = ((seq >> (8 * b)) & 0xFF).to(torch.uint8)
+    hdr[:, 4] = torch.where(seq % n < d, 0xF1, 0xF2).to(torch.uint8)
+    pad = torch.frombuffer(bytearray(fec.rc4_keystream(b"1234567890123456", slot)), dtype=torch.uint8).cuda()
+    if encrypt:
+        hdr ^= pad[:6]
+    wire[:, :6] = hdr
+    lens = torch.full((npk,), 1476, dtype=torch.int16, device="cuda")
+    sh = torch.empty((n, G, pitch), dtype=torch.uint8, device="cuda")
+    present = torch.zeros(G, dtype=torch.int64, device="cuda")
+    st = torch.zeros(4, dtype=torch.int32, device="cuda")
+
+    def run():
+        present.zero_()
+        enc.rx_assemble(wire, lens, sh, present, shard_size=S, pad=pad if encrypt else None, stats=st)
+        enc.reconstruct_batch(sh, present, shard_size=S, data_only=True, shard_major=True)
+
+    run()
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    s = torch.cuda.current_stream()
+    e[0].record(s)
+    for _ in range(reps):
+        present.zero_()
+        enc.rx_assemble(wire, lens, sh, present, shard_size=S, pad=pad if encrypt else None, stats=st)
+    e[1].record(s)
+    for _ in range(reps):
+        enc.reconstruct_batch(sh, present, shard_size=S, data_only=True, shard_major=True)
+    e[2].record(s)
+    torch.cuda.synchronize()
+    ta = e[0].elapsed_time(e[1]) / reps * 1e-3
+    tr = e[1].elapsed_time(e[2]) / reps * 1e-3
+    asm_bytes = npk * (1476 + S)  # packet read + slot write
+    return [{"case": f"rx assemble (10+3) loss={loss} rc4={encrypt}", "groups": G, "packets": npk,
+             "us": ta * 1e6, "GBps": asm_bytes / ta / 1e9, "Mpkt_per_s": npk / ta / 1e6},
+            {"case": f"rx reconstruct data-only after assemble", "groups": G, "us": tr * 1e6,
+             "Mpkt_per_s_total": npk / (ta + tr) / 1e6}]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     res = []
+    res += rx_case(65536, 0.05, args.reps)
+    res += rx_case(65536, 0.05, args.reps, encrypt=False)
     res += device_case(32, 8, 9000, 8192, 8, args.reps)
     res += host_case(32, 8, 9000, 8192, 8, args.reps, pinned=True)
     res += host_case(10, 3, 1350, 65536, 3, args.reps, pinned=True)

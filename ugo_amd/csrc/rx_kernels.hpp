@@ -1,0 +1,30 @@
+// rx_kernels.hpp -- internal interface of the RX group-assembly kernel.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace ugo {
+namespace kern {
+
+struct RxArgs {
+  const uint8_t* wire;     // packet i at wire + i*slot (device, 16-B aligned slots)
+  const uint16_t* lens;    // packet lengths (device)
+  const uint8_t* pad;      // keystream XORed over each packet from byte 0, >= slot bytes, or null
+  uint8_t* shards;         // batch base (device)
+  uint64_t* present;       // per-group presence masks (device, OR-ed)
+  uint32_t* stats;         // accepted, bad flag, out of window, too short (device, nullable)
+  uint64_t npk;
+  uint64_t slot;
+  uint64_t first_group;
+  uint64_t groups;
+  uint64_t rstride;
+  uint64_t gstride;
+  uint32_t S;              // shard size (payload bytes kept per row)
+  uint32_t n;              // d + p
+};
+
+hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s);
+
+}  // namespace kern
+}  // namespace ugo

@@ -19,6 +19,8 @@
 
 #include "fec_kernels.hpp"
 #include "gf256.hpp"
+#include "host/rc4.hpp"
+#include "rx_kernels.hpp"
 
 namespace {
 
@@ -522,6 +524,45 @@ int ugo_fec_reconstruct_host(ugo_fec* c, uint8_t* shards, const uint64_t* presen
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
   return host_path(c, shards, present, groups, S, pitch, true, flags, status);
+}
+
+int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
+                        const uint8_t* pad, uint64_t first_group, size_t groups, uint8_t* shards, size_t S,
+                        size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats,
+                        void* stream) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
+  if (npk == 0) return UGO_FEC_OK;
+  if (!wire || !lens || !shards || !present || groups == 0 || c->n > 64) return UGO_FEC_ERR_INVALID_ARG;
+  if (slot_stride % 16 || slot_stride < 16 || reinterpret_cast<uintptr_t>(wire) % 16 ||
+      reinterpret_cast<uintptr_t>(shards) % 16 || row_stride % 16 || group_stride % 16 ||
+      (pad && reinterpret_cast<uintptr_t>(pad) % 16) || S > 0xffffffffu)
+    return UGO_FEC_ERR_INVALID_ARG;
+  if ((c->n > 1 && row_stride < S) || (groups > 1 && group_stride < S)) return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  ugo::kern::RxArgs a{};
+  a.wire = wire;
+  a.lens = lens;
+  a.pad = pad;
+  a.shards = shards;
+  a.present = present;
+  a.stats = stats;
+  a.npk = npk;
+  a.slot = slot_stride;
+  a.first_group = first_group;
+  a.groups = groups;
+  a.rstride = row_stride;
+  a.gstride = group_stride;
+  a.S = static_cast<uint32_t>(S);
+  a.n = static_cast<uint32_t>(c->n);
+  return hip_status(ugo::kern::launch_rx_scatter(a, static_cast<hipStream_t>(stream)));
+}
+
+int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size_t n) {
+  if (!key || key_len == 0 || key_len > 256 || (n && !out)) return UGO_FEC_ERR_INVALID_ARG;
+  ugo::rc4_keystream(key, key_len, out, n);
+  return UGO_FEC_OK;
 }
 
 int ugo_fec_host_alloc(size_t bytes, void** out) {

@@ -116,6 +116,8 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_strerror.argtypes = [i]
     lib.ugo_fec_strerror.restype = ctypes.c_char_p
     lib.ugo_fec_abi_version.argtypes = []
+    lib.ugo_fec_rx_assemble.argtypes = [vp, vp, sz, vp, sz, vp, ctypes.c_uint64, sz, vp, sz, sz, sz, vp, vp, vp]
+    lib.ugo_fec_rc4_keystream.argtypes = [vp, sz, vp, sz]
     _lib = lib
     return lib
 
@@ -220,6 +222,21 @@ class Encoder:
                                                           gs, RECONSTRUCT_DATA_ONLY if data_only else 0, st,
                                                           _stream_handle(stream)))
 
+    def rx_assemble(self, wire, lens, shards, present, first_group: int = 0, shard_size: Optional[int] = None,
+                    pad=None, stats=None, stream=None, shard_major: bool = True):
+        """RX group assembly (include/ugo_fec.h ugo_fec_rx_assemble): wire = uint8 CUDA
+        tensor [npk, slot] of received packets, lens = int16/uint16 CUDA tensor [npk];
+        pad = uint8 CUDA keystream (>= slot bytes) or None; present = int64 CUDA [G]
+        (zeroed by the caller); stats = int32 CUDA [4] or None."""
+        G, pitch, rs, gs = self._geom(shards, shard_major)
+        npk, slot = wire.shape
+        assert wire.is_contiguous() and lens.is_contiguous() and lens.element_size() == 2 and lens.numel() == npk
+        S = pitch if shard_size is None else shard_size
+        _raise(load_library().ugo_fec_rx_assemble(
+            self._h, wire.data_ptr(), slot, lens.data_ptr(), npk, None if pad is None else pad.data_ptr(),
+            first_group, G, shards.data_ptr(), S, rs, gs, present.data_ptr(),
+            None if stats is None else stats.data_ptr(), _stream_handle(stream)))
+
     # ------------------------------------------------------ host-buffer batch
     def encode_host(self, shards: np.ndarray, shard_size: Optional[int] = None):
         assert shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"] and shards.ndim == 3
@@ -285,6 +302,14 @@ class Encoder:
 
     def ReconstructData(self, shards: list) -> None:
         self._reconstruct(shards, data_only=True)
+
+
+def rc4_keystream(key: bytes, n: int) -> bytes:
+    """RC4 keystream prefix (ugo/crypto.go's fixed-key per-packet cipher)."""
+    out = (ctypes.c_uint8 * n)()
+    k = (ctypes.c_uint8 * len(key)).from_buffer_copy(key)
+    _raise(load_library().ugo_fec_rc4_keystream(ctypes.addressof(k), len(key), ctypes.addressof(out), n))
+    return bytes(out)
 
 
 def New(data_shards: int, parity_shards: int, device: int = 0) -> Encoder:
