@@ -162,10 +162,15 @@ def rx_case(G, loss, reps, encrypt=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="")
     args = ap.parse_args()
     res = []
     res += rx_case(65536, 0.05, args.reps)
     res += rx_case(65536, 0.05, args.reps, encrypt=False)
+    if args.only == "rx":
+        for r in res:
+            print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
+        return
     res += device_case(32, 8, 9000, 8192, 8, args.reps)
     res += host_case(32, 8, 9000, 8192, 8, args.reps, pinned=True)
     res += host_case(10, 3, 1350, 65536, 3, args.reps, pinned=True)
