@@ -84,7 +84,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dtab, tab.size()));
   CK(hipMemcpy(dtab, tab.data(), tab.size(), hipMemcpyHostToDevice));
 
+  std::vector<uint8_t> hmul(256 * 32);
+  ugo::gf::perm_tables(hmul.data());
+  uint32_t* dmul;
+  CK(hipMalloc(&dmul, hmul.size()));
+  CK(hipMemcpy(dmul, hmul.data(), hmul.size(), hipMemcpyHostToDevice));
   Batch a{};
+  a.mult = dmul;
   a.base = buf; a.gstride = n * pitch; a.rstride = pitch; a.nmask = (1ull << n) - 1; a.S = S;
   a.chunks = 85; a.items = G * 85; a.desc = dtab; a.present = masks; a.desc_stride = stride; a.d = d;
   a.dpad = dpad; a.epad = epad;
@@ -114,8 +120,16 @@ int main(int argc, char** argv) {
     add(k_apply<10, 1, 0>, b, dec_bytes, "dec " + L + " nt0");
     add(k_apply<10, 1, 1>, b, dec_bytes, "dec " + L + " nt1");
     add(k_apply<10, 1, 3>, b, dec_bytes, "dec " + L + " nt3");
-    add(k_apply_w<10, 1, 3>, b, dec_bytes, "dec " + L + " nt3 wave-scalar-desc");
-    add(k_apply_w<10, 1, 1>, b, dec_bytes, "dec " + L + " nt1 wave-scalar-desc");
+    {
+      Batch b1 = b;
+      b1.pass = (b.items + 63u) / 64u * 64u;
+      add(k_apply_w<10, 1, 3, 1>, b1, dec_bytes, "dec " + L + " nt3 wave-scalar-desc cpt1");
+    }
+        add(k_apply_p<10, 1, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick");
+    add(k_apply_p<10, 1, 1, 1, 7>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick wpe7");
+    add(k_apply_p<10, 1, 1, 1, 8>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick wpe8");
+    add(k_apply_p<10, 1, 1, 2>, b, dec_bytes, "dec " + L + " nt1 perm-tables vector-tables");
+    add(k_apply_p<12, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables dmax12");
     Batch bf = b;
     bf.present = masks_fixed;
     add(k_apply<10, 1, 3>, bf, dec_bytes, "dec " + L + " nt3 fixed-pattern");
@@ -139,6 +153,30 @@ int main(int argc, char** argv) {
   pair(k_encode_c<10, 3, 3>, k_apply<10, 1, 3>, pl, "pair planar enc-nt3 dec-nt3");
   pair(k_encode_c<10, 3, 1>, k_apply<10, 1, 1>, pl, "pair planar enc-nt1 dec-nt1");
 
+  {  // k_apply_p must reproduce k_apply_w bit for bit (random masks, planar)
+    const uint32_t grid = (pl.items + 255) / 256;
+    Batch b1 = pl;
+    b1.pass = (pl.items + 63u) / 64u * 64u;
+    std::vector<uint8_t> h1(h.size()), h2(h.size());
+    hipLaunchKernelGGL((k_apply_w<10, 1, 3, 1>), dim3(grid), dim3(256), 0, 0, b1);
+    CK(hipMemcpy(h1.data(), buf, h.size(), hipMemcpyDeviceToHost));
+    CK(hipMemset(buf, 0x5a, h.size() / 2));
+    CK(hipMemcpy(buf, h1.data(), h.size(), hipMemcpyHostToDevice));
+    // clobber erased rows so the check sees fresh outputs
+    for (uint64_t g = 0; g < G; ++g)
+      for (int r = 0; r < n; ++r)
+        if (!(hm[g] >> r & 1)) CK(hipMemset(buf + r * pl.rstride + g * pl.gstride, 0xee, S));
+    hipLaunchKernelGGL((k_apply_p<10, 1, 3, 1>), dim3(grid), dim3(256), 0, 0, pl);
+    CK(hipMemcpy(h2.data(), buf, h.size(), hipMemcpyDeviceToHost));
+    printf("{\"check\":\"k_apply_p<1> == k_apply_w\",\"equal\":%s}\n", h1 == h2 ? "true" : "false");
+    for (uint64_t g = 0; g < G; ++g)
+      for (int r = 0; r < n; ++r)
+        if (!(hm[g] >> r & 1)) CK(hipMemset(buf + r * pl.rstride + g * pl.gstride, 0xee, S));
+    hipLaunchKernelGGL((k_apply_p<10, 1, 3, 2>), dim3(grid), dim3(256), 0, 0, pl);
+    CK(hipMemcpy(h2.data(), buf, h.size(), hipMemcpyDeviceToHost));
+    printf("{\"check\":\"k_apply_p<2> == k_apply_w\",\"equal\":%s}\n", h1 == h2 ? "true" : "false");
+    fflush(stdout);
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

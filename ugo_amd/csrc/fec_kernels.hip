@@ -347,13 +347,169 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
 // each lane selects its group's words with v_cndmask.  This removes the
 // per-lane mask -> descriptor -> data dependent vector-load chain of k_apply
 // and the per-lane descriptor loads.
+//
+// CPT > 1: a thread owns CPT chunks `a.pass` items apart (a.pass % 64 == 0, so
+// every range is still wave-aligned); all CPT sets of survivor loads are
+// issued before the first chunk's arithmetic, so later chunks' data arrives
+// while earlier ones compute.
+template <int DMAX>
+struct WItem {
+  const uint8_t* dA;
+  const uint8_t* dB;
+  uint8_t* gp;
+  uint32_t nb, e, orows;
+  bool inB, live;
+  V4 x[DMAX];
+};
+
 template <int DMAX, int MODE, int NT>
-__global__ __launch_bounds__(256) void k_apply_w(Batch a) {
-  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+__device__ __forceinline__ void witem_issue(WItem<DMAX>& it, const Batch& a, uint32_t wfirst, uint32_t item) {
+  it.live = false;
   if (wfirst >= a.items) return;
   const uint32_t wlast = min(wfirst + 63u, a.items - 1u);
   const uint32_t gA = wfirst / a.chunks;
   const uint32_t gB = wlast / a.chunks;  // gA or gA + 1
+  it.dA = desc_for<MODE>(a, a.g0 + gA);
+  it.dB = desc_for<MODE>(a, a.g0 + gB);
+  constexpr int NW = (DMAX + 3) / 4;
+  const uint32_t hA = ld32(it.dA), hB = ld32(it.dB);
+  uint32_t rA[NW], rB[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    rA[w] = ld32(it.dA + 4 + 4 * w);
+    rB[w] = ld32(it.dB + 4 + 4 * w);
+  }
+  const uint32_t oA = ld32(it.dA + 4 + a.dpad), oB = ld32(it.dB + 4 + a.dpad);  // output rows (e <= 4)
+  if (item >= a.items) return;
+  const uint32_t gl = item / a.chunks;
+  it.inB = gl != gA;
+  const uint32_t c = item - gl * a.chunks;
+  const uint64_t g = a.g0 + gl;
+  const uint32_t hdr = it.inB ? hB : hA;
+  const uint32_t st = (hdr >> 16) & 0xffu;
+  if (MODE != 0 && a.status != nullptr && c == 0) a.status[g] = static_cast<int8_t>(st);
+  it.e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
+  if (st != 0 || it.e == 0) return;
+  it.live = true;
+  it.gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
+  it.nb = a.S - c * 16u;
+  it.orows = it.inB ? oB : oA;
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    if (k < static_cast<int>(a.d)) {
+      const uint32_t rw = it.inB ? rB[k >> 2] : rA[k >> 2];
+      const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
+      it.x[k] = load16<NT>(it.gp + static_cast<uint64_t>(r) * a.rstride);
+    } else {
+      it.x[k] = V4{{0u, 0u, 0u, 0u}};
+    }
+  }
+}
+
+template <int DMAX, int NT>
+__device__ __forceinline__ void witem_finish(const WItem<DMAX>& it, const Batch& a) {
+  if (!it.live) return;
+  constexpr int NW = (DMAX + 3) / 4;
+  const uint32_t cbase = 4 + a.dpad + a.epad;
+  for (uint32_t i = 0; i < it.e; ++i) {
+    uint32_t cw[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const uint32_t ca = ld32(it.dA + cbase + i * a.dpad + 4 * w);
+      const uint32_t cb = ld32(it.dB + cbase + i * a.dpad + 4 * w);
+      cw[w] = it.inB ? cb : ca;
+    }
+    const V4 y = horner_var<DMAX>(it.x, cw);
+    const uint32_t r = (it.orows >> (8 * i)) & 0xffu;
+    store16<NT>(it.gp + static_cast<uint64_t>(r) * a.rstride, y, it.nb);
+  }
+}
+
+template <int DMAX, int MODE, int NT, int CPT = 1>
+__global__ __launch_bounds__(256) void k_apply_w(Batch a) {
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  WItem<DMAX> it[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) witem_issue<DMAX, MODE, NT>(it[j], a, wfirst + j * a.pass, item + j * a.pass);
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) witem_finish<DMAX, NT>(it[j], a);
+}
+
+// Table form of the wave-scalar kernel.  The masked Horner of k_apply_w costs
+// 8 * (d + 4) ops per output dword (+ mask extraction); here each product
+// c * x is three v_perm_b32 lookups into 8-byte split tables of c
+// (gf::perm_tables): T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6].  The selector
+// bytes of an input are extracted once and shared by all outputs (inputs
+// outer, outputs inner, accumulators live), and a coefficient's five table
+// dwords come from the scalar cache (8 KiB table), selected per lane between
+// the wave's two groups.  Output rows beyond a group's e get coefficient 0
+// (zero tables) and are not stored.
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// TSEL: how a lane gets its group's tables when the wave spans groups A, B.
+//   0: wave-uniform (dA == dB), scalar loads only
+//   1: scalar loads of both, per-lane pick as arithmetic
+//   2: per-lane vector loads of the picked group's table (L1-resident)
+template <int DMAX, int TSEL>
+__device__ __forceinline__ void p_accum(V4* acc, const V4* x, const Batch& a, const uint8_t* dA,
+                                        const uint8_t* dB, uint32_t mB, uint32_t emax) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
+  const uint32_t cbase = 4 + a.dpad + a.epad;
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    if (k >= static_cast<int>(a.d)) continue;
+    uint32_t s0[4], s1[4], s2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s0[j] = x[k].v[j] & 0x07070707u;
+      s1[j] = (x[k].v[j] >> 3) & 0x07070707u;
+      s2[j] = (x[k].v[j] >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i >= static_cast<int>(emax)) continue;
+      const uint32_t off = cbase + i * a.dpad + (k & ~3);
+      const uint32_t cA = (ld32(dA + off) >> (8 * (k & 3))) & 0xffu;
+      const uint32_t* tA = a.mult + 8u * cA;
+      uint32_t t[5];
+      if constexpr (TSEL == 0) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) t[q] = tA[q];
+      } else {
+        const uint32_t cB = (ld32(dB + off) >> (8 * (k & 3))) & 0xffu;
+        const uint32_t* tB = a.mult + 8u * cB;
+        if constexpr (TSEL == 1) {
+#pragma unroll
+          for (int q = 0; q < 5; ++q) {  // arithmetic pick: a select would be folded
+            const uint32_t va = tA[q];   // into one per-lane vector load
+            const uint32_t vb = tB[q];
+            t[q] = va ^ ((va ^ vb) & mB);
+          }
+        } else {
+          const uint32_t* tp = mB ? tB : tA;
+#pragma unroll
+          for (int q = 0; q < 5; ++q) t[q] = tp[q];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i].v[j] = xor3(acc[i].v[j], perm(t[1], t[0], s0[j]), perm(t[3], t[2], s1[j])) ^ perm(0u, t[4], s2[j]);
+    }
+  }
+}
+
+template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_p(Batch a) {
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (wfirst >= a.items) return;
+  const uint32_t wlast = min(wfirst + 63u, a.items - 1u);
+  const uint32_t gA = wfirst / a.chunks;
+  const uint32_t gB = wlast / a.chunks;
   const uint8_t* dA = desc_for<MODE>(a, a.g0 + gA);
   const uint8_t* dB = desc_for<MODE>(a, a.g0 + gB);
   constexpr int NW = (DMAX + 3) / 4;
@@ -364,9 +520,12 @@ __global__ __launch_bounds__(256) void k_apply_w(Batch a) {
     rA[w] = ld32(dA + 4 + 4 * w);
     rB[w] = ld32(dB + 4 + 4 * w);
   }
-  const uint32_t oA = ld32(dA + 4 + a.dpad), oB = ld32(dB + 4 + a.dpad);  // output rows (e <= 4)
-
-  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t oA = ld32(dA + 4 + a.dpad), oB = ld32(dB + 4 + a.dpad);
+  // wave-uniform output count: the larger of the two groups' (a failed group
+  // contributes nothing: its lanes leave below)
+  const uint32_t eA = ((hA >> 16) & 0xffu) ? 0u : (a.data_only ? ((hA >> 8) & 0xffu) : (hA & 0xffu));
+  const uint32_t eB = ((hB >> 16) & 0xffu) ? 0u : (a.data_only ? ((hB >> 8) & 0xffu) : (hB & 0xffu));
+  const uint32_t emax = max(eA, eB);
   if (item >= a.items) return;
   const uint32_t gl = item / a.chunks;
   const bool inB = gl != gA;
@@ -374,10 +533,17 @@ __global__ __launch_bounds__(256) void k_apply_w(Batch a) {
   const uint64_t g = a.g0 + gl;
   const uint32_t hdr = inB ? hB : hA;
   const uint32_t st = (hdr >> 16) & 0xffu;
-  if (MODE != 0 && a.status != nullptr && c == 0) a.status[g] = static_cast<int8_t>(st);
-  const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
-  if (st != 0 || e == 0) return;
+  // (the status store comes last: a vector store ahead of the table reads
+  // would stop them being scalar loads)
+  const bool wst = MODE != 0 && a.status != nullptr && c == 0;
+  const uint32_t e = inB ? eB : eA;
+  if (e == 0) {
+    if (wst) a.status[g] = static_cast<int8_t>(st);
+    return;
+  }
+  const uint32_t mB = inB ? ~0u : 0u;
   uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
+  const uint32_t nb = a.S - c * 16u;
   V4 x[DMAX];
 #pragma unroll
   for (int k = 0; k < DMAX; ++k) {
@@ -385,25 +551,21 @@ __global__ __launch_bounds__(256) void k_apply_w(Batch a) {
       const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
       const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
       x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
-    } else {
-      x[k] = V4{{0u, 0u, 0u, 0u}};
     }
   }
-  const uint32_t nb = a.S - c * 16u;
+  V4 acc[4];
+  if (dA == dB)  // one descriptor for the whole wave: no per-lane table pick
+    p_accum<DMAX, 0>(acc, x, a, dA, dA, 0u, emax);
+  else
+    p_accum<DMAX, TSEL>(acc, x, a, dA, dB, mB, emax);
   const uint32_t orows = inB ? oB : oA;
-  const uint32_t cbase = 4 + a.dpad + a.epad;
-  for (uint32_t i = 0; i < e; ++i) {
-    uint32_t cw[NW];
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const uint32_t ca = ld32(dA + cbase + i * a.dpad + 4 * w);
-      const uint32_t cb = ld32(dB + cbase + i * a.dpad + 4 * w);
-      cw[w] = inB ? cb : ca;
-    }
-    const V4 y = horner_var<DMAX>(x, cw);
+  for (int i = 0; i < 4; ++i) {
+    if (i >= static_cast<int>(e)) continue;
     const uint32_t r = (orows >> (8 * i)) & 0xffu;
-    store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, y, nb);
+    store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, acc[i], nb);
   }
+  if (wst) a.status[g] = 0;
 }
 
 // generic: any alignment / stride / d (<= 255); 4 columns per lane, byte I/O
@@ -559,6 +721,7 @@ static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
 // Launch policy (tuned with tools/kvariants.hip on MI355X)
 constexpr int kEncNT = 1;    // nontemporal loads, plain stores
 constexpr int kApplyNT = 3;  // nontemporal loads and stores
+constexpr int kApplyPNT = 1; // k_apply_p: nontemporal loads, plain stores (-6% vs 3)
 
 int apply_dmax(int d) {
   if (d <= 4) return 4;
@@ -589,8 +752,17 @@ hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
 template <int DMAX, int MODE>
 static void launch_apply_dm(const Batch& a, hipStream_t s) {
   const dim3 grid(blocks_for(a.items, 256)), block(256);
-  if (a.chunks >= 64 && a.epad == 4)
-    hipLaunchKernelGGL((k_apply_w<DMAX, MODE, kApplyNT>), grid, block, 0, s, a);
+  if constexpr (DMAX <= 16) {
+    if (a.chunks >= 64 && a.epad == 4) {
+      hipLaunchKernelGGL((k_apply_p<DMAX, MODE, kApplyPNT, 1>), grid, block, 0, s, a);
+      return;
+    }
+  }
+  if (a.chunks >= 64 && a.epad == 4) {
+    Batch b = a;
+    b.pass = (a.items + 63u) / 64u * 64u;
+    hipLaunchKernelGGL((k_apply_w<DMAX, MODE, kApplyNT, 1>), grid, block, 0, s, b);
+  }
   else
     hipLaunchKernelGGL((k_apply<DMAX, MODE, kApplyNT>), grid, block, 0, s, a);
 }

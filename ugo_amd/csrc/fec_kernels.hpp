@@ -27,6 +27,8 @@ struct Batch {
   uint32_t dpad;
   uint32_t epad;
   uint32_t data_only;
+  uint32_t pass;            // k_apply_w with CPT > 1: item distance between a thread's chunks
+  const uint32_t* mult;     // gf::perm_tables (256 x 8 dwords, device) for k_apply_p
 };
 
 struct Prep {

@@ -100,6 +100,22 @@ constexpr bool build_matrix(int d, int p, uint8_t* m, uint8_t* scratch) {
 }
 
 // Compile-time matrix for the geometries the kernels specialise on.
+// Split multiplication tables for the v_perm_b32 kernels: for coefficient c,
+// 8 dwords at out + 32*c: T0[j] = c*j (j < 8), T1[j] = c*(j << 3) (j < 8),
+// T2[j] = c*(j << 6) (j < 4), packed little-endian (T0 lo/hi, T1 lo/hi, T2,
+// 3 zero dwords), so c*x = T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6].
+inline void perm_tables(uint8_t* out) {
+  for (int c = 0; c < 256; ++c) {
+    uint8_t* t = out + 32 * c;
+    for (int j = 0; j < 32; ++j) t[j] = 0;
+    for (int j = 0; j < 8; ++j) {
+      t[j] = mul(static_cast<uint8_t>(c), static_cast<uint8_t>(j));
+      t[8 + j] = mul(static_cast<uint8_t>(c), static_cast<uint8_t>(j << 3));
+    }
+    for (int j = 0; j < 4; ++j) t[16 + j] = mul(static_cast<uint8_t>(c), static_cast<uint8_t>(j << 6));
+  }
+}
+
 template <int D, int P>
 struct CodeMatrix {
   static constexpr int N = D + P;

@@ -51,7 +51,7 @@ struct ugo_fec {
   uint32_t dpad = 0, epad = 0, desc_stride = 0;
   int table_max = 16;       // d+p <= table_max -> host-built pattern table (MODE 1)
   uint8_t* d_M = nullptr;
-  uint8_t* d_gf = nullptr;  // exp[512] | log[256]
+  uint8_t* d_gf = nullptr;  // exp[512] | log[256] | pad | gf::perm_tables at +1024
   uint8_t* d_encdesc = nullptr;
   uint8_t* d_table = nullptr;
   uint8_t* d_work = nullptr;  // MODE 2 per-group descriptors
@@ -160,6 +160,7 @@ ugo::kern::Batch base_batch(const ugo_fec* c, uint8_t* shards, size_t S, const L
   a.d = static_cast<uint32_t>(c->d);
   a.dpad = c->dpad;
   a.epad = c->epad;
+  a.mult = reinterpret_cast<const uint32_t*>(c->d_gf + 1024);
   return a;
 }
 
@@ -420,9 +421,10 @@ int ugo_fec_create(int device, int data_shards, int parity_shards, ugo_fec** out
   if (hipMalloc(&c->d_M, c->M.size()) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
   if (hipMemcpy(c->d_M, c->M.data(), c->M.size(), hipMemcpyHostToDevice) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
   {
-    std::vector<uint8_t> gf(768);
+    std::vector<uint8_t> gf(1024 + 256 * 32, 0);  // exp | log | pad | perm tables
     std::memcpy(gf.data(), ugo::gf::kTables.exp, 512);
     std::memcpy(gf.data() + 512, ugo::gf::kTables.log, 256);
+    ugo::gf::perm_tables(gf.data() + 1024);
     if (hipMalloc(&c->d_gf, gf.size()) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
     if (hipMemcpy(c->d_gf, gf.data(), gf.size(), hipMemcpyHostToDevice) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
   }
