@@ -144,6 +144,27 @@ int ugo_fec_rx_assemble(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, c
                         uint8_t* shards, size_t shard_size, size_t row_stride, size_t group_stride,
                         uint64_t* present, uint32_t* stats, void* stream);
 
+/* TX group assembly for a batch of `groups` outgoing groups (device memory,
+ * stream-ordered, asynchronous) -- replaces the sender loop ugo/conn.go:643-685
+ * (markData, copy into the group buffers, calcECC(group, 6, maxsize),
+ * markFEC, ecc[k][:maxsize]) plus crypt.Encrypt (ugo/conn.go:634) per packet:
+ *   pkts:   data packet k of group g at pkts + (g*d + k)*slot_in, lens[g*d + k]
+ *           bytes (6-B header space first, as markData expects), 6..max_len;
+ *   wire:   wire packet r of group g (r < d data, then p parity) at
+ *           wire + (g*(d+p) + r)*slot_out, length wire_lens[g*(d+p) + r]:
+ *           header (LE32 seqid, LE16 0xf1 / 0xf2), payload or parity over the
+ *           window [6, maxsize) of zero-padded group buffers, XOR pad (when not
+ *           null: the fixed-key RC4 keystream, >= round_up(max_len, 16) bytes).
+ * Seqids run from first_seq (a multiple of d+p below paws, as FEC.next always
+ * is at a group boundary) and wrap at paws like markFEC.  A group with a
+ * length outside [6, max_len] gets status UGO_FEC_ERR_SHARD_SIZE and
+ * wire_lens 0.  slot_in, slot_out: multiples of 16, >= round_up(max_len, 16);
+ * d <= 32. */
+int ugo_fec_tx_assemble(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, const uint16_t* lens,
+                        size_t groups, uint32_t first_seq, const uint8_t* pad, size_t max_len,
+                        uint8_t* wire, size_t slot_out, uint16_t* wire_lens, int8_t* status,
+                        void* stream);
+
 /* RC4 keystream (crypto/rc4 KSA + PRGA) of a key, host memory: the pad above
  * for ugo's fixed-key rc4StreamCrypto (ugo/crypto.go:14-39). */
 int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size_t n);

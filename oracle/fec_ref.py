@@ -11,6 +11,9 @@ Only tests/ may import this module, as the checker for the C++ host mirror
   input      ugo/fec.go:107-226  expiry sweep, ordered insert + dedupe, group window
                                  search, no-loss release, Reconstruct, rxlimit trim
   calcECC    ugo/fec.go:228-243  Encode over data[k][offset:maxlen]
+  tx_group   ugo/conn.go:643-685 the sender loop (markData, copy, calcECC(.., 6,
+                                 maxsize), markFEC, ecc[k][:maxsize]) for one group,
+                                 then crypt.Encrypt (ugo/conn.go:634) per packet
 
 Go's sync.Pool (ugo/fec.go:26, :67-69) is modelled as a LIFO free list (the
 C++ mirror uses the same discipline), so stale-tail bytes are deterministic.
@@ -190,3 +193,29 @@ def handle(fec: FEC, wire: bytes):
     if pkt.flag in (typeData, typeFEC):
         rec = fec.input(pkt)
     return pkt.seqid, pkt.flag, rec
+
+
+def tx_group(fec: FEC, data_pkts, key=None, buf_size=maxPacketSize):
+    """One group of the sender loop ugo/conn.go:643-685 on FRESH, zero-filled
+    group buffers (the reference reuses its 13 buffers without clearing them, so
+    its parity bytes past a short packet's end depend on earlier groups; the
+    batch TX contract is the fresh-buffer result), followed by the fixed-key
+    RC4 encryption of every wire packet (ugo/conn.go:634, ugo/crypto.go:33-39).
+    Returns the d + p wire packets in send order."""
+    import rc4_ref
+    d, n = fec.dataShards, fec.shardSize
+    group = [bytearray(max(buf_size, max(len(x) for x in data_pkts))) for _ in range(n)]
+    out, maxsize = [], 0
+    for k, ori in enumerate(data_pkts):
+        ori = bytearray(ori)
+        fec.markData(ori)
+        group[k][:len(ori)] = ori
+        maxsize = max(maxsize, len(ori))
+        out.append(bytes(ori))
+    ecc = fec.calcECC(group, fecHeaderSize, maxsize)
+    for k in range(n - d):
+        fec.markFEC(ecc[k])
+        out.append(bytes(ecc[k][:maxsize]))
+    if key is not None:
+        out = [rc4_ref.xor_stream(key, w) for w in out]
+    return out

@@ -159,12 +159,52 @@ def rx_case(G, loss, reps, encrypt=True):
              "Mpkt_per_s_total": npk / (ta + tr) / 1e6}]
 
 
+def tx_case(G, reps, encrypt=True, full=True):
+    """TX path device-resident (ugo_fec_tx_assemble): G groups of 10 outgoing
+    data packets (16-B slots of 1488 B) -> headers + parity over [6, maxsize) +
+    RC4 pad XOR -> 13 wire packets per group.  Bytes = packet bytes read +
+    wire bytes written."""
+    d, p, n, slot = 10, 3, 13, 1488
+    enc = fec.New(d, p)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    pk = torch.randint(0, 256, (G * d, slot), dtype=torch.uint8, device="cuda", generator=gen)
+    if full:
+        lens = torch.full((G * d,), 1476, dtype=torch.int16, device="cuda")
+    else:
+        lens = torch.randint(6, 1477, (G * d,), dtype=torch.int16, device="cuda", generator=gen)
+    wire = torch.empty((G * n, slot), dtype=torch.uint8, device="cuda")
+    wl = torch.empty(G * n, dtype=torch.int16, device="cuda")
+    pad = torch.frombuffer(bytearray(fec.rc4_keystream(b"1234567890123456", slot)), dtype=torch.uint8).cuda()
+    run = lambda: enc.tx_assemble(pk, lens, wire, wl, pad=pad if encrypt else None)  # noqa: E731
+    run()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e[0].record(s)
+    for _ in range(reps):
+        run()
+    e[1].record(s)
+    torch.cuda.synchronize()
+    t = e[0].elapsed_time(e[1]) / reps * 1e-3
+    L = lens.to(torch.int64).view(G, d)
+    moved = int(2 * L.sum().item() + p * L.max(dim=1).values.sum().item())
+    return [{"case": f"tx assemble (10+3) full={full} rc4={encrypt}", "groups": G, "packets_out": G * n,
+             "us": t * 1e6, "GBps": moved / t / 1e9, "Mpkt_per_s": G * n / t / 1e6}]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     res = []
+    res += tx_case(65536, args.reps)
+    res += tx_case(65536, args.reps, full=False)
+    res += tx_case(65536, args.reps, encrypt=False)
+    if args.only == "tx":
+        for r in res:
+            print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
+        return
     res += rx_case(65536, 0.05, args.reps)
     res += rx_case(65536, 0.05, args.reps, encrypt=False)
     if args.only == "rx":

@@ -1,0 +1,223 @@
+// gf_device.hpp -- gfx950 device building blocks shared by the FEC kernels
+// (fec_kernels.hip) and the TX assembly kernel (tx_kernels.hip): packed
+// GF(2^8) xtime, bitop3 XOR forms, 16-byte loads/stores with cache policy,
+// and the compile-time coefficient networks (Horner over coefficient bits).
+// See fec_kernels.hip's header for the arithmetic.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "gf256.hpp"
+
+namespace ugo {
+namespace kern {
+
+// ---------------------------------------------------------------- helpers
+struct V4 {
+  uint32_t v[4];
+};
+
+__device__ __forceinline__ uint32_t xt1(uint32_t y) {
+  const uint32_t s8 = y << 8;
+  const uint32_t m = __builtin_amdgcn_perm(s8, y, 0x090b080au);
+  return ((y & 0x7f7f7f7fu) << 1) ^ (m & 0x1d1d1d1du);
+}
+
+__device__ __forceinline__ void xt4(V4& y) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y.v[j] = xt1(y.v[j]);
+}
+
+__device__ __forceinline__ void xor4(V4& y, const V4& x) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y.v[j] ^= x.v[j];
+}
+
+// v_bitop3_b32 truth tables (bit index = a*4 + b*2 + c)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c
+}
+__device__ __forceinline__ uint32_t xor_and(uint32_t y, uint32_t x, uint32_t m) {
+  return __builtin_amdgcn_bitop3_b32(y, x, m, 0x78);  // y ^ (x & m)
+}
+
+__device__ __forceinline__ void xor4_2(V4& y, const V4& a, const V4& b) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y.v[j] = xor3(y.v[j], a.v[j], b.v[j]);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// NT policy bits: 1 = nontemporal loads, 2 = nontemporal stores (streaming
+// data touched once; keeps it from displacing L2 / Infinity-Cache lines)
+template <int NT>
+__device__ __forceinline__ V4 load16(const uint8_t* p) {
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  u32x4 v;
+  if constexpr (NT & 1) {
+    v = __builtin_nontemporal_load(q);
+  } else {
+    v = *q;
+  }
+  return V4{{v.x, v.y, v.z, v.w}};
+}
+
+// store the first nb (1..16) bytes of a chunk
+template <int NT>
+__device__ __forceinline__ void store16(uint8_t* p, const V4& y, uint32_t nb) {
+  if (nb >= 16) {
+    const u32x4 v = {y.v[0], y.v[1], y.v[2], y.v[3]};
+    if constexpr (NT & 2) {
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    } else {
+      *reinterpret_cast<u32x4*>(p) = v;
+    }
+    return;
+  }
+  // tail chunk of a row whose length is not a multiple of 16 (rare lanes).
+  // No runtime indexing into y: that would demote it to scratch / LDS.
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t lo = 4u * j;
+    if (nb >= lo + 4) {
+      *reinterpret_cast<uint32_t*>(p + lo) = y.v[j];
+    } else if (nb > lo) {
+      const uint32_t w = y.v[j], rem = nb - lo;
+      p[lo] = static_cast<uint8_t>(w);
+      if (rem >= 2) p[lo + 1] = static_cast<uint8_t>(w >> 8);
+      if (rem >= 3) p[lo + 2] = static_cast<uint8_t>(w >> 16);
+    }
+  }
+}
+
+// ------------------------------------------------ compile-time coefficients
+template <int D, int P, int I, int B, int K>
+__device__ __forceinline__ constexpr bool cbit() {
+  return ((gf::Code<D, P>::M.at(D + I, K) >> B) & 1) != 0;
+}
+
+template <int D, int P, int I, int B, int... K>
+__device__ __forceinline__ constexpr bool any_bit(std::integer_sequence<int, K...>) {
+  return (cbit<D, P, I, B, K>() || ...);
+}
+
+template <int D, int P, int I, int B>
+__device__ __forceinline__ constexpr bool any_bit_at_or_above() {
+  if constexpr (B > 7) {
+    return false;
+  } else {
+    return any_bit<D, P, I, B>(std::make_integer_sequence<int, D>{}) ||
+           any_bit_at_or_above<D, P, I, B + 1>();
+  }
+}
+
+// The inputs whose coefficient has bit B set, for output I, as a compile-time list.
+template <int D, int P, int I, int B>
+struct Terms {
+  struct List {
+    int n;
+    int k[D];
+  };
+  static constexpr List make() {
+    List l{};
+    for (int k = 0; k < D; ++k)
+      if ((gf::Code<D, P>::M.at(D + I, k) >> B) & 1) l.k[l.n++] = k;
+    return l;
+  }
+  static constexpr List L = make();
+};
+
+// y ^= x[terms J..], two terms per v_bitop3 (3-input XOR)
+template <int D, int P, int I, int B, int J>
+__device__ __forceinline__ void cterms(V4& y, const V4* x) {
+  constexpr int n = Terms<D, P, I, B>::L.n;
+  if constexpr (J + 1 < n) {
+    constexpr int k0 = Terms<D, P, I, B>::L.k[J];
+    constexpr int k1 = Terms<D, P, I, B>::L.k[J + 1];
+    xor4_2(y, x[k0], x[k1]);
+    cterms<D, P, I, B, J + 2>(y, x);
+  } else if constexpr (J < n) {
+    constexpr int k0 = Terms<D, P, I, B>::L.k[J];
+    xor4(y, x[k0]);
+  }
+}
+
+// Horner step for bit B of output I (called for B = 7 .. 0)
+template <int D, int P, int I, int B>
+__device__ __forceinline__ void chorner(V4& y, const V4* x) {
+  constexpr int n = Terms<D, P, I, B>::L.n;
+  if constexpr (any_bit_at_or_above<D, P, I, B + 1>()) {
+    xt4(y);  // y *= 2
+    cterms<D, P, I, B, 0>(y, x);
+  } else if constexpr (n > 0) {
+    constexpr int k0 = Terms<D, P, I, B>::L.k[0];
+    y = x[k0];  // first non-zero bit plane: y was 0
+    cterms<D, P, I, B, 1>(y, x);
+  }
+  if constexpr (B > 0) chorner<D, P, I, B - 1>(y, x);
+}
+
+template <int D, int P, int I>
+__device__ __forceinline__ V4 cparity(const V4* x) {
+  V4 y{{0u, 0u, 0u, 0u}};
+  chorner<D, P, I, 7>(y, x);
+  return y;
+}
+
+// compute and store parity rows one at a time (short live ranges)
+template <int D, int P, int NT, int... I>
+__device__ __forceinline__ void cparity_store(uint8_t* gp, uint64_t pitch, uint32_t nb, const V4* x,
+                                              std::integer_sequence<int, I...>) {
+  ((store16<NT>(gp + static_cast<uint64_t>(D + I) * pitch, cparity<D, P, I>(x), nb)), ...);
+}
+
+// y = sum_k c_k * x_k over GF(2^8) with per-lane coefficients: Horner over the
+// coefficient bits; bit b of c_k becomes a lane mask (v_bfe_i32) that enters
+// the 4 dwords of the chunk through v_bitop3 y ^ (x & m).  The mask and its
+// four uses are one asm unit: left to itself the compiler computes all 8*DMAX
+// masks once, keeps them live to share across the 4 dwords, and runs out of
+// VGPRs (124 -> 60 for DMAX = 10).
+template <int POS>
+__device__ __forceinline__ void mxor4(V4& y, const V4& x, uint32_t cw) {
+  uint32_t m;
+  asm("v_bfe_i32 %4, %5, %6, 1\n\t"
+      "v_bitop3_b32 %0, %0, %7, %4 bitop3:0x78\n\t"
+      "v_bitop3_b32 %1, %1, %8, %4 bitop3:0x78\n\t"
+      "v_bitop3_b32 %2, %2, %9, %4 bitop3:0x78\n\t"
+      "v_bitop3_b32 %3, %3, %10, %4 bitop3:0x78"
+      : "+v"(y.v[0]), "+v"(y.v[1]), "+v"(y.v[2]), "+v"(y.v[3]), "=&v"(m)
+      : "v"(cw), "i"(POS), "v"(x.v[0]), "v"(x.v[1]), "v"(x.v[2]), "v"(x.v[3]));
+}
+
+template <int DMAX, int B, int K>
+__device__ __forceinline__ void hv_terms(V4& y, const V4* x, const uint32_t* cw) {
+  mxor4<8 * (K & 3) + B>(y, x[K], cw[K >> 2]);
+  if constexpr (K + 1 < DMAX) hv_terms<DMAX, B, K + 1>(y, x, cw);
+}
+
+template <int DMAX, int B>
+__device__ __forceinline__ void hv_bits(V4& y, const V4* x, const uint32_t* cw) {
+  if constexpr (B != 7) xt4(y);
+  hv_terms<DMAX, B, 0>(y, x, cw);
+  if constexpr (B > 0) hv_bits<DMAX, B - 1>(y, x, cw);
+}
+
+template <int DMAX>
+__device__ __forceinline__ V4 horner_var(const V4* x, const uint32_t* cw) {
+  V4 y{{0u, 0u, 0u, 0u}};
+  hv_bits<DMAX, 7>(y, x, cw);
+  return y;
+}
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
+  return *reinterpret_cast<const uint32_t*>(p);
+}
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+}  // namespace kern
+}  // namespace ugo

@@ -1,0 +1,204 @@
+// tx_kernels.hip -- TX group assembly on gfx950.
+//
+// Replaces, for a whole batch of outgoing groups at once, the sender loop
+// ugo/conn.go:643-685 (sendEncryptedData) and the per-packet encryption of
+// Conn.sendPacket (ugo/conn.go:634):
+//   markData(ori)                     LE32 next, LE16 0xf1 at [0,6)  ugo/fec.go:91-95
+//   copy(fecGroup[k], ori); maxsize = max len
+//   calcECC(fecGroup, 6, maxsize)     Encode of the window [6, maxsize) ugo/fec.go:228-243
+//   markFEC(ecc[k]); ecc[k][:maxsize] LE32 next, LE16 0xf2, paws wrap ugo/fec.go:97-104
+//   crypt.Encrypt(pkt, pkt)           fixed-key RC4 = XOR with one pad  ugo/crypto.go:33-39
+//
+// No realignment is needed: parity is column-independent, so a lane that
+// holds *packet* bytes [16m, 16m+16) of every data packet (payload bytes
+// [16m-6, 16m+10), header bytes zeroed) computes exactly the parity packet's
+// bytes [16m, 16m+16).  Every load and store is an aligned 16-B chunk.
+//
+// Group buffers are zero-filled past each data packet's length (the reference
+// loop reuses its 13 buffers without clearing them, so its parity bytes past a
+// short packet depend on earlier groups; a fresh FEC -- or this batch -- sees
+// zeros).  DESIGN.md §6 states this contract.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gf_device.hpp"
+#include "tx_kernels.hpp"
+
+namespace ugo {
+namespace kern {
+
+namespace {
+
+constexpr uint32_t kTypeData = 0xf1u;  // ugo/constants.go:18
+constexpr uint32_t kTypeFEC = 0xf2u;   // ugo/constants.go:19
+constexpr int8_t kBadLength = 5;       // UGO_FEC_ERR_SHARD_SIZE
+
+__device__ __forceinline__ uint32_t keep_mask(uint32_t keep, int j) {
+  const uint32_t lo = 4u * j;
+  if (keep >= lo + 4u) return 0xffffffffu;
+  if (keep <= lo) return 0u;
+  return (1u << (8u * (keep - lo))) - 1u;
+}
+
+// bytes [keep, 16) of the chunk cleared (keep clamped to 0..16 by the masks)
+__device__ __forceinline__ V4 keep_bytes(const V4& x, uint32_t keep) {
+  V4 y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) y.v[j] = x.v[j] & keep_mask(keep, j);
+  return y;
+}
+
+__device__ __forceinline__ void put_header(V4& x, uint32_t seq, uint32_t flag) {
+  x.v[0] = seq;                                  // LE32 seqid
+  x.v[1] = (x.v[1] & 0xffff0000u) | flag;        // LE16 flag
+}
+
+__device__ __forceinline__ void store_full(uint8_t* p, const V4& y) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  *reinterpret_cast<u32x4*>(p) = u32x4{y.v[0], y.v[1], y.v[2], y.v[3]};
+}
+
+struct TxItem {
+  uint64_t g;        // absolute group
+  uint32_t o;        // packet byte offset of this lane's chunk
+  uint32_t maxsz;    // parity packet length (max data packet length of the group)
+  uint32_t seq0;     // seqid of the group's first packet
+  V4 padc;
+  bool live;
+};
+
+// Lengths, status, data packets out.  x[k] receives the parity inputs
+// (packet chunk, bytes past the length and the header bytes zeroed).
+template <int DN>
+__device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x) {
+  TxItem t{};
+  const uint64_t gl = item / a.chunks;
+  const uint32_t m = item - static_cast<uint32_t>(gl) * a.chunks;
+  t.g = a.g0 + gl;
+  t.o = 16u * m;
+  const uint16_t* L = a.lens + t.g * a.d;
+  bool bad = false;
+  uint32_t maxsz = 0;
+  for (uint32_t k = 0; k < a.d; ++k) {
+    const uint32_t Lk = L[k];
+    bad |= Lk < 6u || Lk > a.max_len;
+    maxsz = max(maxsz, Lk);
+  }
+  const uint32_t n = a.d + a.p;
+  if (bad) {
+    if (m == 0) {
+      if (a.status) a.status[t.g] = kBadLength;
+      for (uint32_t r = 0; r < n; ++r) a.wire_lens[t.g * n + r] = 0;
+    }
+    t.live = false;
+    return t;
+  }
+  t.maxsz = maxsz;
+  t.live = t.o < maxsz;
+  t.seq0 = static_cast<uint32_t>((uint64_t(a.first_seq) + t.g * n) % a.paws);
+  if (!t.live) return t;
+  t.padc = a.pad ? load16<0>(a.pad + t.o) : V4{{0u, 0u, 0u, 0u}};
+  const uint8_t* src = a.pkts + t.g * a.d * a.slot_in + t.o;
+  uint8_t* dst = a.wire + t.g * n * a.slot_out + t.o;
+#pragma unroll
+  for (int k = 0; k < DN; ++k) {
+    if (k < static_cast<int>(a.d)) {
+      const uint32_t Lk = L[k];
+      V4 v{{0u, 0u, 0u, 0u}};
+      if (t.o < Lk) v = load16<1>(src + static_cast<uint64_t>(k) * a.slot_in);
+      v = keep_bytes(v, Lk - min(Lk, t.o));
+      if (t.o < Lk) {
+        V4 w = v;
+        if (m == 0) put_header(w, t.seq0 + k, kTypeData);
+        xor4(w, t.padc);
+        store_full(dst + static_cast<uint64_t>(k) * a.slot_out, keep_bytes(w, Lk - t.o));
+      }
+      if (m == 0) {
+        v.v[0] = 0u;
+        v.v[1] &= 0xffff0000u;
+        a.wire_lens[t.g * n + k] = static_cast<uint16_t>(Lk);
+      }
+      x[k] = v;
+    } else {
+      x[k] = V4{{0u, 0u, 0u, 0u}};
+    }
+  }
+  return t;
+}
+
+__device__ __forceinline__ void tx_parity_out(const TxArgs& a, const TxItem& t, uint32_t i, V4 y) {
+  const uint32_t n = a.d + a.p;
+  if (t.o == 0) put_header(y, t.seq0 + a.d + i, kTypeFEC);
+  xor4(y, t.padc);
+  store_full(a.wire + (t.g * n + a.d + i) * a.slot_out + t.o, keep_bytes(y, t.maxsz - t.o));
+  if (t.o == 0) a.wire_lens[t.g * n + a.d + i] = static_cast<uint16_t>(t.maxsz);
+}
+
+template <int D, int P, int... I>
+__device__ __forceinline__ void tx_cparity(const TxArgs& a, const TxItem& t, const V4* x,
+                                           std::integer_sequence<int, I...>) {
+  (tx_parity_out(a, t, I, cparity<D, P, I>(x)), ...);
+}
+
+// (10,3) / (32,8): the compile-time XOR networks of k_encode_c.
+template <int D, int P>
+__global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.groups * a.chunks) return;
+  V4 x[D];
+  const TxItem t = tx_data<D>(a, item, x);
+  if (!t.live) return;
+  tx_cparity<D, P>(a, t, x, std::make_integer_sequence<int, P>{});
+  if (t.o == 0 && a.status) a.status[t.g] = 0;
+}
+
+// Any other geometry: coefficients from the encode descriptor (uniform, so
+// the coefficient words are scalar loads), masked Horner per parity row.
+template <int DMAX>
+__global__ __launch_bounds__(256) void k_tx_var(TxArgs a) {
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.groups * a.chunks) return;
+  V4 x[DMAX];
+  const TxItem t = tx_data<DMAX>(a, item, x);
+  if (!t.live) return;
+  constexpr int NW = (DMAX + 3) / 4;
+  const uint32_t cbase = 4 + a.dpad + a.epad;
+  for (uint32_t i = 0; i < a.p; ++i) {
+    uint32_t cw[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) cw[w] = ld32(a.desc + cbase + i * a.dpad + 4 * w);
+    tx_parity_out(a, t, i, horner_var<DMAX>(x, cw));
+  }
+  if (t.o == 0 && a.status) a.status[t.g] = 0;
+}
+
+}  // namespace
+
+hipError_t launch_tx_assemble(int dmax, const TxArgs& a, hipStream_t s) {
+  const uint64_t items = a.groups * a.chunks;
+  if (items == 0) return hipSuccess;
+  const dim3 grid(static_cast<uint32_t>((items + 255) / 256)), block(256);
+  switch (dmax) {
+    case 0:
+      if (a.d == 10 && a.p == 3)
+        hipLaunchKernelGGL((k_tx_c<10, 3>), grid, block, 0, s, a);
+      else if (a.d == 32 && a.p == 8)
+        hipLaunchKernelGGL((k_tx_c<32, 8>), grid, block, 0, s, a);
+      else
+        return hipErrorInvalidValue;
+      break;
+    case 4: hipLaunchKernelGGL((k_tx_var<4>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_tx_var<8>), grid, block, 0, s, a); break;
+    case 10: hipLaunchKernelGGL((k_tx_var<10>), grid, block, 0, s, a); break;
+    case 12: hipLaunchKernelGGL((k_tx_var<12>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_tx_var<16>), grid, block, 0, s, a); break;
+    case 24: hipLaunchKernelGGL((k_tx_var<24>), grid, block, 0, s, a); break;
+    case 32: hipLaunchKernelGGL((k_tx_var<32>), grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kern
+}  // namespace ugo

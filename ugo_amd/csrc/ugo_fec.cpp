@@ -21,6 +21,7 @@
 #include "gf256.hpp"
 #include "host/rc4.hpp"
 #include "rx_kernels.hpp"
+#include "tx_kernels.hpp"
 
 namespace {
 
@@ -559,6 +560,50 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   a.S = static_cast<uint32_t>(S);
   a.n = static_cast<uint32_t>(c->n);
   return hip_status(ugo::kern::launch_rx_scatter(a, static_cast<hipStream_t>(stream)));
+}
+
+int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const uint16_t* lens, size_t groups,
+                        uint32_t first_seq, const uint8_t* pad, size_t max_len, uint8_t* wire, size_t slot_out,
+                        uint16_t* wire_lens, int8_t* status, void* stream) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (groups == 0) return UGO_FEC_OK;
+  const uint64_t n = static_cast<uint64_t>(c->n);
+  const uint32_t paws = static_cast<uint32_t>((0xffffffffull / n - 1) * n);  // ugo/fec.go:58
+  const size_t need = round_up(max_len, 16);
+  if (!pkts || !lens || !wire || !wire_lens || c->d > 32 || max_len < 6 || max_len > 0xffff ||
+      slot_in % 16 || slot_out % 16 || slot_in < need || slot_out < need ||
+      reinterpret_cast<uintptr_t>(pkts) % 16 || reinterpret_cast<uintptr_t>(wire) % 16 ||
+      (pad && reinterpret_cast<uintptr_t>(pad) % 16) || first_seq % n || first_seq >= paws)
+    return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  ugo::kern::TxArgs a{};
+  a.pkts = pkts;
+  a.lens = lens;
+  a.pad = pad;
+  a.desc = c->d_encdesc;
+  a.wire = wire;
+  a.wire_lens = wire_lens;
+  a.status = status;
+  a.slot_in = slot_in;
+  a.slot_out = slot_out;
+  a.first_seq = first_seq;
+  a.paws = paws;
+  a.max_len = static_cast<uint32_t>(max_len);
+  a.chunks = static_cast<uint32_t>(need / 16);
+  a.d = static_cast<uint32_t>(c->d);
+  a.p = static_cast<uint32_t>(c->p);
+  a.dpad = c->dpad;
+  a.epad = c->epad;
+  const int dmax = ugo::kern::has_const_encode(c->d, c->p) ? 0 : ugo::kern::apply_dmax(c->d);
+  const uint64_t per_launch = (1ull << 31) / a.chunks;  // items of one launch fit 32 bits
+  for (uint64_t g0 = 0; g0 < groups; g0 += per_launch) {
+    a.g0 = g0;
+    a.groups = std::min<uint64_t>(per_launch, groups - g0);
+    const int st = hip_status(ugo::kern::launch_tx_assemble(dmax, a, static_cast<hipStream_t>(stream)));
+    if (st != UGO_FEC_OK) return st;
+  }
+  return UGO_FEC_OK;
 }
 
 int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size_t n) {

@@ -118,6 +118,7 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_abi_version.argtypes = []
     lib.ugo_fec_rx_assemble.argtypes = [vp, vp, sz, vp, sz, vp, ctypes.c_uint64, sz, vp, sz, sz, sz, vp, vp, vp]
     lib.ugo_fec_rc4_keystream.argtypes = [vp, sz, vp, sz]
+    lib.ugo_fec_tx_assemble.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp, vp]
     _lib = lib
     return lib
 
@@ -236,6 +237,27 @@ class Encoder:
             self._h, wire.data_ptr(), slot, lens.data_ptr(), npk, None if pad is None else pad.data_ptr(),
             first_group, G, shards.data_ptr(), S, rs, gs, present.data_ptr(),
             None if stats is None else stats.data_ptr(), _stream_handle(stream)))
+
+    def tx_assemble(self, pkts, lens, wire, wire_lens, first_seq: int = 0, pad=None, max_len: int = 1476,
+                    status=None, stream=None):
+        """TX group assembly (include/ugo_fec.h ugo_fec_tx_assemble): pkts = uint8 CUDA
+        tensor [G*d, slot_in] of outgoing data packets (6-B header space first),
+        lens = int16/uint16 CUDA [G*d]; wire = uint8 CUDA [G*(d+p), slot_out],
+        wire_lens = int16/uint16 CUDA [G*(d+p)]; pad = uint8 CUDA keystream or None;
+        status = int8 CUDA [G] or None."""
+        d, n = self.DataShards, self.Shards
+        npk, slot_in = pkts.shape
+        assert npk % d == 0, "pkts must hold whole groups of d data packets"
+        G = npk // d
+        assert wire.shape[0] == G * n and wire_lens.numel() == G * n and lens.numel() == npk
+        assert pkts.is_contiguous() and wire.is_contiguous() and lens.is_contiguous() and wire_lens.is_contiguous()
+        assert lens.element_size() == 2 and wire_lens.element_size() == 2
+        if status is not None:
+            assert status.numel() == G and status.element_size() == 1
+        _raise(load_library().ugo_fec_tx_assemble(
+            self._h, pkts.data_ptr(), slot_in, lens.data_ptr(), G, first_seq,
+            None if pad is None else pad.data_ptr(), max_len, wire.data_ptr(), wire.shape[1],
+            wire_lens.data_ptr(), None if status is None else status.data_ptr(), _stream_handle(stream)))
 
     # ------------------------------------------------------ host-buffer batch
     def encode_host(self, shards: np.ndarray, shard_size: Optional[int] = None):
