@@ -64,6 +64,8 @@ static uint8_t MUL[256][256];
 static int g_init = 0;
 
 /* galois.go [upstream]: exp/log tables for generator 2 over x^8+x^4+x^3+x^2+1 */
+static void simd_tables(void);
+
 void oracle_init(void) {
   if (g_init) return;
   int x = 1;
@@ -78,6 +80,7 @@ void oracle_init(void) {
   for (int a = 0; a < 256; a++)
     for (int b = 0; b < 256; b++)
       MUL[a][b] = (a == 0 || b == 0) ? 0 : EXP[LOG[a] + LOG[b]];
+  simd_tables();
   g_init = 1;
 }
 
@@ -182,9 +185,122 @@ int oracle_matrix(int d, int p, uint8_t* out) {
   return st;
 }
 
+/* ---- SIMD forms of codeSomeShards (CPU BASELINE ONLY) ----------------------
+ * The upstream library does its column work with SIMD: pshufb low/high nibble
+ * tables (galMulAVX2*, the mulAvxTwo_RxC fused kernels that load every input
+ * once per column block and keep all outputs in registers) and, on AVX-512
+ * hosts with GFNI, one vgf2p8affineqb per byte vector and coefficient
+ * (mulGFNI_RxC).  These restate that strategy so the timed CPU baseline is a
+ * fair stand-in for the Go library's speed; bench.py selects the best level
+ * the host supports.  The checker default stays scalar (level 0), and
+ * tests/test_oracle.py requires every level to match it byte for byte. */
+static int g_simd = 0;
+static uint8_t NIB_LO[256][32], NIB_HI[256][32];
+static uint64_t GFNI_A[256];
+
+static void simd_tables(void) {
+  for (int c = 0; c < 256; c++) {
+    for (int j = 0; j < 16; j++) {
+      NIB_LO[c][j] = NIB_LO[c][16 + j] = MUL[c][j];
+      NIB_HI[c][j] = NIB_HI[c][16 + j] = MUL[c][j << 4];
+    }
+    /* affine matrix of x -> c*x: byte (7-i) bit j = bit i of c*2^j */
+    uint64_t a = 0;
+    for (int i = 0; i < 8; i++) {
+      uint8_t row = 0;
+      for (int j = 0; j < 8; j++) row |= (uint8_t)(((MUL[c][1 << j] >> i) & 1) << j);
+      a |= (uint64_t)row << (8 * (7 - i));
+    }
+    GFNI_A[c] = a;
+  }
+}
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+
+#define OR_MAXOUT 8
+__attribute__((target("avx2")))
+static void code_some_avx2(const uint8_t* rows, int nin, int nout,
+                           const uint8_t* const* in, uint8_t* const* out, size_t S) {
+  const __m256i m4 = _mm256_set1_epi8(0x0f);
+  for (int o0 = 0; o0 < nout; o0 += OR_MAXOUT) {
+    const int no = nout - o0 < OR_MAXOUT ? nout - o0 : OR_MAXOUT;
+    size_t j = 0;
+    for (; j + 32 <= S; j += 32) {
+      __m256i acc[OR_MAXOUT];
+      for (int o = 0; o < no; o++) acc[o] = _mm256_setzero_si256();
+      for (int i = 0; i < nin; i++) {
+        const __m256i x = _mm256_loadu_si256((const __m256i*)(in[i] + j));
+        const __m256i lo = _mm256_and_si256(x, m4);
+        const __m256i hi = _mm256_and_si256(_mm256_srli_epi64(x, 4), m4);
+        for (int o = 0; o < no; o++) {
+          const uint8_t c = rows[(size_t)(o0 + o) * nin + i];
+          const __m256i tl = _mm256_loadu_si256((const __m256i*)NIB_LO[c]);
+          const __m256i th = _mm256_loadu_si256((const __m256i*)NIB_HI[c]);
+          acc[o] = _mm256_xor_si256(acc[o], _mm256_xor_si256(_mm256_shuffle_epi8(tl, lo), _mm256_shuffle_epi8(th, hi)));
+        }
+      }
+      for (int o = 0; o < no; o++) _mm256_storeu_si256((__m256i*)(out[o0 + o] + j), acc[o]);
+    }
+    for (; j < S; j++)
+      for (int o = 0; o < no; o++) {
+        uint8_t v = 0;
+        for (int i = 0; i < nin; i++) v ^= MUL[rows[(size_t)(o0 + o) * nin + i]][in[i][j]];
+        out[o0 + o][j] = v;
+      }
+  }
+}
+
+__attribute__((target("avx512f,avx512bw,gfni")))
+static void code_some_gfni(const uint8_t* rows, int nin, int nout,
+                           const uint8_t* const* in, uint8_t* const* out, size_t S) {
+  for (int o0 = 0; o0 < nout; o0 += OR_MAXOUT) {
+    const int no = nout - o0 < OR_MAXOUT ? nout - o0 : OR_MAXOUT;
+    size_t j = 0;
+    for (; j < S; j += 64) {
+      const size_t nb = S - j < 64 ? S - j : 64;
+      const __mmask64 k = nb == 64 ? ~(__mmask64)0 : (((__mmask64)1 << nb) - 1);
+      __m512i acc[OR_MAXOUT];
+      for (int o = 0; o < no; o++) acc[o] = _mm512_setzero_si512();
+      for (int i = 0; i < nin; i++) {
+        const __m512i x = _mm512_maskz_loadu_epi8(k, in[i] + j);
+        for (int o = 0; o < no; o++) {
+          const __m512i a = _mm512_set1_epi64((long long)GFNI_A[rows[(size_t)(o0 + o) * nin + i]]);
+          acc[o] = _mm512_xor_si512(acc[o], _mm512_gf2p8affine_epi64_epi8(x, a, 0));
+        }
+      }
+      for (int o = 0; o < no; o++) _mm512_mask_storeu_epi8(out[o0 + o] + j, k, acc[o]);
+    }
+  }
+}
+#endif
+
+/* 0 = scalar (checker default), 1 = AVX2 nibble tables, 2 = AVX-512 GFNI,
+ * -1 = best the host supports.  Returns the level in effect. */
+int oracle_set_simd(int level) {
+  oracle_init();
+  int best = 0;
+#if defined(__x86_64__)
+  __builtin_cpu_init();
+  if (__builtin_cpu_supports("avx2")) best = 1;
+  if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+      __builtin_cpu_supports("gfni"))
+    best = 2;
+#endif
+  if (level < 0 || level > best) level = best;
+  g_simd = level;
+  return g_simd;
+}
+
+int oracle_simd_level(void) { return g_simd; }
+
 /* codeSomeShards [upstream]: out[o][j] = XOR_i rows[o][i] * in[i][j] */
 static void code_some(const uint8_t* rows, int nin, int nout,
                       const uint8_t* const* in, uint8_t* const* out, size_t S) {
+#if defined(__x86_64__)
+  if (g_simd == 2) { code_some_gfni(rows, nin, nout, in, out, S); return; }
+  if (g_simd == 1) { code_some_avx2(rows, nin, nout, in, out, S); return; }
+#endif
   for (int o = 0; o < nout; o++) {
     uint8_t* dst = out[o];
     memset(dst, 0, S);
@@ -222,8 +338,10 @@ int oracle_encode(int d, int p, uint8_t* shards, size_t G, size_t S, size_t pitc
 
 /* Reconstruct(shards) [upstream], one group.  present_mask bit r = shard r is
  * non-empty (len(shards[r]) != 0).  Erased rows are (over)written. */
+/* inv_cache (nullable): per-pattern inverse cache like upstream's
+ * inversionTree -- entry [mask] holds d*d bytes + a valid flag byte. */
 static int recon_group(int d, int p, const uint8_t* M, uint8_t* grp, uint64_t present_mask,
-                       size_t S, size_t pitch, int data_only) {
+                       size_t S, size_t pitch, int data_only, uint8_t* inv_cache) {
   int n = d + p;
   int npresent = 0, dpresent = 0;
   for (int r = 0; r < n; r++)
@@ -239,27 +357,41 @@ static int recon_group(int d, int p, const uint8_t* M, uint8_t* grp, uint64_t pr
   /* first d present rows in index order */
   for (int r = 0; r < n && cnt < d; r++)
     if ((present_mask >> r) & 1) { valid[cnt] = r; subsh[cnt] = grp + (size_t)r * pitch; cnt++; }
-  for (int i = 0; i < d; i++) memcpy(sub + (size_t)i * d, M + (size_t)valid[i] * d, (size_t)d);
-  int st = oracle_invert(d, sub, inv);
-  if (st) { free(valid); free(sub); free(inv); free(subsh); return st; }
+  uint8_t* ce = inv_cache ? inv_cache + present_mask * ((size_t)d * d + 1) : NULL;
+  if (ce && ce[(size_t)d * d]) {
+    memcpy(inv, ce, (size_t)d * d);
+  } else {
+    for (int i = 0; i < d; i++) memcpy(sub + (size_t)i * d, M + (size_t)valid[i] * d, (size_t)d);
+    int st = oracle_invert(d, sub, inv);
+    if (st) { free(valid); free(sub); free(inv); free(subsh); return st; }
+    if (ce) { memcpy(ce, inv, (size_t)d * d); ce[(size_t)d * d] = 1; }
+  }
 
-  /* stage 1: missing data rows from the survivors */
+  /* stage 1: missing data rows from the survivors (one codeSomeShards call
+   * over all of them, as upstream) */
+  uint8_t* rows = (uint8_t*)malloc((size_t)n * d);
+  uint8_t** outs = (uint8_t**)malloc(sizeof(void*) * n);
+  int no = 0;
   for (int r = 0; r < d; r++) {
     if ((present_mask >> r) & 1) continue;
-    uint8_t* dst = grp + (size_t)r * pitch;
-    code_some(inv + (size_t)r * d, d, 1, subsh, &dst, S);
+    memcpy(rows + (size_t)no * d, inv + (size_t)r * d, (size_t)d);
+    outs[no++] = grp + (size_t)r * pitch;
   }
+  if (no) code_some(rows, d, no, subsh, outs, S);
   if (!data_only) {
     /* stage 2: missing parity rows re-encoded from the completed data rows */
     const uint8_t** data = (const uint8_t**)malloc(sizeof(void*) * d);
     for (int k = 0; k < d; k++) data[k] = grp + (size_t)k * pitch;
+    no = 0;
     for (int r = d; r < n; r++) {
       if ((present_mask >> r) & 1) continue;
-      uint8_t* dst = grp + (size_t)r * pitch;
-      code_some(M + (size_t)r * d, d, 1, data, &dst, S);
+      memcpy(rows + (size_t)no * d, M + (size_t)r * d, (size_t)d);
+      outs[no++] = grp + (size_t)r * pitch;
     }
+    if (no) code_some(rows, d, no, data, outs, S);
     free(data);
   }
+  free(rows); free(outs);
   free(valid); free(sub); free(inv); free(subsh);
   return OR_OK;
 }
@@ -278,12 +410,15 @@ static void* recon_worker(void* arg) {
   recon_job* j = (recon_job*)arg;
   int n = j->d + j->p;
   j->rc = OR_OK;
+  /* per-thread pattern cache for n <= 16 (no locking) */
+  uint8_t* cache = n <= 16 ? (uint8_t*)calloc((size_t)1 << n, (size_t)j->d * j->d + 1) : NULL;
   for (size_t g = j->g0; g < j->g1; g++) {
     int st = recon_group(j->d, j->p, j->M, j->shards + g * (size_t)n * j->pitch,
-                         j->present[g], j->S, j->pitch, j->data_only);
+                         j->present[g], j->S, j->pitch, j->data_only, cache);
     if (j->status) j->status[g] = (int8_t)st;
     if (st && !j->rc) j->rc = st;
   }
+  free(cache);
   return NULL;
 }
 

@@ -189,10 +189,21 @@ def load_c_oracle():
     lib.oracle_check_geometry.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.oracle_fill.argtypes = [ctypes.c_void_p, ctypes.c_int, sz, sz, sz, ctypes.c_uint64, ctypes.c_int]
     lib.oracle_fill.restype = None
+    lib.oracle_set_simd.argtypes = [ctypes.c_int]
+    lib.oracle_simd_level.argtypes = []
     lib.oracle_init()
     del u8p
     _lib = lib
     return lib
+
+
+def set_simd(level: int) -> int:
+    """CPU-baseline SIMD level of the C oracle (0 scalar, 1 AVX2, 2 AVX-512
+    GFNI, -1 best available); returns the level in effect."""
+    return load_c_oracle().oracle_set_simd(level)
+
+
+SIMD_NAMES = {0: "scalar", 1: "avx2-nibble-pshufb", 2: "avx512-gfni-affine"}
 
 
 def _ptr(a: np.ndarray):

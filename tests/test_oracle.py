@@ -191,3 +191,32 @@ def test_oracle_errors():
     assert lib.oracle_check_shards(3, lens, 0, ctypes.byref(out)) == 5
     lens = (ctypes.c_size_t * 2)(0, 0)
     assert lib.oracle_check_shards(2, lens, 1, ctypes.byref(out)) == 4
+
+
+@pytest.mark.parametrize("d,p,S", [(10, 3, 1350), (32, 8, 9000), (5, 3, 77), (17, 7, 1)])
+def test_simd_baseline_levels_match_scalar(d, p, S):
+    """The SIMD forms used only for the timed CPU baseline (AVX2 nibble tables,
+    AVX-512 GFNI) reproduce the scalar checker byte for byte."""
+    n = d + p
+    rng = np.random.default_rng(d * 100 + S)
+    base = rng.integers(0, 256, (6, n, S), dtype=np.uint8)
+    masks = np.full(6, (1 << n) - 1, np.uint64)
+    for g in range(6):
+        for r in rng.choice(n, p, replace=False):
+            masks[g] &= ~np.uint64(1 << int(r))
+    outs = []
+    try:
+        for level in (0, 1, 2):
+            got = rs_ref.set_simd(level)
+            sh = base.copy()
+            rs_ref.c_encode(d, p, sh)
+            enc = sh.copy()
+            sh[:, :, :] = np.where(((masks[:, None] >> np.arange(n, dtype=np.uint64)) & 1).astype(bool)[:, :, None], enc, 0)
+            rs_ref.c_reconstruct(d, p, sh, masks)
+            outs.append((got, enc, sh))
+    finally:
+        rs_ref.set_simd(0)
+    for got, enc, sh in outs[1:]:
+        assert np.array_equal(enc, outs[0][1]), f"level {got} encode"
+        assert np.array_equal(sh, outs[0][2]), f"level {got} reconstruct"
+        assert np.array_equal(sh, outs[0][1])

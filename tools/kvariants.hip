@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&masks_fixed, G * 8));
   std::vector<uint64_t> hf(G, ((1ull << n) - 1) & ~(1ull << 3) & ~(1ull << 11));
   CK(hipMemcpy(masks_fixed, hf.data(), G * 8, hipMemcpyHostToDevice));
-  for (int lay = 0; lay < 2; ++lay) {
+  for (int lay = 1; lay < 2; ++lay) {  // 0 = interleaved: see profiles/r1/kvariants_interleaved_ab.jsonl
     const Batch& b = lay ? pl : a;
     const std::string L = lay ? "planar" : "interl";
     add(k_encode_c<10, 3, 0>, b, enc_bytes, "enc " + L + " nt0");
@@ -126,8 +126,6 @@ int main(int argc, char** argv) {
       add(k_apply_w<10, 1, 3, 1>, b1, dec_bytes, "dec " + L + " nt3 wave-scalar-desc cpt1");
     }
         add(k_apply_p<10, 1, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick");
-    add(k_apply_p<10, 1, 1, 1, 7>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick wpe7");
-    add(k_apply_p<10, 1, 1, 1, 8>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick wpe8");
     add(k_apply_p<10, 1, 1, 2>, b, dec_bytes, "dec " + L + " nt1 perm-tables vector-tables");
     add(k_apply_p<12, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables dmax12");
     Batch bf = b;
@@ -149,9 +147,11 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(kd, dim3(grid), dim3(256), 0, 0, b);
     }, {}});
   };
-  pair(k_encode_c<10, 3, 1>, k_apply<10, 1, 3>, pl, "pair planar enc-nt1 dec-nt3");
-  pair(k_encode_c<10, 3, 3>, k_apply<10, 1, 3>, pl, "pair planar enc-nt3 dec-nt3");
-  pair(k_encode_c<10, 3, 1>, k_apply<10, 1, 1>, pl, "pair planar enc-nt1 dec-nt1");
+  pair(k_encode_c<10, 3, 1>, k_apply_p<10, 1, 1>, pl, "pair planar enc-nt1 perm-nt1");
+  pair(k_encode_c<10, 3, 3>, k_apply_p<10, 1, 1>, pl, "pair planar enc-nt3 perm-nt1");
+  pair(k_encode_c<10, 3, 1>, k_apply_p<10, 1, 3>, pl, "pair planar enc-nt1 perm-nt3");
+  pair(k_encode_c<10, 3, 3>, k_apply_p<10, 1, 3>, pl, "pair planar enc-nt3 perm-nt3");
+  pair(k_encode_c<10, 3, 1>, k_apply_p<10, 1, 0>, pl, "pair planar enc-nt1 perm-nt0");
 
   {  // k_apply_p must reproduce k_apply_w bit for bit (random masks, planar)
     const uint32_t grid = (pl.items + 255) / 256;

@@ -1,0 +1,74 @@
+// A/B timing of TX assembly kernel variants (store policy, scalar lengths).
+// Not product code: includes the kernel TU.  Output: one JSON line per variant.
+#include "../ugo_amd/csrc/tx_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+using namespace ugo::kern;
+
+int main(int argc, char** argv) {
+  const uint64_t G = argc > 1 ? atoll(argv[1]) : 65536;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 11;
+  const uint32_t d = 10, p = 3, n = 13, slot = 1488, maxl = 1476;
+  uint8_t *pk, *wire, *pad;
+  uint16_t *lens, *wl;
+  CK(hipMalloc(&pk, G * d * slot));
+  CK(hipMalloc(&wire, G * n * slot));
+  CK(hipMalloc(&pad, slot));
+  CK(hipMalloc(&lens, G * d * 2));
+  CK(hipMalloc(&wl, G * n * 2));
+  CK(hipMemset(pk, 0x3c, G * d * slot));
+  CK(hipMemset(pad, 0x5a, slot));
+  std::vector<uint16_t> hl(G * d, maxl);
+  CK(hipMemcpy(lens, hl.data(), hl.size() * 2, hipMemcpyHostToDevice));
+  TxArgs a{};
+  a.pkts = pk; a.lens = lens; a.pad = pad; a.wire = wire; a.wire_lens = wl;
+  a.groups = G; a.slot_in = slot; a.slot_out = slot; a.first_seq = 0; a.paws = (0xffffffffu / n - 1) * n;
+  a.max_len = maxl; a.chunks = (maxl + 15) / 16; a.d = d; a.p = p; a.dpad = 12; a.epad = 4;
+  const double bytes = double(G) * (2.0 * d * maxl + p * maxl);
+  const uint32_t grid = (G * a.chunks + 255) / 256;
+  struct Var { std::string name; std::function<void()> go; std::vector<float> t; };
+  std::vector<Var> vars;
+  auto add = [&](auto k, std::string nm) {
+    vars.push_back({nm, [=]() { hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, a); }, {}});
+  };
+  add(k_tx_c<10, 3, 1, false>, "tx nt1 vector-lens");
+  add(k_tx_c<10, 3, 1, true>, "tx nt1 scalar-lens");
+  add(k_tx_c<10, 3, 3, false>, "tx nt3 vector-lens");
+  add(k_tx_c<10, 3, 3, true>, "tx nt3 scalar-lens");
+  add(k_tx_c<10, 3, 0, true>, "tx nt0 scalar-lens");
+  // correctness: every variant writes the same wire bytes
+  std::vector<uint8_t> ref(G * n * slot), got(G * n * slot);
+  for (size_t v = 0; v < vars.size(); ++v) {
+    CK(hipMemset(wire, 0, G * n * slot));
+    vars[v].go();
+    CK(hipMemcpy(v ? got.data() : ref.data(), wire, ref.size(), hipMemcpyDeviceToHost));
+    if (v) printf("{\"check\":\"%s\",\"equal\":%s}\n", vars[v].name.c_str(), got == ref ? "true" : "false");
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int r = 0; r < rounds; ++r)
+    for (auto& v : vars) {
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < 5; ++i) v.go();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.t.push_back(ms / 5);
+    }
+  for (auto& v : vars) {
+    std::sort(v.t.begin(), v.t.end());
+    const float med = v.t[v.t.size() / 2];
+    printf("{\"variant\":\"%s\",\"median_us\":%.2f,\"min_us\":%.2f,\"GBps\":%.1f}\n", v.name.c_str(), med * 1e3,
+           v.t[0] * 1e3, bytes / (med * 1e-3) / 1e9);
+  }
+  return 0;
+}

@@ -54,10 +54,10 @@ __device__ __forceinline__ void put_header(V4& x, uint32_t seq, uint32_t flag) {
   x.v[1] = (x.v[1] & 0xffff0000u) | flag;        // LE16 flag
 }
 
-__device__ __forceinline__ void store_full(uint8_t* p, const V4& y) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  *reinterpret_cast<u32x4*>(p) = u32x4{y.v[0], y.v[1], y.v[2], y.v[3]};
-}
+// launch policy (tools/txvariants.hip A/B): nontemporal loads of the packet
+// stream; store policy / scalar lengths as measured
+constexpr int kTxNT = 1;
+constexpr bool kTxSL = false;
 
 struct TxItem {
   uint64_t g;        // absolute group
@@ -70,20 +70,46 @@ struct TxItem {
 
 // Lengths, status, data packets out.  x[k] receives the parity inputs
 // (packet chunk, bytes past the length and the header bytes zeroed).
-template <int DN>
+//
+// SL (even DN == d only): the lengths are read with scalar loads for the two
+// groups a wave can span (>= 64 chunks per group) and picked per lane, instead
+// of one broadcast vector load per packet per wave.
+template <int DN, int NT, bool SL>
 __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x) {
   TxItem t{};
   const uint64_t gl = item / a.chunks;
   const uint32_t m = item - static_cast<uint32_t>(gl) * a.chunks;
   t.g = a.g0 + gl;
   t.o = 16u * m;
-  const uint16_t* L = a.lens + t.g * a.d;
+  uint32_t Ls[DN];
+  if constexpr (SL) {
+    static_assert(DN % 2 == 0, "scalar lengths need an even d");
+    const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+    const uint64_t items = a.groups * a.chunks;
+    const uint64_t wlast = min(static_cast<uint64_t>(wfirst) + 63u, items - 1u);
+    const uint64_t gA = a.g0 + wfirst / a.chunks;
+    const uint64_t gB = a.g0 + wlast / a.chunks;  // gA or gA + 1, never past the batch
+    const uint8_t* lA = reinterpret_cast<const uint8_t*>(a.lens + gA * DN);
+    const uint8_t* lB = reinterpret_cast<const uint8_t*>(a.lens + gB * DN);
+    const bool inB = t.g != gA;
+#pragma unroll
+    for (int w = 0; w < DN / 2; ++w) {
+      const uint32_t wa = ld32(lA + 4 * w), wb = ld32(lB + 4 * w);
+      const uint32_t v = inB ? wb : wa;
+      Ls[2 * w] = v & 0xffffu;
+      Ls[2 * w + 1] = v >> 16;
+    }
+  } else {
+    const uint16_t* L = a.lens + t.g * a.d;
+#pragma unroll
+    for (int k = 0; k < DN; ++k) Ls[k] = k < static_cast<int>(a.d) ? L[k] : 6u;
+  }
   bool bad = false;
   uint32_t maxsz = 0;
-  for (uint32_t k = 0; k < a.d; ++k) {
-    const uint32_t Lk = L[k];
-    bad |= Lk < 6u || Lk > a.max_len;
-    maxsz = max(maxsz, Lk);
+#pragma unroll
+  for (int k = 0; k < DN; ++k) {
+    bad |= Ls[k] < 6u || Ls[k] > a.max_len;
+    maxsz = max(maxsz, Ls[k]);
   }
   const uint32_t n = a.d + a.p;
   if (bad) {
@@ -104,7 +130,7 @@ __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x)
 #pragma unroll
   for (int k = 0; k < DN; ++k) {
     if (k < static_cast<int>(a.d)) {
-      const uint32_t Lk = L[k];
+      const uint32_t Lk = Ls[k];
       V4 v{{0u, 0u, 0u, 0u}};
       if (t.o < Lk) v = load16<1>(src + static_cast<uint64_t>(k) * a.slot_in);
       v = keep_bytes(v, Lk - min(Lk, t.o));
@@ -112,7 +138,7 @@ __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x)
         V4 w = v;
         if (m == 0) put_header(w, t.seq0 + k, kTypeData);
         xor4(w, t.padc);
-        store_full(dst + static_cast<uint64_t>(k) * a.slot_out, keep_bytes(w, Lk - t.o));
+        store16<NT>(dst + static_cast<uint64_t>(k) * a.slot_out, keep_bytes(w, Lk - t.o), 16u);
       }
       if (m == 0) {
         v.v[0] = 0u;
@@ -127,29 +153,30 @@ __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x)
   return t;
 }
 
+template <int NT>
 __device__ __forceinline__ void tx_parity_out(const TxArgs& a, const TxItem& t, uint32_t i, V4 y) {
   const uint32_t n = a.d + a.p;
   if (t.o == 0) put_header(y, t.seq0 + a.d + i, kTypeFEC);
   xor4(y, t.padc);
-  store_full(a.wire + (t.g * n + a.d + i) * a.slot_out + t.o, keep_bytes(y, t.maxsz - t.o));
+  store16<NT>(a.wire + (t.g * n + a.d + i) * a.slot_out + t.o, keep_bytes(y, t.maxsz - t.o), 16u);
   if (t.o == 0) a.wire_lens[t.g * n + a.d + i] = static_cast<uint16_t>(t.maxsz);
 }
 
-template <int D, int P, int... I>
+template <int D, int P, int NT, int... I>
 __device__ __forceinline__ void tx_cparity(const TxArgs& a, const TxItem& t, const V4* x,
                                            std::integer_sequence<int, I...>) {
-  (tx_parity_out(a, t, I, cparity<D, P, I>(x)), ...);
+  (tx_parity_out<NT>(a, t, I, cparity<D, P, I>(x)), ...);
 }
 
 // (10,3) / (32,8): the compile-time XOR networks of k_encode_c.
-template <int D, int P>
+template <int D, int P, int NT = kTxNT, bool SL = kTxSL>
 __global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
   if (item >= a.groups * a.chunks) return;
   V4 x[D];
-  const TxItem t = tx_data<D>(a, item, x);
+  const TxItem t = tx_data<D, NT, SL>(a, item, x);
   if (!t.live) return;
-  tx_cparity<D, P>(a, t, x, std::make_integer_sequence<int, P>{});
+  tx_cparity<D, P, NT>(a, t, x, std::make_integer_sequence<int, P>{});
   if (t.o == 0 && a.status) a.status[t.g] = 0;
 }
 
@@ -160,7 +187,7 @@ __global__ __launch_bounds__(256) void k_tx_var(TxArgs a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
   if (item >= a.groups * a.chunks) return;
   V4 x[DMAX];
-  const TxItem t = tx_data<DMAX>(a, item, x);
+  const TxItem t = tx_data<DMAX, kTxNT, false>(a, item, x);
   if (!t.live) return;
   constexpr int NW = (DMAX + 3) / 4;
   const uint32_t cbase = 4 + a.dpad + a.epad;
@@ -168,7 +195,7 @@ __global__ __launch_bounds__(256) void k_tx_var(TxArgs a) {
     uint32_t cw[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) cw[w] = ld32(a.desc + cbase + i * a.dpad + 4 * w);
-    tx_parity_out(a, t, i, horner_var<DMAX>(x, cw));
+    tx_parity_out<kTxNT>(a, t, i, horner_var<DMAX>(x, cw));
   }
   if (t.o == 0 && a.status) a.status[t.g] = 0;
 }
