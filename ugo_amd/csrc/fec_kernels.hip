@@ -251,51 +251,74 @@ __global__ __launch_bounds__(256) void k_apply_w(Batch a) {
 //   0: wave-uniform (dA == dB), scalar loads only
 //   1: scalar loads of both, per-lane pick as arithmetic
 //   2: per-lane vector loads of the picked group's table (L1-resident)
+template <int TSEL>
+__device__ __forceinline__ void p_tables(uint32_t* t, const Batch& a, const uint8_t* dA, const uint8_t* dB,
+                                         uint32_t off, int k, uint32_t mB) {
+  const uint32_t cA = (ld32(dA + off) >> (8 * (k & 3))) & 0xffu;
+  const uint32_t* tA = a.mult + 8u * cA;
+  if constexpr (TSEL == 0) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) t[q] = tA[q];
+  } else {
+    const uint32_t cB = (ld32(dB + off) >> (8 * (k & 3))) & 0xffu;
+    const uint32_t* tB = a.mult + 8u * cB;
+    if constexpr (TSEL == 1) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {  // vA ^ ((vA ^ vB) & mB): the XOR of the two scalar
+        const uint32_t va = tA[q];   // words is SALU work, the pick two VALU ops with one
+        const uint32_t vb = tB[q];   // SGPR each (mB is opaque, so this is not rewritten
+        t[q] = va ^ ((va ^ vb) & mB);  // into a select / per-lane vector load)
+      }
+    } else {
+      const uint32_t* tp = mB ? tB : tA;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) t[q] = tp[q];
+    }
+  }
+}
+
+__device__ __forceinline__ void p_sel(const V4& x, uint32_t* s0, uint32_t* s1, uint32_t* s2) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s0[j] = x.v[j] & 0x07070707u;
+    s1[j] = (x.v[j] >> 3) & 0x07070707u;
+    s2[j] = (x.v[j] >> 6) & 0x03030303u;
+  }
+}
+
+// TSEL: how a lane gets its group's tables when the wave spans groups A, B.
+//   0: wave-uniform (dA == dB), scalar loads only
+//   1: scalar loads of both, per-lane pick as arithmetic
+//   2: per-lane vector loads of the picked group's table (L1-resident)
+// Inputs are taken in pairs so that the six table lookups of two products fold
+// into an accumulator with three xor3 (DMAX is even; a missing odd input is a
+// zero chunk, whose lookups are zero whatever the coefficient).
 template <int DMAX, int TSEL>
 __device__ __forceinline__ void p_accum(V4* acc, const V4* x, const Batch& a, const uint8_t* dA,
                                         const uint8_t* dB, uint32_t mB, uint32_t emax) {
+  static_assert(DMAX % 2 == 0, "inputs are taken in pairs");
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
   const uint32_t cbase = 4 + a.dpad + a.epad;
 #pragma unroll
-  for (int k = 0; k < DMAX; ++k) {
+  for (int k = 0; k < DMAX; k += 2) {
     if (k >= static_cast<int>(a.d)) continue;
-    uint32_t s0[4], s1[4], s2[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s0[j] = x[k].v[j] & 0x07070707u;
-      s1[j] = (x[k].v[j] >> 3) & 0x07070707u;
-      s2[j] = (x[k].v[j] >> 6) & 0x03030303u;
-    }
+    uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
+    p_sel(x[k], s0, s1, s2);
+    p_sel(x[k + 1], r0, r1, r2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (i >= static_cast<int>(emax)) continue;
       const uint32_t off = cbase + i * a.dpad + (k & ~3);
-      const uint32_t cA = (ld32(dA + off) >> (8 * (k & 3))) & 0xffu;
-      const uint32_t* tA = a.mult + 8u * cA;
-      uint32_t t[5];
-      if constexpr (TSEL == 0) {
+      uint32_t t[5], u[5];
+      p_tables<TSEL>(t, a, dA, dB, off, k, mB);
+      p_tables<TSEL>(u, a, dA, dB, off, k + 1, mB);
 #pragma unroll
-        for (int q = 0; q < 5; ++q) t[q] = tA[q];
-      } else {
-        const uint32_t cB = (ld32(dB + off) >> (8 * (k & 3))) & 0xffu;
-        const uint32_t* tB = a.mult + 8u * cB;
-        if constexpr (TSEL == 1) {
-#pragma unroll
-          for (int q = 0; q < 5; ++q) {  // arithmetic pick: a select would be folded
-            const uint32_t va = tA[q];   // into one per-lane vector load
-            const uint32_t vb = tB[q];
-            t[q] = va ^ ((va ^ vb) & mB);
-          }
-        } else {
-          const uint32_t* tp = mB ? tB : tA;
-#pragma unroll
-          for (int q = 0; q < 5; ++q) t[q] = tp[q];
-        }
+      for (int j = 0; j < 4; ++j) {
+        uint32_t y = xor3(acc[i].v[j], perm(t[1], t[0], s0[j]), perm(t[3], t[2], s1[j]));
+        y = xor3(y, perm(0u, t[4], s2[j]), perm(u[1], u[0], r0[j]));
+        acc[i].v[j] = xor3(y, perm(u[3], u[2], r1[j]), perm(0u, u[4], r2[j]));
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i].v[j] = xor3(acc[i].v[j], perm(t[1], t[0], s0[j]), perm(t[3], t[2], s1[j])) ^ perm(0u, t[4], s2[j]);
     }
   }
 }
@@ -339,7 +362,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (wst) a.status[g] = static_cast<int8_t>(st);
     return;
   }
-  const uint32_t mB = inB ? ~0u : 0u;
+  uint32_t mB;  // all-ones in group-B lanes; opaque to the optimizer (see p_tables)
+  asm("v_mov_b32 %0, %1" : "=v"(mB) : "v"(inB ? ~0u : 0u));
   uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
   const uint32_t nb = a.S - c * 16u;
   V4 x[DMAX];
@@ -349,6 +373,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
       const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
       x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
+    } else {
+      x[k] = V4{{0u, 0u, 0u, 0u}};
     }
   }
   V4 acc[4];
