@@ -126,7 +126,7 @@ int main(int argc, char** argv) {
       add(k_apply_w<10, 1, 3, 1>, b1, dec_bytes, "dec " + L + " nt3 wave-scalar-desc cpt1");
     }
         add(k_apply_p<10, 1, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick");
-    add(k_apply_p<10, 1, 1, 2>, b, dec_bytes, "dec " + L + " nt1 perm-tables vector-tables");
+    add(k_apply_q<4, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables streaming ring4 (k_apply_q)");
     add(k_apply_p<12, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables dmax12");
     Batch bf = b;
     bf.present = masks_fixed;

@@ -392,6 +392,103 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (wst) a.status[g] = 0;
 }
 
+// Streaming form of k_apply_p for wide codes ((32,8) jumbo: d up to 255,
+// e <= EMAX outputs): inputs are not held -- a 4-deep ring of survivor
+// chunks is loaded ahead while the current pair is folded into EMAX live
+// accumulators -- so registers hold 4*EMAX accumulator dwords plus the ring,
+// independent of d (vs k_apply's d-sized input block and masked Horner).
+template <int EMAX, int MODE, int NT, int TSEL = 1>
+__global__ __launch_bounds__(256) void k_apply_q(Batch a) {
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (wfirst >= a.items) return;
+  const uint32_t wlast = min(wfirst + 63u, a.items - 1u);
+  const uint32_t gA = wfirst / a.chunks;
+  const uint32_t gB = wlast / a.chunks;
+  const uint8_t* dA = desc_for<MODE>(a, a.g0 + gA);
+  const uint8_t* dB = desc_for<MODE>(a, a.g0 + gB);
+  const uint32_t hA = ld32(dA), hB = ld32(dB);
+  const uint32_t eA = ((hA >> 16) & 0xffu) ? 0u : (a.data_only ? ((hA >> 8) & 0xffu) : (hA & 0xffu));
+  const uint32_t eB = ((hB >> 16) & 0xffu) ? 0u : (a.data_only ? ((hB >> 8) & 0xffu) : (hB & 0xffu));
+  const uint32_t emax = max(eA, eB);
+  if (item >= a.items) return;
+  const uint32_t gl = item / a.chunks;
+  const bool inB = gl != gA;
+  const uint32_t c = item - gl * a.chunks;
+  const uint64_t g = a.g0 + gl;
+  const uint32_t st = ((inB ? hB : hA) >> 16) & 0xffu;
+  const bool wst = MODE != 0 && a.status != nullptr && c == 0;
+  const uint32_t e = inB ? eB : eA;
+  if (e == 0) {
+    if (wst) a.status[g] = static_cast<int8_t>(st);
+    return;
+  }
+  uint32_t mB;
+  asm("v_mov_b32 %0, %1" : "=v"(mB) : "v"(inB ? ~0u : 0u));
+  const uint8_t* dS = dA == dB ? dA : nullptr;  // wave-uniform descriptor
+  uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
+  const uint32_t nb = a.S - c * 16u;
+  auto row_of = [&](uint32_t k) -> uint32_t {
+    const uint32_t wa = ld32(dA + 4 + (k & ~3u)), wb = ld32(dB + 4 + (k & ~3u));
+    return ((inB ? wb : wa) >> (8 * (k & 3u))) & 0xffu;
+  };
+  auto load_in = [&](uint32_t k) -> V4 {
+    if (k >= a.d) return V4{{0u, 0u, 0u, 0u}};
+    return load16<NT>(gp + static_cast<uint64_t>(row_of(k)) * a.rstride);
+  };
+  V4 acc[EMAX];
+#pragma unroll
+  for (int i = 0; i < EMAX; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
+  V4 ring[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ring[j] = load_in(j);
+  const uint32_t cbase = 4 + a.dpad + a.epad;
+  for (uint32_t k0 = 0; k0 < a.d; k0 += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+      const uint32_t k = k0 + j;
+      uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
+      p_sel(ring[j], s0, s1, s2);
+      p_sel(ring[j + 1], r0, r1, r2);
+      ring[j] = load_in(k + 4);
+      ring[j + 1] = load_in(k + 5);
+#pragma unroll
+      for (int i = 0; i < EMAX; ++i) {
+        if (i >= static_cast<int>(emax)) continue;
+        const uint32_t off = cbase + i * a.dpad + k0;  // coefficient word of inputs k0..k0+3
+        uint32_t t[5], u[5];
+        if (dS) {
+          p_tables<0>(t, a, dS, dS, off, j, 0u);
+          p_tables<0>(u, a, dS, dS, off, j + 1, 0u);
+        } else {
+          p_tables<TSEL>(t, a, dA, dB, off, j, mB);
+          p_tables<TSEL>(u, a, dA, dB, off, j + 1, mB);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t y = xor3(acc[i].v[q], perm(t[1], t[0], s0[q]), perm(t[3], t[2], s1[q]));
+          y = xor3(y, perm(0u, t[4], s2[q]), perm(u[1], u[0], r0[q]));
+          acc[i].v[q] = xor3(y, perm(u[3], u[2], r1[q]), perm(0u, u[4], r2[q]));
+        }
+      }
+    }
+  }
+  constexpr int NO = (EMAX + 3) / 4;
+  uint32_t orw[NO];
+#pragma unroll
+  for (int w = 0; w < NO; ++w) {
+    const uint32_t oa = ld32(dA + 4 + a.dpad + 4 * w), ob = ld32(dB + 4 + a.dpad + 4 * w);
+    orw[w] = inB ? ob : oa;
+  }
+#pragma unroll
+  for (int i = 0; i < EMAX; ++i) {
+    if (i >= static_cast<int>(e)) continue;
+    const uint32_t r = (orw[i >> 2] >> (8 * (i & 3))) & 0xffu;
+    store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, acc[i], nb);
+  }
+  if (wst) a.status[g] = 0;
+}
+
 // generic: any alignment / stride / d (<= 255); 4 columns per lane, byte I/O
 __device__ __forceinline__ uint32_t gfmul_var(uint32_t cbyte, uint32_t x) {
   uint32_t t = 0;
@@ -581,6 +678,13 @@ static void launch_apply_dm(const Batch& a, hipStream_t s) {
       hipLaunchKernelGGL((k_apply_p<DMAX, MODE, kApplyPNT, 1>), grid, block, 0, s, a);
       return;
     }
+  }
+  if (a.chunks >= 64 && a.epad <= 8) {  // wide codes: streaming inputs
+    if (a.epad == 4)
+      hipLaunchKernelGGL((k_apply_q<4, MODE, kApplyPNT, 1>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((k_apply_q<8, MODE, kApplyPNT, 1>), grid, block, 0, s, a);
+    return;
   }
   if (a.chunks >= 64 && a.epad == 4) {
     Batch b = a;
