@@ -43,8 +43,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, GB/s (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50,
+                    help="untimed steps; the clocks take ~20 ms of load to reach steady state")
     ap.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
     ap.add_argument("--total-groups", type=int, default=0, help="if set: strong scaling over this many groups")
     ap.add_argument("--data-shards", type=int, default=10)

@@ -57,6 +57,45 @@ static void build_table(int d, int p, uint32_t dpad, uint32_t epad, uint32_t str
   }
 }
 
+// Memory-pattern ceiling of the reconstruct: the wave-scalar descriptor
+// prologue, survivor loads and erased-row stores of k_apply_p, with the GF
+// arithmetic replaced by a plain XOR of the survivors (wrong values, same bytes).
+template <int NT>
+__global__ __launch_bounds__(256) void k_pattern_rec(Batch a) {
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (wfirst >= a.items) return;
+  const uint32_t wlast = min(wfirst + 63u, a.items - 1u);
+  const uint32_t gA = wfirst / a.chunks, gB = wlast / a.chunks;
+  const uint8_t* dA = desc_for<1>(a, a.g0 + gA);
+  const uint8_t* dB = desc_for<1>(a, a.g0 + gB);
+  const uint32_t hA = ld32(dA), hB = ld32(dB);
+  uint32_t rA[3], rB[3];
+  for (int w = 0; w < 3; ++w) { rA[w] = ld32(dA + 4 + 4 * w); rB[w] = ld32(dB + 4 + 4 * w); }
+  const uint32_t oA = ld32(dA + 4 + a.dpad), oB = ld32(dB + 4 + a.dpad);
+  if (item >= a.items) return;
+  const uint32_t gl = item / a.chunks;
+  const bool inB = gl != gA;
+  const uint32_t c = item - gl * a.chunks;
+  const uint32_t e = (inB ? hB : hA) & 0xffu;
+  uint8_t* gp = a.base + (a.g0 + gl) * a.gstride + static_cast<uint64_t>(c) * 16u;
+  const uint32_t nb = a.S - c * 16u;
+  V4 y{{0u, 0u, 0u, 0u}};
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
+    const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
+    xor4(y, load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride));
+  }
+  const uint32_t orows = inB ? oB : oA;
+  for (int i = 0; i < 4; ++i) {
+    if (i >= static_cast<int>(e)) continue;
+    const uint32_t r = (orows >> (8 * i)) & 0xffu;
+    y.v[0] += i;
+    store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, y, nb);
+  }
+}
+
 int main(int argc, char** argv) {
   const int d = 10, p = 3, n = 13;
   const uint32_t S = 1350, pitch = 1360;
@@ -126,7 +165,10 @@ int main(int argc, char** argv) {
       add(k_apply_w<10, 1, 3, 1>, b1, dec_bytes, "dec " + L + " nt3 wave-scalar-desc cpt1");
     }
         add(k_apply_p<10, 1, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick");
-    add(k_apply_q<4, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables streaming ring4 (k_apply_q)");
+    add(k_apply_p<10, 1, 1, 1, 1, 3, true>, b, dec_bytes, "dec " + L + " nt1 perm pair emax3");
+    add(k_apply_p<10, 1, 1, 1, 1, 3, false>, b, dec_bytes, "dec " + L + " nt1 perm single emax3");
+    add(k_pattern_rec<1>, b, dec_bytes, "dec " + L + " MEMORY PATTERN ONLY nt1 (xor, no GF)");
+    add(k_pattern_rec<3>, b, dec_bytes, "dec " + L + " MEMORY PATTERN ONLY nt3 (xor, no GF)");
     add(k_apply_p<12, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables dmax12");
     Batch bf = b;
     bf.present = masks_fixed;

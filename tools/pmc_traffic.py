@@ -57,6 +57,18 @@ def main():
     os.makedirs(dst, exist_ok=True)
     for f in glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True):
         shutil.copy(f, os.path.join(dst, "kernel_stats.csv"))
+    # per-dispatch durations: the bench's timed steps are the LAST `steps`
+    # dispatches of each kernel (the warmup dispatches before them run while
+    # the clocks ramp), so report that average beside rocprof's all-dispatch one
+    timed = {}
+    for f in glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True):
+        durs = defaultdict(list)
+        for row in csv.DictReader(open(f)):
+            k = kind(row["Kernel_Name"])
+            if k:
+                durs[(k, row["Kernel_Name"])].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+        for (k, name), v in durs.items():
+            timed[k] = {"kernel": name, "dispatches": len(v), "all_avg_ns": sum(v) / len(v)}
     bench = {}
     for f in glob.glob(os.path.join(src, "trace.bench.json")):
         lines = [ln for ln in open(f) if ln.strip().startswith("{")]
@@ -66,7 +78,18 @@ def main():
     G, d, p, S, e = (cfg.get(k) for k in ("groups_per_gpu", "data_shards", "parity_shards", "shard_size", "erasures"))
     pitch = cfg.get("pitch")
     alg = {"encode": G * (d + p) * S, "reconstruct": G * (d + e) * S} if G else {}
-    summary = {"tag": tag, "bench_config": cfg, "kernels": {}}
+    steps = bench.get("steps")
+    for f in glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True):
+        durs = defaultdict(list)
+        for row in csv.DictReader(open(f)):
+            k = kind(row["Kernel_Name"])
+            if k:
+                durs[k].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+        for k, v in durs.items():
+            if steps and len(v) >= steps:
+                timed[k]["timed_steps"] = steps
+                timed[k]["timed_avg_ns"] = sum(v[-steps:]) / steps
+    summary = {"tag": tag, "bench_config": cfg, "kernels": {}, "dispatch_durations": timed}
     merged = defaultdict(dict)
     for sub in ("fetch", "write", "sq"):
         for k, cs in counters(os.path.join(src, sub)).items():

@@ -293,37 +293,45 @@ __device__ __forceinline__ void p_sel(const V4& x, uint32_t* s0, uint32_t* s1, u
 // Inputs are taken in pairs so that the six table lookups of two products fold
 // into an accumulator with three xor3 (DMAX is even; a missing odd input is a
 // zero chunk, whose lookups are zero whatever the coefficient).
-template <int DMAX, int TSEL>
+template <int DMAX, int TSEL, int EMAX, bool PAIR>
 __device__ __forceinline__ void p_accum(V4* acc, const V4* x, const Batch& a, const uint8_t* dA,
                                         const uint8_t* dB, uint32_t mB, uint32_t emax) {
-  static_assert(DMAX % 2 == 0, "inputs are taken in pairs");
+  static_assert(DMAX % 2 == 0 || !PAIR, "inputs are taken in pairs");
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
+  for (int i = 0; i < EMAX; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
   const uint32_t cbase = 4 + a.dpad + a.epad;
+  constexpr int KS = PAIR ? 2 : 1;
 #pragma unroll
-  for (int k = 0; k < DMAX; k += 2) {
+  for (int k = 0; k < DMAX; k += KS) {
     if (k >= static_cast<int>(a.d)) continue;
     uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
     p_sel(x[k], s0, s1, s2);
-    p_sel(x[k + 1], r0, r1, r2);
+    if constexpr (PAIR) p_sel(x[k + 1], r0, r1, r2);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < EMAX; ++i) {
       if (i >= static_cast<int>(emax)) continue;
       const uint32_t off = cbase + i * a.dpad + (k & ~3);
       uint32_t t[5], u[5];
       p_tables<TSEL>(t, a, dA, dB, off, k, mB);
-      p_tables<TSEL>(u, a, dA, dB, off, k + 1, mB);
+      if constexpr (PAIR) {
+        p_tables<TSEL>(u, a, dA, dB, off, k + 1, mB);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t y = xor3(acc[i].v[j], perm(t[1], t[0], s0[j]), perm(t[3], t[2], s1[j]));
-        y = xor3(y, perm(0u, t[4], s2[j]), perm(u[1], u[0], r0[j]));
-        acc[i].v[j] = xor3(y, perm(u[3], u[2], r1[j]), perm(0u, u[4], r2[j]));
+        for (int j = 0; j < 4; ++j) {
+          uint32_t y = xor3(acc[i].v[j], perm(t[1], t[0], s0[j]), perm(t[3], t[2], s1[j]));
+          y = xor3(y, perm(0u, t[4], s2[j]), perm(u[1], u[0], r0[j]));
+          acc[i].v[j] = xor3(y, perm(u[3], u[2], r1[j]), perm(0u, u[4], r2[j]));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i].v[j] = xor3(acc[i].v[j], perm(t[1], t[0], s0[j]), perm(t[3], t[2], s1[j])) ^
+                        perm(0u, t[4], s2[j]);
       }
     }
   }
 }
 
-template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1>
+template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1, int EMAX = 4, bool PAIR = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_p(Batch a) {
   const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
@@ -377,14 +385,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       x[k] = V4{{0u, 0u, 0u, 0u}};
     }
   }
-  V4 acc[4];
+  V4 acc[EMAX];
   if (dA == dB)  // one descriptor for the whole wave: no per-lane table pick
-    p_accum<DMAX, 0>(acc, x, a, dA, dA, 0u, emax);
+    p_accum<DMAX, 0, EMAX, PAIR>(acc, x, a, dA, dA, 0u, emax);
   else
-    p_accum<DMAX, TSEL>(acc, x, a, dA, dB, mB, emax);
+    p_accum<DMAX, TSEL, EMAX, PAIR>(acc, x, a, dA, dB, mB, emax);
   const uint32_t orows = inB ? oB : oA;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < EMAX; ++i) {
     if (i >= static_cast<int>(e)) continue;
     const uint32_t r = (orows >> (8 * i)) & 0xffu;
     store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, acc[i], nb);
