@@ -192,12 +192,77 @@ def tx_case(G, reps, encrypt=True, full=True):
              "us": t * 1e6, "GBps": moved / t / 1e9, "Mpkt_per_s": G * n / t / 1e6}]
 
 
+def _uvarint_np(v, nbytes):
+    """v (uint64 array) as fixed-width uvarints of nbytes (continuation bits set)."""
+    out = np.zeros((v.size, nbytes), np.uint8)
+    for j in range(nbytes):
+        out[:, j] = ((v >> np.uint64(7 * j)) & np.uint64(0x7F)).astype(np.uint8)
+        if j < nbytes - 1:
+            out[:, j] |= 0x80
+    return out
+
+
+def pkt_case(npk, reps, ack_frac=0.25):
+    """Wire-codec decode (ugo_fec_packet_decode) of a batch of received,
+    FEC-framed, RC4-encrypted ugo data packets: 6-B FEC header, flags (PSH, a
+    quarter with a SACK), 3-byte packet number, one segment (4-byte offset,
+    BE16 length, 1400 data bytes).  Synthetic; parity is tests/test_packet_codec.py."""
+    slot = 1488
+    rng = np.random.default_rng(11)
+    host = rng.integers(0, 256, (npk, slot), dtype=np.uint8)
+    seq = np.arange(npk, dtype=np.uint64)
+    host[:, 0:4] = seq.astype("<u4").view(np.uint8).reshape(npk, 4)
+    host[:, 4] = 0xF1
+    host[:, 5] = 0
+    ack = rng.random(npk) < ack_frac
+    pos = np.full(npk, 6)
+    host[:, 6] = np.where(ack, 0xA0, 0x20)
+    pos += 1
+    # SACK without missing ranges: type 0, largest (3 B), delay (2 B), first block length (1 B)
+    sack = np.concatenate([np.zeros((npk, 1), np.uint8), _uvarint_np(seq + np.uint64(1 << 15), 3),
+                           np.full((npk, 2), 7, np.uint8), np.full((npk, 1), 5, np.uint8)], axis=1)
+    rows = np.nonzero(ack)[0]
+    host[rows[:, None], 7 + np.arange(7)[None, :]] = sack[rows]
+    pos[ack] += 7
+    pn = _uvarint_np(seq + np.uint64(1 << 15), 3)
+    seg = np.concatenate([_uvarint_np(seq * np.uint64(1400), 4),
+                          np.tile(np.array([[1400 >> 8, 1400 & 0xFF]], np.uint8), (npk, 1))], axis=1)
+    hdr = np.concatenate([pn, seg], axis=1)  # 9 bytes
+    for j in range(9):
+        host[np.arange(npk), pos + j] = hdr[:, j]
+    lens = (pos + 9 + 1400).astype(np.int16)
+    ks = np.frombuffer(fec.rc4_keystream(b"1234567890123456", slot), np.uint8)
+    host ^= ks[None, :]
+    enc = fec.New(10, 3)
+    d_pk = torch.from_numpy(host).cuda()
+    d_len = torch.from_numpy(lens).cuda()
+    pad = torch.from_numpy(ks.copy()).cuda()
+    info, _, _ = enc.packet_decode(d_pk, d_len, pad=pad, framed=True, max_ranges=4, max_segments=2)
+    torch.cuda.synchronize()
+    st = info.cpu().numpy().view(fec.PKT_INFO_DTYPE).reshape(-1)
+    assert (st["status"] == 0).all() and (st["n_segments"] == 1).all(), "synthetic packets must decode"
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    s = torch.cuda.current_stream()
+    e[0].record(s)
+    for _ in range(reps):
+        enc.packet_decode(d_pk, d_len, pad=pad, framed=True, max_ranges=4, max_segments=2)
+    e[1].record(s)
+    torch.cuda.synchronize()
+    t = e[0].elapsed_time(e[1]) / reps * 1e-3
+    return [{"case": "packet decode (FEC-framed, RC4, 1 segment, 25% SACK)", "packets": npk, "us": t * 1e6,
+             "Mpkt_per_s": npk / t / 1e6, "out_bytes_per_pkt": 64 + 4 * 16 + 2 * 16}]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     res = []
+    if args.only == "pkt":
+        for r in pkt_case(851968, args.reps):
+            print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
+        return
     res += tx_case(65536, args.reps)
     res += tx_case(65536, args.reps, full=False)
     res += tx_case(65536, args.reps, encrypt=False)

@@ -22,6 +22,7 @@
 #include "host/rc4.hpp"
 #include "rx_kernels.hpp"
 #include "tx_kernels.hpp"
+#include "pkt_kernels.hpp"
 
 namespace {
 
@@ -604,6 +605,35 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
     if (st != UGO_FEC_OK) return st;
   }
   return UGO_FEC_OK;
+}
+
+int ugo_fec_packet_decode(ugo_fec* c, const uint8_t* pkts, size_t slot, const uint16_t* lens, size_t npk,
+                          const uint8_t* pad, unsigned flags, ugo_pkt_info* info, uint64_t* ranges,
+                          size_t max_ranges, ugo_pkt_segment* segs, size_t max_segments, void* stream) {
+  static_assert(sizeof(ugo_pkt_info) == 64, "ugo_pkt_info is 64 bytes");
+  static_assert(sizeof(ugo_pkt_segment) == 16, "ugo_pkt_segment is 16 bytes");
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (npk == 0) return UGO_FEC_OK;
+  if (!pkts || !lens || !info || slot % 16 || slot == 0 || slot > 0xffff ||
+      reinterpret_cast<uintptr_t>(pkts) % 16 || (pad && reinterpret_cast<uintptr_t>(pad) % 16) ||
+      (max_ranges && !ranges) || (max_segments && !segs) || max_ranges > 0xffff || max_segments > 0xffff ||
+      (flags & ~UGO_PKT_FEC_FRAMED))
+    return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  ugo::kern::PktArgs a{};
+  a.pkts = pkts;
+  a.lens = lens;
+  a.pad = pad;
+  a.info = info;
+  a.ranges = ranges;
+  a.segs = segs;
+  a.npk = npk;
+  a.slot = slot;
+  a.max_ranges = static_cast<uint32_t>(max_ranges);
+  a.max_segments = static_cast<uint32_t>(max_segments);
+  a.framed = flags & UGO_PKT_FEC_FRAMED;
+  return hip_status(ugo::kern::launch_packet_decode(a, static_cast<hipStream_t>(stream)));
 }
 
 int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size_t n) {

@@ -39,6 +39,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libugofec.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ugo_fec.h")
 CONN_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ugo_fec_conn.h")
+PKT_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ugo_pkt.h")
 
 OK = 0
 RECONSTRUCT_DATA_ONLY = 1
@@ -89,6 +90,15 @@ _ERRORS = {c.code: c for c in (ErrInvShardNum, ErrMaxShardNum, ErrTooFewShards, 
 
 _lib = None
 
+# include/ugo_pkt.h
+PKT_FEC_FRAMED = 1
+PKT_INFO_DTYPE = np.dtype([("packet_number", "<u8"), ("stop_waiting", "<u8"), ("largest_acked", "<u8"),
+                           ("largest_in_order", "<u8"), ("delay_us", "<u8"), ("status", "<u4"),
+                           ("payload_off", "<u4"), ("n_ranges", "<u2"), ("n_segments", "<u2"), ("flags", "u1"),
+                           ("fec_flag_lo", "u1"), ("reserved", "u1", (10,))])
+PKT_SEGMENT_DTYPE = np.dtype([("offset", "<u8"), ("data_off", "<u4"), ("len", "<u2"), ("avail", "<u2")])
+assert PKT_INFO_DTYPE.itemsize == 64 and PKT_SEGMENT_DTYPE.itemsize == 16
+
 
 def load_library(path: str = LIB_PATH):
     """Load libugofec.so.  Raises loudly if it was not built (no fallback)."""
@@ -119,12 +129,13 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_rx_assemble.argtypes = [vp, vp, sz, vp, sz, vp, ctypes.c_uint64, sz, vp, sz, sz, sz, vp, vp, vp]
     lib.ugo_fec_rc4_keystream.argtypes = [vp, sz, vp, sz]
     lib.ugo_fec_tx_assemble.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp, vp]
+    lib.ugo_fec_packet_decode.argtypes = [vp, vp, sz, vp, sz, vp, u, vp, vp, sz, vp, sz, vp]
     _lib = lib
     return lib
 
 
-def header_symbols(paths=(HEADER_PATH, CONN_HEADER_PATH)) -> List[str]:
-    """Every entry point declared in include/ugo_fec.h and include/ugo_fec_conn.h."""
+def header_symbols(paths=(HEADER_PATH, CONN_HEADER_PATH, PKT_HEADER_PATH)) -> List[str]:
+    """Every entry point declared in include/ugo_fec.h, ugo_fec_conn.h and ugo_pkt.h."""
     out = set()
     for path in paths:
         src = open(path).read()
@@ -258,6 +269,24 @@ class Encoder:
             self._h, pkts.data_ptr(), slot_in, lens.data_ptr(), G, first_seq,
             None if pad is None else pad.data_ptr(), max_len, wire.data_ptr(), wire.shape[1],
             wire_lens.data_ptr(), None if status is None else status.data_ptr(), _stream_handle(stream)))
+
+    def packet_decode(self, pkts, lens, pad=None, framed: bool = False, max_ranges: int = 32,
+                      max_segments: int = 8, stream=None):
+        """Batch ugoPacket.decode (include/ugo_pkt.h): pkts = uint8 CUDA [npk, slot],
+        lens = int16/uint16 CUDA [npk].  Returns CUDA tensors (info [npk, 64] bytes --
+        view on the host with PKT_INFO_DTYPE --, ranges int64 [npk, max_ranges, 2],
+        segs [npk, max_segments, 16] bytes -- PKT_SEGMENT_DTYPE)."""
+        npk, slot = pkts.shape
+        assert pkts.is_contiguous() and lens.is_contiguous() and lens.element_size() == 2 and lens.numel() == npk
+        dev = pkts.device
+        info = torch.empty((npk, 64), dtype=torch.uint8, device=dev)
+        ranges = torch.zeros((npk, max(max_ranges, 1), 2), dtype=torch.int64, device=dev)
+        segs = torch.zeros((npk, max(max_segments, 1), 16), dtype=torch.uint8, device=dev)
+        _raise(load_library().ugo_fec_packet_decode(
+            self._h, pkts.data_ptr(), slot, lens.data_ptr(), npk, None if pad is None else pad.data_ptr(),
+            PKT_FEC_FRAMED if framed else 0, info.data_ptr(), ranges.data_ptr(), max_ranges, segs.data_ptr(),
+            max_segments, _stream_handle(stream)))
+        return info, ranges, segs
 
     # ------------------------------------------------------ host-buffer batch
     def encode_host(self, shards: np.ndarray, shard_size: Optional[int] = None):
