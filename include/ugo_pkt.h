@@ -35,7 +35,7 @@ typedef enum ugo_pkt_status {
   UGO_PKT_VARINT_OVERFLOW = 3,         /* "binary: varint overflows a 64-bit integer" */
   UGO_PKT_INVALID_ACK_RANGES = 4,      /* errInvalidAckRanges (ugo/packet.go:42) */
   UGO_PKT_INVALID_FIRST_ACK_RANGE = 5, /* errInvalidFirstAckRange (ugo/packet.go:44) */
-  UGO_PKT_CAPACITY = 6                 /* more ACK ranges / segments than the caller's arrays hold */
+  UGO_PKT_CAPACITY = 6                 /* decoded OK, but more ACK ranges / segments than the caller's arrays hold */
 } ugo_pkt_status;
 
 /* Decoded fixed fields of one packet (64 bytes). */
@@ -47,8 +47,8 @@ typedef struct ugo_pkt_info {
   uint64_t delay_us;         /* ufloat16-decoded delay, microseconds */
   uint32_t status;           /* ugo_pkt_status */
   uint32_t payload_off;      /* where the ugoPacket starts in the slot (0, or 6 after a typeData FEC header) */
-  uint16_t n_ranges;         /* ACK ranges in ranges[i*max_ranges ...] */
-  uint16_t n_segments;       /* segments in segs[i*max_segments ...] */
+  uint16_t n_ranges;         /* ACK ranges stored in ranges[i*max_ranges ...] */
+  uint16_t n_segments;       /* segments stored in segs[i*max_segments ...] */
   uint8_t flags;             /* ugoPacket flags byte */
   uint8_t fec_flag_lo;       /* low byte of the FEC header flag (framed mode), else 0 */
   uint8_t reserved[10];
@@ -72,8 +72,10 @@ typedef struct ugo_pkt_segment {
  * slots), lens[i] bytes.  pad (nullable, >= slot bytes) is XORed over each
  * packet from byte 0 first (the fixed-key RC4 Decrypt, ugo/conn.go:390).
  * info[npackets]; ranges[npackets][max_ranges][2] = {first, last} packet
- * numbers, highest range first; segs[npackets][max_segments].  A packet whose
- * ranges or segments exceed the caps gets UGO_PKT_CAPACITY.  Returns a
+ * numbers, highest range first; segs[npackets][max_segments].  A packet that
+ * decodes without error but has more ranges or segments than the caps gets
+ * UGO_PKT_CAPACITY (the first max_* are stored); a packet the reference would
+ * reject gets the reference's error whatever its size.  Returns a
  * ugo_fec_status (argument / launch errors); per-packet results are in info. */
 int ugo_fec_packet_decode(ugo_fec* ctx, const uint8_t* pkts, size_t slot, const uint16_t* lens, size_t npackets,
                           const uint8_t* pad, unsigned flags, ugo_pkt_info* info, uint64_t* ranges,

@@ -173,7 +173,12 @@ def _check(pk, info, ranges, segs, framed=False, max_ranges=32, max_segments=8):
         if st == pr.PKT_OK:
             nr = len(out["sack"]["ranges"]) if out["sack"] else 0
             if nr > max_ranges or len(out["segments"]) > max_segments:
-                assert I["status"] == 6, i  # UGO_PKT_CAPACITY
+                assert I["status"] == 6, i  # UGO_PKT_CAPACITY: the first max_* are stored
+                assert I["n_ranges"] == min(nr, max_ranges) and I["n_segments"] == min(len(out["segments"]),
+                                                                                        max_segments)
+                if out["sack"] is not None:
+                    k = min(nr, max_ranges)
+                    assert [tuple(x) for x in ranges[i, :k]] == out["sack"]["ranges"][:k], i
                 continue
         assert I["status"] == st, f"packet {i} {b.hex()}: status {I['status']} vs {st}"
         if st != pr.PKT_OK:

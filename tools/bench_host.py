@@ -237,7 +237,8 @@ def pkt_case(npk, reps, ack_frac=0.25):
     d_pk = torch.from_numpy(host).cuda()
     d_len = torch.from_numpy(lens).cuda()
     pad = torch.from_numpy(ks.copy()).cuda()
-    info, _, _ = enc.packet_decode(d_pk, d_len, pad=pad, framed=True, max_ranges=4, max_segments=2)
+    bufs = enc.packet_decode(d_pk, d_len, pad=pad, framed=True, max_ranges=4, max_segments=2)
+    info = bufs[0]
     torch.cuda.synchronize()
     st = info.cpu().numpy().view(fec.PKT_INFO_DTYPE).reshape(-1)
     assert (st["status"] == 0).all() and (st["n_segments"] == 1).all(), "synthetic packets must decode"
@@ -245,7 +246,7 @@ def pkt_case(npk, reps, ack_frac=0.25):
     s = torch.cuda.current_stream()
     e[0].record(s)
     for _ in range(reps):
-        enc.packet_decode(d_pk, d_len, pad=pad, framed=True, max_ranges=4, max_segments=2)
+        enc.packet_decode(d_pk, d_len, pad=pad, framed=True, max_ranges=4, max_segments=2, out=bufs)
     e[1].record(s)
     torch.cuda.synchronize()
     t = e[0].elapsed_time(e[1]) / reps * 1e-3

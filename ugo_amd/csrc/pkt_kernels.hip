@@ -97,8 +97,12 @@ __device__ __forceinline__ uint32_t read_ufloat16(ByteReader& r, uint64_t& v) {
   return kOK;
 }
 
-// parseSack + validateAckRanges.  Ranges go straight to the output row.
-__device__ uint32_t parse_sack(ByteReader& r, ugo_pkt_info& o, uint64_t* rg, uint32_t cap, uint32_t& nr) {
+// parseSack + validateAckRanges, streaming: a range is final once the next
+// one starts (only the last range is ever modified or dropped, ugo/packet.go:
+// 285-306), so it is validated against its predecessor and stored then.
+// Ranges beyond the caller's cap are validated but not stored (`over`).
+// Returns a hard error, or OK with `over` telling whether ranges were dropped.
+__device__ uint32_t parse_sack(ByteReader& r, ugo_pkt_info& o, uint64_t* rg, uint32_t cap, bool& over) {
   uint32_t type_byte;
   uint32_t st = read_byte(r, type_byte);
   if (st) return st;
@@ -116,17 +120,27 @@ __device__ uint32_t parse_sack(ByteReader& r, ugo_pkt_info& o, uint64_t* rg, uin
   if ((st = read_uvarint(r, blen))) return st;
   if (blen < 1) return kInvalidFirst;
   if (blen > largest) return kInvalidRanges;
-  nr = 0;
   if (!has_missing) {
     o.largest_in_order = largest + 1 - blen;
     return kOK;
   }
-  // ranges live in the caller's row; one beyond the cap is tracked in
-  // registers (cur) so the last-range fixups work before the cap check
   uint64_t cf = largest - blen + 1, cl = largest;  // current (last) range
-  uint32_t n = 1;                                    // ranges so far, cur included
+  uint64_t pf = 0;                                  // first of the last final range
+  uint32_t nfinal = 0;
+  bool invalid = false;
+  auto finalize = [&](uint64_t f, uint64_t l) {
+    if (f > l) invalid = true;
+    if (nfinal > 0 && (pf <= f || pf <= l + 1)) invalid = true;
+    if (nfinal < cap) {
+      rg[2 * nfinal] = f;
+      rg[2 * nfinal + 1] = l;
+    } else {
+      over = true;
+    }
+    pf = f;
+    ++nfinal;
+  };
   bool in_long = false, last_complete = false;
-  bool over = false;
   for (uint32_t i = 0; i < nblocks; ++i) {
     uint32_t gap;
     if ((st = read_byte(r, gap))) return st;
@@ -136,47 +150,19 @@ __device__ uint32_t parse_sack(ByteReader& r, ugo_pkt_info& o, uint64_t* rg, uin
       cl -= gap;
     } else {
       last_complete = false;
-      // retire cur to the output row, start a new one
-      if (n - 1 < cap) {
-        rg[2 * (n - 1)] = cf;
-        rg[2 * (n - 1) + 1] = cl;
-      } else {
-        over = true;
-      }
-      const uint64_t last = cf - gap - 1;
-      cl = last;
-      cf = last - blen + 1;
-      ++n;
+      finalize(cf, cl);
+      cl = cf - gap - 1;
+      cf = cl - blen + 1;
     }
     if (blen > 0) last_complete = true;
     in_long = blen == 0;
   }
-  if (!last_complete) {
-    // drop cur: the previous range (in the row) becomes the last one
-    --n;
-    if (n - 1 < cap) {
-      cf = rg[2 * (n - 1)];
-      cl = rg[2 * (n - 1) + 1];
-    }
-  } else if (n - 1 < cap) {
-    rg[2 * (n - 1)] = cf;
-    rg[2 * (n - 1) + 1] = cl;
-  } else {
-    over = true;
-  }
-  if (over || n > cap) return kCapacity;
-  nr = n;
-  o.largest_in_order = rg[2 * (n - 1)];
-  // validateAckRanges (len >= 1 here)
-  if (n == 1) return kInvalidRanges;
-  if (rg[1] != largest) return kInvalidRanges;
-  for (uint32_t i = 0; i < n; ++i)
-    if (rg[2 * i] > rg[2 * i + 1]) return kInvalidRanges;
-  for (uint32_t i = 1; i < n; ++i) {
-    const uint64_t pf = rg[2 * (i - 1)];
-    if (pf <= rg[2 * i]) return kInvalidRanges;
-    if (pf <= rg[2 * i + 1] + 1) return kInvalidRanges;
-  }
+  if (last_complete) finalize(cf, cl);  // else the last range is dropped
+  o.n_ranges = static_cast<uint16_t>(min(nfinal, cap));
+  o.largest_in_order = pf;
+  // validateAckRanges: >= 2 ranges; range 0 ends at largest (it is never
+  // modified after it is final, so this holds by construction)
+  if (nfinal == 1 || invalid) return kInvalidRanges;
   return kOK;
 }
 
@@ -186,10 +172,9 @@ __device__ uint32_t decode_one(ByteReader& r, ugo_pkt_info& o, uint64_t* rg, uin
   uint32_t st = read_byte(r, flags);
   if (st) return st;
   o.flags = static_cast<uint8_t>(flags);
+  bool over = false;  // more ranges / segments than the caller's arrays hold
   if (flags & 0x80u) {
-    uint32_t nr = 0;
-    st = parse_sack(r, o, rg, rcap, nr);
-    o.n_ranges = static_cast<uint16_t>(nr);
+    st = parse_sack(r, o, rg, rcap, over);
     if (st) return st;
   }
   if (flags != 0x80u && (st = read_uvarint(r, o.packet_number))) return st;
@@ -210,11 +195,15 @@ __device__ uint32_t decode_one(ByteReader& r, ugo_pkt_info& o, uint64_t* rg, uin
       avail = min(len, r.left());
       r.pos += avail;
     }
-    if (ns >= scap) return kCapacity;
-    sg[ns] = ugo_pkt_segment{off, data_off, static_cast<uint16_t>(len), static_cast<uint16_t>(avail)};
-    o.n_segments = static_cast<uint16_t>(++ns);
+    if (ns < scap) {
+      sg[ns] = ugo_pkt_segment{off, data_off, static_cast<uint16_t>(len), static_cast<uint16_t>(avail)};
+      o.n_segments = static_cast<uint16_t>(ns + 1);
+    } else {
+      over = true;
+    }
+    ++ns;
   }
-  return kOK;
+  return over ? kCapacity : kOK;
 }
 
 __global__ __launch_bounds__(256) void k_packet_decode(PktArgs a) {

@@ -271,7 +271,7 @@ class Encoder:
             wire_lens.data_ptr(), None if status is None else status.data_ptr(), _stream_handle(stream)))
 
     def packet_decode(self, pkts, lens, pad=None, framed: bool = False, max_ranges: int = 32,
-                      max_segments: int = 8, stream=None):
+                      max_segments: int = 8, stream=None, out=None):
         """Batch ugoPacket.decode (include/ugo_pkt.h): pkts = uint8 CUDA [npk, slot],
         lens = int16/uint16 CUDA [npk].  Returns CUDA tensors (info [npk, 64] bytes --
         view on the host with PKT_INFO_DTYPE --, ranges int64 [npk, max_ranges, 2],
@@ -279,9 +279,14 @@ class Encoder:
         npk, slot = pkts.shape
         assert pkts.is_contiguous() and lens.is_contiguous() and lens.element_size() == 2 and lens.numel() == npk
         dev = pkts.device
-        info = torch.empty((npk, 64), dtype=torch.uint8, device=dev)
-        ranges = torch.zeros((npk, max(max_ranges, 1), 2), dtype=torch.int64, device=dev)
-        segs = torch.zeros((npk, max(max_segments, 1), 16), dtype=torch.uint8, device=dev)
+        if out is not None:  # reuse (info, ranges, segs) from an earlier call
+            info, ranges, segs = out
+            assert info.shape == (npk, 64) and ranges.shape[0] == npk and segs.shape[0] == npk
+            assert ranges.shape[1] >= max(max_ranges, 1) and segs.shape[1] >= max(max_segments, 1)
+        else:
+            info = torch.empty((npk, 64), dtype=torch.uint8, device=dev)
+            ranges = torch.zeros((npk, max(max_ranges, 1), 2), dtype=torch.int64, device=dev)
+            segs = torch.zeros((npk, max(max_segments, 1), 16), dtype=torch.uint8, device=dev)
         _raise(load_library().ugo_fec_packet_decode(
             self._h, pkts.data_ptr(), slot, lens.data_ptr(), npk, None if pad is None else pad.data_ptr(),
             PKT_FEC_FRAMED if framed else 0, info.data_ptr(), ranges.data_ptr(), max_ranges, segs.data_ptr(),
