@@ -260,6 +260,10 @@ def main():
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     res = []
+    if args.only == "jumbo":
+        for r in device_case(32, 8, 9000, 8192, 8, args.reps):
+            print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
+        return
     if args.only == "pkt":
         for r in pkt_case(851968, args.reps):
             print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))

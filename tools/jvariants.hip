@@ -1,0 +1,140 @@
+// A/B timing of jumbo (32+8)x9000 kernel variants, planar layout, 8192 groups.
+// Not product code: includes the kernel TU.  One JSON line per variant.
+#include "../ugo_amd/csrc/fec_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+using namespace ugo;
+using namespace ugo::kern;
+
+int main(int argc, char** argv) {
+  const int d = 32, p = 8, n = 40;
+  const uint32_t S = 9000, pitch = 9008;
+  const uint64_t G = argc > 1 ? atoll(argv[1]) : 8192;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 9;
+  const uint32_t dpad = 32, epad = 8, stride = ((4 + dpad + epad + p * dpad + 15) / 16 * 16);
+  uint8_t* buf;
+  CK(hipMalloc(&buf, G * n * pitch));
+  std::vector<uint8_t> h(G * n * pitch);
+  uint64_t st = 0x5EED;
+  for (auto& b : h) { st = st * 6364136223846793005ull + 1442695040888963407ull; b = st >> 56; }
+  CK(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
+  // matrix, encode descriptor, perm tables, gf tables
+  std::vector<uint8_t> M(n * d), scratch(n * d + 3 * d * d);
+  gf::build_matrix(d, p, M.data(), scratch.data());
+  std::vector<uint8_t> ed(stride + 64, 0);
+  ed[0] = p;
+  for (int i = 0; i < d; ++i) ed[4 + i] = i;
+  for (int i = 0; i < p; ++i) ed[4 + dpad + i] = d + i;
+  for (int i = 0; i < p; ++i)
+    for (int k = 0; k < d; ++k) ed[4 + dpad + epad + i * dpad + k] = M[(d + i) * d + k];
+  std::vector<uint8_t> gfv(1024 + 8192, 0);
+  memcpy(gfv.data(), gf::kTables.exp, 512);
+  memcpy(gfv.data() + 512, gf::kTables.log, 256);
+  gf::perm_tables(gfv.data() + 1024);
+  uint8_t *d_ed, *d_gf, *d_M, *d_work;
+  uint64_t* masks;
+  CK(hipMalloc(&d_ed, ed.size()));
+  CK(hipMalloc(&d_gf, gfv.size()));
+  CK(hipMalloc(&d_M, M.size()));
+  CK(hipMalloc(&d_work, G * stride + 64));
+  CK(hipMalloc(&masks, G * 8));
+  CK(hipMemcpy(d_ed, ed.data(), ed.size(), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_gf, gfv.data(), gfv.size(), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_M, M.data(), M.size(), hipMemcpyHostToDevice));
+  // mixed erasures e ~ U[0,8], positions uniform among the 40 shards
+  std::vector<uint64_t> hm(G);
+  double dec_rows = 0;
+  for (uint64_t g = 0; g < G; ++g) {
+    st = st * 6364136223846793005ull + 1442695040888963407ull;
+    int e = (st >> 33) % 9;
+    uint64_t m = (1ull << n) - 1;
+    while (__builtin_popcountll(((1ull << n) - 1) & ~m) < e) {
+      st = st * 6364136223846793005ull + 1442695040888963407ull;
+      m &= ~(1ull << ((st >> 33) % n));
+    }
+    hm[g] = m;
+    dec_rows += d + e;
+  }
+  CK(hipMemcpy(masks, hm.data(), G * 8, hipMemcpyHostToDevice));
+  Batch a{};
+  a.base = buf; a.gstride = pitch; a.rstride = G * pitch; a.nmask = (1ull << n) - 1; a.S = S;
+  a.chunks = (S + 15) / 16; a.items = G * a.chunks; a.desc_stride = stride; a.d = d;
+  a.dpad = dpad; a.epad = epad; a.mult = reinterpret_cast<const uint32_t*>(d_gf + 1024);
+  Batch ae = a;  // MODE 0: encode through the descriptor kernels
+  ae.desc = d_ed;
+  Batch ar = a;  // MODE 2: per-group descriptors
+  ar.desc = d_work; ar.present = masks; ar.g_desc0 = 0;
+  Prep pr{};
+  pr.desc = d_work; pr.present = masks; pr.M = d_M; pr.gf_exp = d_gf; pr.gf_log = d_gf + 512; pr.g0 = 0;
+  pr.g_desc0 = 0; pr.nmask = a.nmask; pr.desc_stride = stride; pr.d = d; pr.n = n; pr.dpad = dpad; pr.epad = epad;
+  CK(launch_prepare(pr, G, 0));
+  CK(hipDeviceSynchronize());
+  const double enc_bytes = double(G) * n * S, dec_bytes = dec_rows * S;
+  const uint32_t grid = (a.items + 255) / 256;
+  struct Var { std::string name; double bytes; std::function<void()> go; std::vector<float> t; };
+  std::vector<Var> vars;
+  auto add = [&](auto kern, const Batch& b, double bytes, std::string nm) {
+    vars.push_back({nm, bytes, [=]() { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, b); }, {}});
+  };
+  add(k_encode_c<32, 8, 1>, a, enc_bytes, "enc const-network nt1 (production)");
+  add(k_encode_c<32, 8, 3>, a, enc_bytes, "enc const-network nt3");
+  add(k_apply_q<8, 0, 1, 1, 4>, ae, enc_bytes, "enc perm-tables streaming ring4 nt1");
+  add(k_apply_q<8, 0, 1, 1, 8>, ae, enc_bytes, "enc perm-tables streaming ring8 nt1");
+  add(k_apply_q<8, 2, 1, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt1 (production)");
+  add(k_apply_q<8, 2, 1, 1, 8>, ar, dec_bytes, "dec perm streaming ring8 nt1");
+  add(k_apply_q<8, 2, 3, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt3");
+  add(k_apply_q<8, 2, 0, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt0");
+  add(k_apply<32, 2, 3>, ar, dec_bytes, "dec masked-horner k_apply nt3 (before)");
+  vars.push_back({"k_prepare (8192 groups)", 0.0, [=]() { launch_prepare(pr, G, 0); }, {}});
+  // encode variants must agree: run const then perm encode over the same data
+  auto same_rows = [&](const std::vector<uint8_t>& x, const std::vector<uint8_t>& y) {  // bytes [0, S) only
+    for (uint64_t r = 0; r < uint64_t(n); ++r)
+      for (uint64_t g = 0; g < G; ++g)
+        if (memcmp(&x[r * a.rstride + g * pitch], &y[r * a.rstride + g * pitch], S)) return false;
+    return true;
+  };
+  {
+    std::vector<uint8_t> h1(h.size()), h2(h.size());
+    vars[0].go();
+    CK(hipMemcpy(h1.data(), buf, h.size(), hipMemcpyDeviceToHost));
+    CK(hipMemset(buf + size_t(d) * a.rstride, 0, size_t(p) * a.rstride));
+    vars[2].go();
+    CK(hipMemcpy(h2.data(), buf, h.size(), hipMemcpyDeviceToHost));
+    printf("{\"check\":\"perm encode == const encode\",\"equal\":%s}\n", same_rows(h1, h2) ? "true" : "false");
+    std::vector<uint8_t> h3(h.size());
+    vars[4].go();  // reconstruct of a consistent batch rewrites erased rows with the same bytes
+    CK(hipMemcpy(h3.data(), buf, h.size(), hipMemcpyDeviceToHost));
+    printf("{\"check\":\"reconstruct of codewords is idempotent\",\"equal\":%s}\n", same_rows(h3, h1) ? "true" : "false");
+    fflush(stdout);
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (auto& v : vars) v.go();
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < rounds; ++r)
+    for (auto& v : vars) {
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < 3; ++i) v.go();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.t.push_back(ms / 3);
+    }
+  for (auto& v : vars) {
+    std::sort(v.t.begin(), v.t.end());
+    const float med = v.t[v.t.size() / 2];
+    printf("{\"variant\":\"%s\",\"median_us\":%.2f,\"min_us\":%.2f,\"GBps\":%.1f}\n", v.name.c_str(), med * 1e3,
+           v.t[0] * 1e3, v.bytes / (med * 1e-3) / 1e9);
+  }
+  return 0;
+}

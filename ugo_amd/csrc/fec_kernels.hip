@@ -405,8 +405,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // chunks is loaded ahead while the current pair is folded into EMAX live
 // accumulators -- so registers hold 4*EMAX accumulator dwords plus the ring,
 // independent of d (vs k_apply's d-sized input block and masked Horner).
-template <int EMAX, int MODE, int NT, int TSEL = 1>
+template <int EMAX, int MODE, int NT, int TSEL = 1, int RING = 4>
 __global__ __launch_bounds__(256) void k_apply_q(Batch a) {
+  static_assert(RING % 2 == 0, "inputs are consumed in pairs");
   const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
   if (wfirst >= a.items) return;
@@ -447,30 +448,30 @@ __global__ __launch_bounds__(256) void k_apply_q(Batch a) {
   V4 acc[EMAX];
 #pragma unroll
   for (int i = 0; i < EMAX; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
-  V4 ring[4];
+  V4 ring[RING];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) ring[j] = load_in(j);
+  for (int j = 0; j < RING; ++j) ring[j] = load_in(j);
   const uint32_t cbase = 4 + a.dpad + a.epad;
-  for (uint32_t k0 = 0; k0 < a.d; k0 += 4) {
+  for (uint32_t k0 = 0; k0 < a.d; k0 += RING) {
 #pragma unroll
-    for (int j = 0; j < 4; j += 2) {
+    for (int j = 0; j < RING; j += 2) {
       const uint32_t k = k0 + j;
       uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
       p_sel(ring[j], s0, s1, s2);
       p_sel(ring[j + 1], r0, r1, r2);
-      ring[j] = load_in(k + 4);
-      ring[j + 1] = load_in(k + 5);
+      ring[j] = load_in(k + RING);
+      ring[j + 1] = load_in(k + RING + 1);
 #pragma unroll
       for (int i = 0; i < EMAX; ++i) {
         if (i >= static_cast<int>(emax)) continue;
-        const uint32_t off = cbase + i * a.dpad + k0;  // coefficient word of inputs k0..k0+3
+        const uint32_t off = cbase + i * a.dpad + (k & ~3u);  // coefficient word of inputs k, k+1
         uint32_t t[5], u[5];
         if (dS) {
-          p_tables<0>(t, a, dS, dS, off, j, 0u);
-          p_tables<0>(u, a, dS, dS, off, j + 1, 0u);
+          p_tables<0>(t, a, dS, dS, off, j & 3, 0u);
+          p_tables<0>(u, a, dS, dS, off, (j & 3) + 1, 0u);
         } else {
-          p_tables<TSEL>(t, a, dA, dB, off, j, mB);
-          p_tables<TSEL>(u, a, dA, dB, off, j + 1, mB);
+          p_tables<TSEL>(t, a, dA, dB, off, j & 3, mB);
+          p_tables<TSEL>(u, a, dA, dB, off, (j & 3) + 1, mB);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -551,16 +552,26 @@ __device__ __forceinline__ uint8_t lmul(const uint8_t* lg, const uint8_t* ex, ui
   return (a && b) ? ex[lg[a] + lg[b]] : 0;
 }
 
+// One wave per group.  The survivors are the first d present rows: the
+// present data rows P (identity rows of M) then the first e_d present parity
+// rows J, where e_d = number of erased data rows E.  So the d x d inverse
+// reduces to the e_d x e_d block B = M[J][E]:
+//     x_E = B^-1 (y_J + M[J][P] y_P)          (GF(2^8): minus is plus)
+//   Dinv[E_l][pos(J_i)] = Binv[l][i],  Dinv[E_l][pos(P_m)] = sum_i Binv[l][i] M[J_i][P_m]
+// and an erased parity row r gets M[r]·Dinv:
+//   coef[pos(P_m)] = M[r][P_m] + sum_l M[r][E_l] Dinv[E_l][pos],  coef[pos(J_i)] = sum_l M[r][E_l] Binv[l][i]
+// The same linear map as the full Gauss-Jordan of klauspost's Reconstruct
+// (exact arithmetic), at e_d^3 + e_d^2 d instead of d^3 work.
 __global__ __launch_bounds__(64) void k_prepare(Prep a) {
   __shared__ uint8_t ex[512];
   __shared__ uint8_t lg[256];
-  __shared__ uint8_t A[63 * 126];
-  __shared__ uint8_t fcol[64];
-  __shared__ uint8_t surv[64];
-  __shared__ uint8_t outr[64];
+  __shared__ uint8_t Ba[32 * 64];  // [B | I], e_d <= min(d, p) <= 32 since d + p <= 64
+  __shared__ uint8_t DE[32 * 64];  // Dinv rows of the erased data rows, over survivor positions
+  __shared__ uint8_t fcol[32];
+  __shared__ uint8_t surv[64], outr[64], Pl[64], El[64], Jl[64];
   const uint32_t lane = threadIdx.x;
   const uint64_t g = a.g0 + blockIdx.x;
-  const uint32_t d = a.d, n = a.n, w = 2 * d;
+  const uint32_t d = a.d, n = a.n;
   for (uint32_t i = lane; i < 512; i += 64) ex[i] = a.gf_exp[i];
   for (uint32_t i = lane; i < 256; i += 64) lg[i] = a.gf_log[i];
   const uint64_t mask = a.present[g] & a.nmask;
@@ -573,29 +584,34 @@ __global__ __launch_bounds__(64) void k_prepare(Prep a) {
     }
     return;
   }
-  // survivors and erased rows (one candidate row per lane, n <= 64)
+  const uint64_t dmask = (d >= 64) ? ~0ull : ((1ull << d) - 1);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  if (lane < n) {
-    if ((mask >> lane) & 1ull) {
-      const uint32_t rank = __popcll(mask & below);
-      if (rank < d) surv[rank] = static_cast<uint8_t>(lane);
-    } else {
-      const uint32_t er = __popcll(~mask & a.nmask & below);
-      outr[er] = static_cast<uint8_t>(lane);
-    }
-  }
-  __syncthreads();
   const uint32_t e = n - np;
-  const uint32_t e_data = __popcll(~mask & ((d >= 64) ? ~0ull : ((1ull << d) - 1)));
-  // A = [M[surv] | I]
-  for (uint32_t idx = lane; idx < d * w; idx += 64) {
-    const uint32_t r = idx / w, col = idx - r * w;
-    A[idx] = col < d ? a.M[surv[r] * d + col] : static_cast<uint8_t>(col - d == r ? 1 : 0);
+  const uint32_t ed = __popcll(~mask & dmask);  // erased data rows
+  const uint32_t npd = d - ed;                  // present data rows
+  if (lane < n) {
+    const bool present = (mask >> lane) & 1ull;
+    if (lane < d) {
+      if (present) Pl[__popcll(mask & dmask & below)] = static_cast<uint8_t>(lane);
+      else El[__popcll(~mask & dmask & below)] = static_cast<uint8_t>(lane);
+    } else if (present) {
+      const uint32_t rank = __popcll(mask & ~dmask & below);
+      if (rank < ed) Jl[rank] = static_cast<uint8_t>(lane);
+    }
+    if (!present) outr[__popcll(~mask & a.nmask & below)] = static_cast<uint8_t>(lane);
   }
   __syncthreads();
-  for (uint32_t r = 0; r < d; ++r) {
-    if (A[r * w + r] == 0) {  // uniform: every lane reads the same LDS byte
-      const bool cand = lane > r && lane < d && A[lane * w + r] != 0;
+  if (lane < d) surv[lane] = lane < npd ? Pl[lane] : Jl[lane - npd];
+  // [B | I], B[i][l] = M[J_i][E_l]
+  const uint32_t w = 2 * ed;
+  for (uint32_t idx = lane; idx < ed * w; idx += 64) {
+    const uint32_t i = idx / w, col = idx - i * w;
+    Ba[idx] = col < ed ? a.M[Jl[i] * d + El[col]] : static_cast<uint8_t>(col - ed == i ? 1 : 0);
+  }
+  __syncthreads();
+  for (uint32_t r = 0; r < ed; ++r) {
+    if (Ba[r * w + r] == 0) {  // uniform branch (every lane reads the same byte)
+      const bool cand = lane > r && lane < ed && Ba[lane * w + r] != 0;
       const uint64_t bal = __ballot(cand);
       if (bal == 0) {  // singular: cannot happen for an MDS code
         if (lane == 0) *reinterpret_cast<uint32_t*>(desc) = 7u << 16;
@@ -603,39 +619,52 @@ __global__ __launch_bounds__(64) void k_prepare(Prep a) {
       }
       const uint32_t b = __ffsll(static_cast<long long>(bal)) - 1;
       for (uint32_t col = lane; col < w; col += 64) {
-        const uint8_t t = A[r * w + col];
-        A[r * w + col] = A[b * w + col];
-        A[b * w + col] = t;
+        const uint8_t t = Ba[r * w + col];
+        Ba[r * w + col] = Ba[b * w + col];
+        Ba[b * w + col] = t;
       }
       __syncthreads();
     }
-    const uint32_t piv = A[r * w + r];
-    const uint32_t s = ex[255 - lg[piv]];  // 1 / piv  (piv != 0)
+    const uint32_t s = ex[255 - lg[Ba[r * w + r]]];  // 1 / pivot
     __syncthreads();
-    for (uint32_t col = lane; col < w; col += 64) A[r * w + col] = lmul(lg, ex, s, A[r * w + col]);
-    if (lane < d) fcol[lane] = A[lane * w + r];
+    for (uint32_t col = lane; col < w; col += 64) Ba[r * w + col] = lmul(lg, ex, s, Ba[r * w + col]);
+    if (lane < ed) fcol[lane] = Ba[lane * w + r];
     __syncthreads();
-    for (uint32_t idx = lane; idx < d * w; idx += 64) {
+    for (uint32_t idx = lane; idx < ed * w; idx += 64) {
       const uint32_t o = idx / w, col = idx - o * w;
-      if (o != r) A[idx] ^= lmul(lg, ex, fcol[o], A[r * w + col]);
+      if (o != r) Ba[idx] ^= lmul(lg, ex, fcol[o], Ba[r * w + col]);
     }
     __syncthreads();
   }
-  // header + rows
+  // Dinv rows of the erased data rows (Binv = Ba[:, ed:])
+  for (uint32_t idx = lane; idx < ed * d; idx += 64) {
+    const uint32_t l = idx / d, pos = idx - l * d;
+    uint8_t v;
+    if (pos >= npd) {
+      v = Ba[l * w + ed + (pos - npd)];
+    } else {
+      v = 0;
+      for (uint32_t i = 0; i < ed; ++i) v ^= lmul(lg, ex, Ba[l * w + ed + i], a.M[Jl[i] * d + Pl[pos]]);
+    }
+    DE[l * 64 + pos] = v;
+  }
+  __syncthreads();
+  // header + rows + coefficients
   const uint32_t dpad = a.dpad, epad = a.epad;
-  if (lane == 0) *reinterpret_cast<uint32_t*>(desc) = (e & 0xffu) | (e_data << 8);
+  if (lane == 0) *reinterpret_cast<uint32_t*>(desc) = (e & 0xffu) | (ed << 8);
   for (uint32_t i = lane; i < dpad; i += 64) desc[4 + i] = i < d ? surv[i] : 0;
   for (uint32_t i = lane; i < epad; i += 64) desc[4 + dpad + i] = i < e ? outr[i] : 0;
   uint8_t* coef = desc + 4 + dpad + epad;
   for (uint32_t idx = lane; idx < e * dpad; idx += 64) {
-    const uint32_t i = idx / dpad, k = idx - i * dpad;
+    const uint32_t i = idx / dpad, pos = idx - i * dpad;
     uint8_t v = 0;
-    if (k < d) {
-      const uint32_t r = outr[i];
-      if (r < d) {
-        v = A[r * w + d + k];
+    if (pos < d) {
+      if (i < ed) {
+        v = DE[i * 64 + pos];
       } else {
-        for (uint32_t j = 0; j < d; ++j) v ^= lmul(lg, ex, a.M[r * d + j], A[j * w + d + k]);
+        const uint32_t r = outr[i];
+        if (pos < npd) v = a.M[r * d + Pl[pos]];
+        for (uint32_t l = 0; l < ed; ++l) v ^= lmul(lg, ex, a.M[r * d + El[l]], DE[l * 64 + pos]);
       }
     }
     coef[idx] = v;
@@ -649,8 +678,10 @@ static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
 
 // Launch policy (tuned with tools/kvariants.hip on MI355X)
 constexpr int kEncNT = 1;    // nontemporal loads, plain stores
+constexpr int kEncJumboNT = 3;  // (32,8): NT loads and stores (578 vs 615 us, tools/jvariants.hip)
 constexpr int kApplyNT = 3;  // nontemporal loads and stores
 constexpr int kApplyPNT = 1; // k_apply_p: nontemporal loads, plain stores (-6% vs 3)
+constexpr int kApplyQNT = 3; // k_apply_q (jumbo): NT loads and stores (548 vs 572 us)
 
 int apply_dmax(int d) {
   if (d <= 4) return 4;
@@ -670,7 +701,7 @@ hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   if (d == 10 && p == 3)
     hipLaunchKernelGGL((k_encode_c<10, 3, kEncNT>), grid, block, 0, s, a);
   else if (d == 32 && p == 8)
-    hipLaunchKernelGGL((k_encode_c<32, 8, kEncNT>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((k_encode_c<32, 8, kEncJumboNT>), grid, block, 0, s, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -689,9 +720,9 @@ static void launch_apply_dm(const Batch& a, hipStream_t s) {
   }
   if (a.chunks >= 64 && a.epad <= 8) {  // wide codes: streaming inputs
     if (a.epad == 4)
-      hipLaunchKernelGGL((k_apply_q<4, MODE, kApplyPNT, 1>), grid, block, 0, s, a);
+      hipLaunchKernelGGL((k_apply_q<4, MODE, kApplyQNT, 1>), grid, block, 0, s, a);
     else
-      hipLaunchKernelGGL((k_apply_q<8, MODE, kApplyPNT, 1>), grid, block, 0, s, a);
+      hipLaunchKernelGGL((k_apply_q<8, MODE, kApplyQNT, 1>), grid, block, 0, s, a);
     return;
   }
   if (a.chunks >= 64 && a.epad == 4) {
