@@ -169,6 +169,30 @@ int ugo_fec_tx_assemble(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, const
  * for ugo's fixed-key rc4StreamCrypto (ugo/crypto.go:14-39). */
 int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size_t n);
 
+/* ---- launch timing (measurement) -----------------------------------------
+ * Between ugo_fec_timing_begin and ugo_fec_timing_end, the first max_launches
+ * kernels this context launches are issued with hipExtLaunchKernel start/stop
+ * events, which take the dispatch's own begin/end timestamps: per-launch
+ * kernel durations with nothing inserted into the stream between kernels.
+ * timing_end waits for those launches, writes up to `cap` records (launch
+ * order) and reports how many launches ran untimed past max_launches. */
+#define UGO_FEC_KERNEL_ENCODE 1      /* encode                                  */
+#define UGO_FEC_KERNEL_RECONSTRUCT 2 /* reconstruct (descriptor apply)          */
+#define UGO_FEC_KERNEL_PREPARE 3     /* per-group decode descriptors (d+p > 16) */
+#define UGO_FEC_KERNEL_BYTES 4       /* byte-granular encode / reconstruct      */
+#define UGO_FEC_KERNEL_RX 5          /* ugo_fec_rx_assemble                     */
+#define UGO_FEC_KERNEL_TX 6          /* ugo_fec_tx_assemble                     */
+#define UGO_FEC_KERNEL_PACKET 7      /* ugo_fec_packet_decode                   */
+
+typedef struct ugo_fec_launch_time {
+  uint32_t kernel; /* UGO_FEC_KERNEL_* */
+  float ms;        /* kernel duration */
+} ugo_fec_launch_time;
+
+int ugo_fec_timing_begin(ugo_fec* ctx, size_t max_launches);
+int ugo_fec_timing_end(ugo_fec* ctx, ugo_fec_launch_time* out, size_t cap, size_t* n_out,
+                       size_t* n_untimed);
+
 /* ---- helpers ------------------------------------------------------------- */
 int ugo_fec_host_alloc(size_t bytes, void** out);  /* pinned host memory */
 int ugo_fec_host_free(void* p);

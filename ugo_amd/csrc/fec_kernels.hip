@@ -43,6 +43,7 @@
 #include "fec_kernels.hpp"
 #include "gf256.hpp"
 #include "gf_device.hpp"
+#include "launch.hpp"
 
 namespace ugo {
 namespace kern {
@@ -672,6 +673,11 @@ __global__ __launch_bounds__(64) void k_prepare(Prep a) {
 }
 
 // ------------------------------------------------------------- launchers
+LaunchTimer*& current_timer() {
+  static thread_local LaunchTimer* t = nullptr;
+  return t;
+}
+
 static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
   return static_cast<uint32_t>((items + bs - 1) / bs);
 }
@@ -699,9 +705,9 @@ bool has_const_encode(int d, int p) { return (d == 10 && p == 3) || (d == 32 && 
 hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   const dim3 grid(blocks_for(a.items, 256)), block(256);
   if (d == 10 && p == 3)
-    hipLaunchKernelGGL((k_encode_c<10, 3, kEncNT>), grid, block, 0, s, a);
+    launch(kKEncode, k_encode_c<10, 3, kEncNT>, grid, block, 0, s, a);
   else if (d == 32 && p == 8)
-    hipLaunchKernelGGL((k_encode_c<32, 8, kEncJumboNT>), grid, block, 0, s, a);
+    launch(kKEncode, k_encode_c<32, 8, kEncJumboNT>, grid, block, 0, s, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -714,24 +720,24 @@ static void launch_apply_dm(const Batch& a, hipStream_t s) {
   const dim3 grid(blocks_for(a.items, 256)), block(256);
   if constexpr (DMAX <= 16) {
     if (a.chunks >= 64 && a.epad == 4) {
-      hipLaunchKernelGGL((k_apply_p<DMAX, MODE, kApplyPNT, 1>), grid, block, 0, s, a);
+      launch(kKReconstruct, k_apply_p<DMAX, MODE, kApplyPNT, 1>, grid, block, 0, s, a);
       return;
     }
   }
   if (a.chunks >= 64 && a.epad <= 8) {  // wide codes: streaming inputs
     if (a.epad == 4)
-      hipLaunchKernelGGL((k_apply_q<4, MODE, kApplyQNT, 1>), grid, block, 0, s, a);
+      launch(kKReconstruct, k_apply_q<4, MODE, kApplyQNT, 1>, grid, block, 0, s, a);
     else
-      hipLaunchKernelGGL((k_apply_q<8, MODE, kApplyQNT, 1>), grid, block, 0, s, a);
+      launch(kKReconstruct, k_apply_q<8, MODE, kApplyQNT, 1>, grid, block, 0, s, a);
     return;
   }
   if (a.chunks >= 64 && a.epad == 4) {
     Batch b = a;
     b.pass = (a.items + 63u) / 64u * 64u;
-    hipLaunchKernelGGL((k_apply_w<DMAX, MODE, kApplyNT, 1>), grid, block, 0, s, b);
+    launch(kKReconstruct, k_apply_w<DMAX, MODE, kApplyNT, 1>, grid, block, 0, s, b);
   }
   else
-    hipLaunchKernelGGL((k_apply<DMAX, MODE, kApplyNT>), grid, block, 0, s, a);
+    launch(kKReconstruct, k_apply<DMAX, MODE, kApplyNT>, grid, block, 0, s, a);
 }
 
 template <int MODE>
@@ -761,16 +767,16 @@ hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s) {
 hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s) {
   const dim3 grid(blocks_for(a.items, 256)), block(256);
   switch (mode) {
-    case 0: hipLaunchKernelGGL((k_apply_bytes<0>), grid, block, 0, s, a); break;
-    case 1: hipLaunchKernelGGL((k_apply_bytes<1>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((k_apply_bytes<2>), grid, block, 0, s, a); break;
+    case 0: launch(kKBytes, k_apply_bytes<0>, grid, block, 0, s, a); break;
+    case 1: launch(kKBytes, k_apply_bytes<1>, grid, block, 0, s, a); break;
+    case 2: launch(kKBytes, k_apply_bytes<2>, grid, block, 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s) {
-  hipLaunchKernelGGL(k_prepare, dim3(groups), dim3(64), 0, s, a);
+  launch(kKPrepare, k_prepare, dim3(groups), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

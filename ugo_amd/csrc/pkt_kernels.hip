@@ -17,6 +17,7 @@
 
 #include <cstdint>
 
+#include "launch.hpp"
 #include "pkt_kernels.hpp"
 
 namespace ugo {
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(256) void k_packet_decode(PktArgs a) {
 hipError_t launch_packet_decode(const PktArgs& a, hipStream_t s) {
   if (a.npk == 0) return hipSuccess;
   const uint64_t blocks = (a.npk + 255) / 256;
-  hipLaunchKernelGGL(k_packet_decode, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a);
+  launch(kKPacket, k_packet_decode, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

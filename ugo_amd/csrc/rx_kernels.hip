@@ -20,6 +20,7 @@
 
 #include <cstdint>
 
+#include "launch.hpp"
 #include "rx_kernels.hpp"
 
 namespace ugo {
@@ -138,7 +139,7 @@ hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
   uint64_t blocks = (waves + 3) / 4;
   if (blocks > 2048u) blocks = 2048u;  // 8 workgroups per CU, grid-stride over packet pairs
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rx_scatter, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a);
+  launch(kKRx, k_rx_scatter, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

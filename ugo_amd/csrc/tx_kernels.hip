@@ -23,6 +23,7 @@
 #include <cstdint>
 
 #include "gf_device.hpp"
+#include "launch.hpp"
 #include "tx_kernels.hpp"
 
 namespace ugo {
@@ -209,19 +210,19 @@ hipError_t launch_tx_assemble(int dmax, const TxArgs& a, hipStream_t s) {
   switch (dmax) {
     case 0:
       if (a.d == 10 && a.p == 3)
-        hipLaunchKernelGGL((k_tx_c<10, 3>), grid, block, 0, s, a);
+        launch(kKTx, k_tx_c<10, 3>, grid, block, 0, s, a);
       else if (a.d == 32 && a.p == 8)
-        hipLaunchKernelGGL((k_tx_c<32, 8>), grid, block, 0, s, a);
+        launch(kKTx, k_tx_c<32, 8>, grid, block, 0, s, a);
       else
         return hipErrorInvalidValue;
       break;
-    case 4: hipLaunchKernelGGL((k_tx_var<4>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_tx_var<8>), grid, block, 0, s, a); break;
-    case 10: hipLaunchKernelGGL((k_tx_var<10>), grid, block, 0, s, a); break;
-    case 12: hipLaunchKernelGGL((k_tx_var<12>), grid, block, 0, s, a); break;
-    case 16: hipLaunchKernelGGL((k_tx_var<16>), grid, block, 0, s, a); break;
-    case 24: hipLaunchKernelGGL((k_tx_var<24>), grid, block, 0, s, a); break;
-    case 32: hipLaunchKernelGGL((k_tx_var<32>), grid, block, 0, s, a); break;
+    case 4: launch(kKTx, k_tx_var<4>, grid, block, 0, s, a); break;
+    case 8: launch(kKTx, k_tx_var<8>, grid, block, 0, s, a); break;
+    case 10: launch(kKTx, k_tx_var<10>, grid, block, 0, s, a); break;
+    case 12: launch(kKTx, k_tx_var<12>, grid, block, 0, s, a); break;
+    case 16: launch(kKTx, k_tx_var<16>, grid, block, 0, s, a); break;
+    case 24: launch(kKTx, k_tx_var<24>, grid, block, 0, s, a); break;
+    case 32: launch(kKTx, k_tx_var<32>, grid, block, 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -20,6 +20,7 @@
 #include "fec_kernels.hpp"
 #include "gf256.hpp"
 #include "host/rc4.hpp"
+#include "launch.hpp"
 #include "rx_kernels.hpp"
 #include "tx_kernels.hpp"
 #include "pkt_kernels.hpp"
@@ -65,9 +66,32 @@ struct ugo_fec {
   int8_t* d_status[kStreams] = {};
   size_t stage_groups = 0;  // groups per staging buffer
   size_t stage_pitch = 0;
+  // launch timing (ugo_fec_timing_begin/end)
+  bool timing = false;
+  ugo::kern::LaunchTimer timer;
 };
 
 namespace {
+
+// Makes the context's launch timer (if on) the one the launchers of this
+// thread see, for the duration of one ABI call.
+struct TimerScope {
+  ugo::kern::LaunchTimer* prev;
+  explicit TimerScope(ugo_fec* c) : prev(ugo::kern::current_timer()) {
+    ugo::kern::current_timer() = (c && c->timing) ? &c->timer : nullptr;
+  }
+  ~TimerScope() { ugo::kern::current_timer() = prev; }
+};
+
+void timer_release(ugo_fec* c) {
+  ugo::kern::LaunchTimer& t = c->timer;
+  for (size_t i = 0; i < 2 * t.cap; ++i)
+    if (t.ev[i]) (void)hipEventDestroy(t.ev[i]);
+  delete[] t.ev;
+  delete[] t.kid;
+  t = ugo::kern::LaunchTimer{};
+  c->timing = false;
+}
 
 // Decode descriptor for one presence mask (layout: fec_kernels.hip).
 // Survivors = first d present rows in index order (klauspost Reconstruct),
@@ -125,6 +149,7 @@ int hip_status(hipError_t e) { return e == hipSuccess ? UGO_FEC_OK : UGO_FEC_ERR
 void free_ctx(ugo_fec* c) {
   if (!c) return;
   DeviceGuard g(c->device);
+  timer_release(c);
   (void)hipFree(c->d_M);
   (void)hipFree(c->d_gf);
   (void)hipFree(c->d_encdesc);
@@ -479,6 +504,7 @@ int ugo_fec_encode_strided(ugo_fec* c, uint8_t* shards, size_t groups, size_t S,
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  TimerScope ts(c);
   return encode_dev(c, shards, groups, S, L, static_cast<hipStream_t>(stream));
 }
 
@@ -496,6 +522,7 @@ int ugo_fec_reconstruct_strided(ugo_fec* c, uint8_t* shards, const uint64_t* pre
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  TimerScope ts(c);
   return reconstruct_dev(c, shards, present, groups, S, L, flags, status, static_cast<hipStream_t>(stream));
 }
 
@@ -514,6 +541,7 @@ int ugo_fec_encode_host(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, si
   if (st || groups == 0 || c->p == 0) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  TimerScope ts(c);
   return host_path(c, shards, nullptr, groups, S, pitch, false, 0, nullptr);
 }
 
@@ -527,6 +555,7 @@ int ugo_fec_reconstruct_host(ugo_fec* c, uint8_t* shards, const uint64_t* presen
   if (c->n > 64) return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  TimerScope ts(c);
   return host_path(c, shards, present, groups, S, pitch, true, flags, status);
 }
 
@@ -545,6 +574,7 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   if ((c->n > 1 && row_stride < S) || (groups > 1 && group_stride < S)) return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  TimerScope ts(c);
   ugo::kern::RxArgs a{};
   a.wire = wire;
   a.lens = lens;
@@ -578,6 +608,7 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
     return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  TimerScope ts(c);
   ugo::kern::TxArgs a{};
   a.pkts = pkts;
   a.lens = lens;
@@ -621,6 +652,7 @@ int ugo_fec_packet_decode(ugo_fec* c, const uint8_t* pkts, size_t slot, const ui
     return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  TimerScope ts(c);
   ugo::kern::PktArgs a{};
   a.pkts = pkts;
   a.lens = lens;
@@ -640,6 +672,53 @@ int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size
   if (!key || key_len == 0 || key_len > 256 || (n && !out)) return UGO_FEC_ERR_INVALID_ARG;
   ugo::rc4_keystream(key, key_len, out, n);
   return UGO_FEC_OK;
+}
+
+int ugo_fec_timing_begin(ugo_fec* c, size_t max_launches) {
+  if (!c || max_launches == 0 || max_launches > (size_t(1) << 20)) return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  timer_release(c);
+  ugo::kern::LaunchTimer& t = c->timer;
+  t.ev = new (std::nothrow) hipEvent_t[2 * max_launches]();
+  t.kid = new (std::nothrow) uint32_t[max_launches]();
+  if (!t.ev || !t.kid) {
+    timer_release(c);
+    return UGO_FEC_ERR_INVALID_ARG;
+  }
+  t.cap = max_launches;
+  for (size_t i = 0; i < 2 * max_launches; ++i)
+    if (hipEventCreate(&t.ev[i]) != hipSuccess) {
+      timer_release(c);
+      return UGO_FEC_ERR_HIP;
+    }
+  c->timing = true;
+  return UGO_FEC_OK;
+}
+
+int ugo_fec_timing_end(ugo_fec* c, ugo_fec_launch_time* out, size_t cap, size_t* n_out, size_t* n_untimed) {
+  if (!c || (cap && !out)) return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  ugo::kern::LaunchTimer& t = c->timer;
+  int st = UGO_FEC_OK;
+  size_t n = 0;
+  for (size_t i = 0; i < t.used; ++i) {
+    if (hipEventSynchronize(t.ev[2 * i + 1]) != hipSuccess) {
+      st = UGO_FEC_ERR_HIP;
+      break;
+    }
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]) != hipSuccess) {
+      st = UGO_FEC_ERR_HIP;
+      break;
+    }
+    if (n < cap) out[n++] = ugo_fec_launch_time{t.kid[i], ms};
+  }
+  if (n_out) *n_out = n;
+  if (n_untimed) *n_untimed = t.dropped;
+  timer_release(c);
+  return st;
 }
 
 int ugo_fec_host_alloc(size_t bytes, void** out) {

@@ -96,6 +96,10 @@ PKT_INFO_DTYPE = np.dtype([("packet_number", "<u8"), ("stop_waiting", "<u8"), ("
                            ("largest_in_order", "<u8"), ("delay_us", "<u8"), ("status", "<u4"),
                            ("payload_off", "<u4"), ("n_ranges", "<u2"), ("n_segments", "<u2"), ("flags", "u1"),
                            ("fec_flag_lo", "u1"), ("reserved", "u1", (10,))])
+# include/ugo_fec.h launch timing
+KERNEL_NAMES = {1: "encode", 2: "reconstruct", 3: "prepare", 4: "bytes", 5: "rx_assemble", 6: "tx_assemble",
+                7: "packet_decode"}
+LAUNCH_TIME_DTYPE = np.dtype([("kernel", "<u4"), ("ms", "<f4")])
 PKT_SEGMENT_DTYPE = np.dtype([("offset", "<u8"), ("data_off", "<u4"), ("len", "<u2"), ("avail", "<u2")])
 assert PKT_INFO_DTYPE.itemsize == 64 and PKT_SEGMENT_DTYPE.itemsize == 16
 
@@ -130,6 +134,8 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_rc4_keystream.argtypes = [vp, sz, vp, sz]
     lib.ugo_fec_tx_assemble.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp, vp]
     lib.ugo_fec_packet_decode.argtypes = [vp, vp, sz, vp, sz, vp, u, vp, vp, sz, vp, sz, vp]
+    lib.ugo_fec_timing_begin.argtypes = [vp, sz]
+    lib.ugo_fec_timing_end.argtypes = [vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     _lib = lib
     return lib
 
@@ -292,6 +298,25 @@ class Encoder:
             PKT_FEC_FRAMED if framed else 0, info.data_ptr(), ranges.data_ptr(), max_ranges, segs.data_ptr(),
             max_segments, _stream_handle(stream)))
         return info, ranges, segs
+
+    # ---------------------------------------------------------- launch timing
+    def timing_begin(self, max_launches: int):
+        """Time the next max_launches kernel launches of this context with
+        hipExtLaunchKernel start/stop events (kernel durations, nothing inserted
+        between kernels).  Read them with timing_end()."""
+        _raise(load_library().ugo_fec_timing_begin(self._h, max_launches))
+        self._timing_cap = max_launches
+
+    def timing_end(self):
+        """Waits for the timed launches; returns (records, untimed): records is a
+        LAUNCH_TIME_DTYPE array (kernel id, ms) in launch order, untimed the
+        number of launches past max_launches."""
+        cap = getattr(self, "_timing_cap", 0)
+        out = np.zeros(cap, LAUNCH_TIME_DTYPE)
+        n, untimed = ctypes.c_size_t(), ctypes.c_size_t()
+        _raise(load_library().ugo_fec_timing_end(self._h, out.ctypes.data if cap else None, cap, ctypes.byref(n),
+                                                 ctypes.byref(untimed)))
+        return out[:n.value], untimed.value
 
     # ------------------------------------------------------ host-buffer batch
     def encode_host(self, shards: np.ndarray, shard_size: Optional[int] = None):
