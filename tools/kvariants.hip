@@ -155,6 +155,7 @@ int main(int argc, char** argv) {
     const std::string L = lay ? "planar" : "interl";
     add(k_encode_c<10, 3, 0>, b, enc_bytes, "enc " + L + " nt0");
     add(k_encode_c<10, 3, 1>, b, enc_bytes, "enc " + L + " nt1");
+    add(k_encode_c<10, 3, 1, 1>, b, enc_bytes, "enc " + L + " nt1 xcd-contiguous");
     add(k_encode_c<10, 3, 3>, b, enc_bytes, "enc " + L + " nt3");
     add(k_apply<10, 1, 0>, b, dec_bytes, "dec " + L + " nt0");
     add(k_apply<10, 1, 1>, b, dec_bytes, "dec " + L + " nt1");
@@ -164,7 +165,8 @@ int main(int argc, char** argv) {
       b1.pass = (b.items + 63u) / 64u * 64u;
       add(k_apply_w<10, 1, 3, 1>, b1, dec_bytes, "dec " + L + " nt3 wave-scalar-desc cpt1");
     }
-        add(k_apply_p<10, 1, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick");
+    add(k_apply_p<10, 1, 1, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables scalar-pick");
+    add(k_apply_p<10, 1, 1, 1, 1, 4, true, 1>, b, dec_bytes, "dec " + L + " nt1 perm-tables xcd-contiguous");
     add(k_apply_p<10, 1, 1, 1, 1, 3, true>, b, dec_bytes, "dec " + L + " nt1 perm pair emax3");
     add(k_apply_p<10, 1, 1, 1, 1, 3, false>, b, dec_bytes, "dec " + L + " nt1 perm single emax3");
     add(k_pattern_rec<1>, b, dec_bytes, "dec " + L + " MEMORY PATTERN ONLY nt1 (xor, no GF)");
@@ -190,6 +192,7 @@ int main(int argc, char** argv) {
     }, {}});
   };
   pair(k_encode_c<10, 3, 1>, k_apply_p<10, 1, 1>, pl, "pair planar enc-nt1 perm-nt1");
+  pair(k_encode_c<10, 3, 1, 1>, k_apply_p<10, 1, 1, 1, 1, 4, true, 1>, pl, "pair planar enc-nt1 perm-nt1 xcd-contiguous");
   pair(k_encode_c<10, 3, 3>, k_apply_p<10, 1, 1>, pl, "pair planar enc-nt3 perm-nt1");
   pair(k_encode_c<10, 3, 1>, k_apply_p<10, 1, 3>, pl, "pair planar enc-nt1 perm-nt3");
   pair(k_encode_c<10, 3, 3>, k_apply_p<10, 1, 3>, pl, "pair planar enc-nt3 perm-nt3");

@@ -70,9 +70,9 @@ __device__ __forceinline__ void load_rows(V4* x, const uint8_t* gp, uint64_t rst
 // Measured on MI355X (tools/kvariants.hip): a full grid at
 // 8 waves/SIMD (62 VGPRs) beats persistent grids and software-pipelined
 // (ping-pong) forms, whose second register set halves occupancy.
-template <int D, int P, int NT>
+template <int D, int P, int NT, int SWZ = 0>
 __global__ __launch_bounds__(256) void k_encode_c(Batch a) {
-  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t item = block_id<SWZ>() * 256u + threadIdx.x;
   if (item >= a.items) return;
   const Loc l = locate(a, item);
   V4 x[D];
@@ -332,10 +332,11 @@ __device__ __forceinline__ void p_accum(V4* acc, const V4* x, const Batch& a, co
   }
 }
 
-template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1, int EMAX = 4, bool PAIR = true>
+template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1, int EMAX = 4, bool PAIR = true, int SWZ = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_p(Batch a) {
-  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
-  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t bid = block_id<SWZ>();
+  const uint32_t wfirst = bid * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  const uint32_t item = bid * 256u + threadIdx.x;
   if (wfirst >= a.items) return;
   const uint32_t wlast = min(wfirst + 63u, a.items - 1u);
   const uint32_t gA = wfirst / a.chunks;

@@ -15,6 +15,20 @@ namespace ugo {
 namespace kern {
 
 // ---------------------------------------------------------------- helpers
+// Block index, optionally XCD-contiguous (SWZ = 1): the hardware deals blocks
+// round-robin to the 8 XCDs; remapped, XCD x runs one contiguous range of
+// tiles (cdna_hip_programming.md §5.5 T1, nwg % 8 != 0 form).
+template <int SWZ>
+__device__ __forceinline__ uint32_t block_id() {
+  if constexpr (SWZ == 0) {
+    return blockIdx.x;
+  } else {
+    const uint32_t nwg = gridDim.x, b = blockIdx.x;
+    const uint32_t q = nwg >> 3, r = nwg & 7u, x = b & 7u;
+    return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + (b >> 3);
+  }
+}
+
 struct V4 {
   uint32_t v[4];
 };

@@ -134,12 +134,155 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
   }
 }
 
-hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
+// Loads-first form for rows of at most 32 * NP chunks (NP = 3 for ugo's
+// 1470-B payloads).  Same decomposition (half a wave per packet), but:
+//  * the keystream chunks at a lane's offsets are the same for every packet,
+//    so they are loaded once and held in registers;
+//  * the next packet's header and length are prefetched, so a packet's
+//    placement is known before its payload arrives, and all NP payload loads of
+//    a packet are issued before its first store (the per-pass load -> store
+//    chain of k_rx_scatter kept one 1-KiB load in flight per wave);
+//  * lengths are clamped to the slot.
+// MODE (A/B timing only, tools/rxvariants.hip): 0 = production, 1 = without
+// the presence atomics, 2 = the same loads and stores without the realignment.
+template <int NP, int MODE = 0>
+__global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
+  __shared__ uint32_t bstats[4];
+  if (threadIdx.x < 4) bstats[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, hl = lane & 31u;
+  const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
+  const uint64_t nwaves = (gridDim.x * 256ull) >> 6;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  const u32x4 K0 = a.pad ? ld16(a.pad) : zero;  // keystream over the header chunk
+  u32x4 K[NP];
+  uint32_t kbx[NP], kby[NP];  // keystream of the neighbour chunk (lane 31 of a half)
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const uint32_t o = 16u * (32u * q + hl);
+    K[q] = (a.pad && o + 16u <= slot) ? ld16(a.pad + o) : zero;
+    kbx[q] = kby[q] = 0u;
+    if (a.pad && hl == 31u && o + 32u <= slot) {
+      const u32x4 B = ld16(a.pad + o + 16u);
+      kbx[q] = B.x;
+      kby[q] = B.y;
+    }
+  }
+  uint64_t i = 2 * wave + half;
+  u32x4 hn = zero;
+  uint32_t ln = 0;
+  if (i < a.npk) {
+    hn = ld16(a.wire + i * a.slot);
+    ln = a.lens[i];
+  }
+  for (uint64_t base = 2 * wave; base < a.npk; base += 2 * nwaves, i += 2 * nwaves) {
+    const bool have = i < a.npk;
+    const uint8_t* pk = a.wire + i * a.slot;
+    const u32x4 h = hn ^ K0;
+    const uint32_t len = have ? min(ln, slot) : 0u;
+    const uint64_t inext = i + 2 * nwaves;
+    if (inext < a.npk) {  // prefetch the next packet's header and length
+      hn = ld16(a.wire + inext * a.slot);
+      ln = a.lens[inext];
+    }
+    const uint32_t seqid = h.x;
+    const uint32_t flag = h.y & 0xffffu;
+    uint32_t why = 0;  // 0 = accept, else stats slot
+    if (!have) why = 4;
+    else if (len < 6u) why = 3;
+    else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
+    const uint32_t row = seqid % a.n;
+    const uint64_t grp = seqid / a.n;
+    if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
+    const bool ok = why == 0;
+    const uint32_t L = ok ? min(len - 6u, a.S) : 0u;  // payload bytes kept
+    const uint32_t lim = ok ? L + 6u : 0u;            // packet bytes [0, lim) are needed
+    u32x4 A[NP];
+    uint32_t bx[NP], by[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      A[q] = o < lim ? ld16(pk + o) : zero;
+      bx[q] = by[q] = 0u;
+      if (hl == 31u && o + 16u < lim) {
+        const u32x4 B = ld16(pk + o + 16u);
+        bx[q] = B.x;
+        by[q] = B.y;
+      }
+    }
+    uint8_t* dst = a.shards + row * a.rstride + (grp - a.first_group) * a.gstride;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      const u32x4 Aq = A[q] ^ K[q];  // bytes past lim are masked below
+      // converged: neighbour's chunk (packet bytes [o+16, o+32)) by DPP
+      uint32_t nx = from_next_lane(Aq.x), ny = from_next_lane(Aq.y);
+      if (hl == 31u) {
+        nx = bx[q] ^ kbx[q];
+        ny = by[q] ^ kby[q];
+      }
+      if (!ok || o >= a.S) continue;
+      uint32_t w[4];
+      if constexpr (MODE == 2) {
+        w[0] = Aq.x; w[1] = Aq.y; w[2] = Aq.z; w[3] = Aq.w;
+      } else {
+        // payload bytes [o, o+16) = packet bytes [o+6, o+22)
+        w[0] = __builtin_amdgcn_alignbyte(Aq.z, Aq.y, 2);
+        w[1] = __builtin_amdgcn_alignbyte(Aq.w, Aq.z, 2);
+        w[2] = __builtin_amdgcn_alignbyte(nx, Aq.w, 2);
+        w[3] = __builtin_amdgcn_alignbyte(ny, nx, 2);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
+        const uint32_t b0 = o + 4u * j;
+        const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
+        w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+      }
+      const uint32_t nb = a.S - o;
+      if (nb >= 16u) {
+        *reinterpret_cast<u32x4*>(dst + o) = u32x4{w[0], w[1], w[2], w[3]};
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t lo = 4u * j;
+          if (nb >= lo + 4u) {
+            *reinterpret_cast<uint32_t*>(dst + o + lo) = w[j];
+          } else if (nb > lo) {
+            for (uint32_t t = 0; t < nb - lo; ++t) dst[o + lo + t] = static_cast<uint8_t>(w[j] >> (8u * t));
+          }
+        }
+      }
+    }
+    if (hl == 0 && why < 4) {
+      if (MODE == 0 && ok) atomicOr(reinterpret_cast<unsigned long long*>(&a.present[grp - a.first_group]), 1ull << row);
+      atomicAdd(&bstats[why], 1u);
+    }
+  }
+  if (a.stats) {
+    __syncthreads();
+    if (threadIdx.x < 4 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+  }
+}
+
+static inline uint32_t rx_blocks(const RxArgs& a) {
   const uint64_t waves = (a.npk + 1) / 2;
   uint64_t blocks = (waves + 3) / 4;
   if (blocks > 2048u) blocks = 2048u;  // 8 workgroups per CU, grid-stride over packet pairs
+  return static_cast<uint32_t>(blocks);
+}
+
+hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
+  const uint32_t blocks = rx_blocks(a);
   if (blocks == 0) return hipSuccess;
-  launch(kKRx, k_rx_scatter, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a);
+  const uint32_t passes = ((a.S + 15u) / 16u + 31u) / 32u;
+  switch (passes) {
+    case 1: launch(kKRx, k_rx_place<1>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 2: launch(kKRx, k_rx_place<2>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 3: launch(kKRx, k_rx_place<3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 4: launch(kKRx, k_rx_place<4>, dim3(blocks), dim3(256), 0, s, a); break;
+    default: launch(kKRx, k_rx_scatter, dim3(blocks), dim3(256), 0, s, a); break;
+  }
   return hipGetLastError();
 }
 
