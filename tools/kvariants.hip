@@ -197,6 +197,42 @@ int main(int argc, char** argv) {
   pair(k_encode_c<10, 3, 1>, k_apply_p<10, 1, 3>, pl, "pair planar enc-nt1 perm-nt3");
   pair(k_encode_c<10, 3, 3>, k_apply_p<10, 1, 3>, pl, "pair planar enc-nt3 perm-nt3");
   pair(k_encode_c<10, 3, 1>, k_apply_p<10, 1, 0>, pl, "pair planar enc-nt1 perm-nt0");
+  // LDS-DMA (global_load_lds_dwordx4 nt) row loads; profiles/r1/kvariants_xcd_rstride.jsonl
+  // holds the row-stride sweep (+-2%, kept at G * pitch)
+  add(k_encode_g<10, 3, 0>, pl, enc_bytes, "enc planar lds-dma nt");
+  add(k_encode_g<10, 3, 0, 8>, pl, enc_bytes, "enc planar lds-dma nt 8 rows + 2 reg");
+  add(k_encode_g<10, 3, 0, 6>, pl, enc_bytes, "enc planar lds-dma nt 6 rows + 4 reg");
+  add(k_encode_g<10, 3, 0, 5>, pl, enc_bytes, "enc planar lds-dma nt 5 rows + 5 reg");
+  add(k_encode_g<10, 3, 0, 3>, pl, enc_bytes, "enc planar lds-dma nt 3 rows + 7 reg");
+  add(k_apply_p<10, 1, 0, 1, 1, 4, true, 0, 10>, pl, dec_bytes, "dec planar perm lds-dma nt");
+  add(k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 4>, pl, dec_bytes, "dec planar perm lds-dma 4 rows + 6 reg");
+  add(k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 2>, pl, dec_bytes, "dec planar perm lds-dma 2 rows + 8 reg");
+  pair(k_encode_g<10, 3, 0, 8>, k_apply_p<10, 1, 1>, pl, "pair planar lds-dma enc 8 rows + perm-nt1");
+  pair(k_encode_g<10, 3, 0>, k_apply_p<10, 1, 0, 1, 1, 4, true, 0, 10>, pl, "pair planar lds-dma enc + perm");
+
+  {  // LDS-DMA variants must reproduce the register-load kernels bit for bit
+    const uint32_t grid = (pl.items + 255) / 256;
+    std::vector<uint8_t> hc(h), h1(h.size()), h2(h.size());
+    for (uint64_t g = 0; g < G; ++g)
+      for (int r = 0; r < n; ++r)
+        if (!(hm[g] >> r & 1)) memset(hc.data() + r * pl.rstride + g * pl.gstride, 0xee, S);
+    auto run_cmp = [&](const char* nm, auto ka, auto kb) {
+      CK(hipMemcpy(buf, hc.data(), hc.size(), hipMemcpyHostToDevice));
+      hipLaunchKernelGGL(ka, dim3(grid), dim3(256), 0, 0, pl);
+      CK(hipMemcpy(h1.data(), buf, h1.size(), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(buf, hc.data(), hc.size(), hipMemcpyHostToDevice));
+      hipLaunchKernelGGL(kb, dim3(grid), dim3(256), 0, 0, pl);
+      CK(hipMemcpy(h2.data(), buf, h2.size(), hipMemcpyDeviceToHost));
+      printf("{\"check\":\"%s\",\"equal\":%s,\"changed\":%s}\n", nm, h1 == h2 ? "true" : "false",
+             h1 == hc ? "false" : "true");
+      fflush(stdout);
+    };
+    run_cmp("k_encode_g == k_encode_c", k_encode_c<10, 3, 1>, k_encode_g<10, 3, 0>);
+    run_cmp("k_encode_g<8> == k_encode_c", k_encode_c<10, 3, 1>, k_encode_g<10, 3, 0, 8>);
+    run_cmp("k_apply_p lds-dma 4 == k_apply_p", k_apply_p<10, 1, 1>, k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 4>);
+    run_cmp("k_apply_p lds-dma == k_apply_p", k_apply_p<10, 1, 1>, k_apply_p<10, 1, 0, 1, 1, 4, true, 0, 10>);
+    CK(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
+  }
 
   {  // k_apply_p must reproduce k_apply_w bit for bit (random masks, planar)
     const uint32_t grid = (pl.items + 255) / 256;

@@ -97,6 +97,61 @@ __global__ __launch_bounds__(256) void k_pattern(uint8_t* base, uint32_t items, 
   }
 }
 
+#define GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+// read-only, one 16-B chunk per thread over a full grid, NT loads (encode's load form)
+__global__ __launch_bounds__(256) void k_read_full(const u32x4* __restrict__ a, uint32_t* out, size_t n) {
+  const size_t i = blockIdx.x * 256ull + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 v = __builtin_nontemporal_load(&a[i]);
+  if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u) out[0] = 1u;
+}
+
+// read-only through LDS-DMA (global_load_lds_dwordx4): U 1-KiB pieces per wave
+// in flight, wave-private LDS, grid-stride; AUX 2 = nt
+template <int U, int AUX>
+__global__ __launch_bounds__(256) void k_read_glds(const uint8_t* a, uint32_t* out, size_t n16) {
+  __shared__ u32x4 buf[4][U][64];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const size_t nw = gridDim.x * 4ull;
+  uint32_t acc = 0;
+  for (size_t base = (blockIdx.x * 4ull + w) * 64u * U; base < n16; base += nw * 64u * U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      __builtin_amdgcn_global_load_lds(GPTR(a + (base + u * 64u + lane) * 16u), LPTR(&buf[w][u][0]), 16, 0, AUX);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    acc ^= buf[w][lane & (U - 1)][lane].x;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
+// the planar encode pattern with the 10 row loads through LDS-DMA
+template <int AUX>
+__global__ __launch_bounds__(256) void k_pattern_glds(uint8_t* base, uint32_t items, uint32_t chunks, uint64_t pitch,
+                                                      uint64_t group_bytes) {
+  __shared__ u32x4 buf[4][10][64];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= items) return;
+  uint32_t g = item / chunks, c = item - g * chunks;
+  uint8_t* gp = base + g * group_bytes + c * 16ull;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) __builtin_amdgcn_global_load_lds(GPTR(gp + (uint64_t)k * pitch), LPTR(&buf[w][k][0]), 16, 0, AUX);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  u32x4 x[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) x[k] = buf[w][k][lane];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    u32x4 y = x[i];
+#pragma unroll
+    for (int k = 3; k < 10; ++k)
+      if ((k + i) & 1) y ^= x[k];
+    *reinterpret_cast<u32x4*>(gp + (uint64_t)(10 + i) * pitch) = y;
+  }
+}
+
 int main(int argc, char** argv) {
   const size_t G = 65536, n = 13, pitch = 1360, S = 1350;
   const size_t bytes = G * n * pitch;
@@ -151,6 +206,28 @@ int main(int argc, char** argv) {
     ms = timeit([&] { hipLaunchKernelGGL(k_pattern<true>, dim3((items + 255) / 256), dim3(256), 0, 0, a, items, chunks, rs, gs); return 0; });
     printf("{\"variant\":\"pattern_nt%s\",\"us\":%.2f,\"alg_GBps\":%.1f,\"moved_GBps\":%.1f}\n", planar ? "_planar" : "", ms * 1e3,
            alg / (ms * 1e-3) / 1e9, moved / (ms * 1e-3) / 1e9);
+  }
+  for (int aux : {0, 2}) {
+    const uint64_t rs = G * pitch, gs = pitch;
+    float ms = timeit([&] {
+      if (aux) hipLaunchKernelGGL(k_pattern_glds<2>, dim3((items + 255) / 256), dim3(256), 0, 0, a, items, chunks, rs, gs);
+      else hipLaunchKernelGGL(k_pattern_glds<0>, dim3((items + 255) / 256), dim3(256), 0, 0, a, items, chunks, rs, gs);
+      return 0; });
+    printf("{\"variant\":\"pattern_glds_planar aux%d\",\"us\":%.2f,\"alg_GBps\":%.1f,\"moved_GBps\":%.1f}\n", aux, ms * 1e3,
+           alg / (ms * 1e-3) / 1e9, moved / (ms * 1e-3) / 1e9);
+  }
+  {
+    float ms = timeit([&] { hipLaunchKernelGGL(k_read_full, dim3((n16 + 255) / 256), dim3(256), 0, 0, (const u32x4*)a, (uint32_t*)b, n16); return 0; });
+    printf("{\"variant\":\"read16 full-grid nt\",\"GBps\":%.1f}\n", bytes / (ms * 1e-3) / 1e9);
+    const size_t n16r = n16 / 1024 * 1024;
+    for (int grid : {1024, 2048, 4096}) {
+      ms = timeit([&] { hipLaunchKernelGGL((k_read_glds<4, 2>), dim3(grid), dim3(256), 0, 0, (const uint8_t*)a, (uint32_t*)b, n16r); return 0; });
+      printf("{\"variant\":\"read glds U4 nt\",\"grid\":%d,\"GBps\":%.1f}\n", grid, n16r * 16.0 / (ms * 1e-3) / 1e9);
+      ms = timeit([&] { hipLaunchKernelGGL((k_read_glds<8, 2>), dim3(grid), dim3(256), 0, 0, (const uint8_t*)a, (uint32_t*)b, n16r); return 0; });
+      printf("{\"variant\":\"read glds U8 nt\",\"grid\":%d,\"GBps\":%.1f}\n", grid, n16r * 16.0 / (ms * 1e-3) / 1e9);
+      ms = timeit([&] { hipLaunchKernelGGL((k_read_glds<8, 0>), dim3(grid), dim3(256), 0, 0, (const uint8_t*)a, (uint32_t*)b, n16r); return 0; });
+      printf("{\"variant\":\"read glds U8 default\",\"grid\":%d,\"GBps\":%.1f}\n", grid, n16r * 16.0 / (ms * 1e-3) / 1e9);
+    }
   }
   return 0;
 }

@@ -80,6 +80,27 @@ __global__ __launch_bounds__(256) void k_encode_c(Batch a) {
   cparity_store<D, P, NT>(l.gp, a.rstride, l.nb, x, std::make_integer_sequence<int, P>{});
 }
 
+// k_encode_c with the first GR row loads staged through LDS by LDS-DMA (nt)
+// and the rest loaded to registers (nt): each wave owns GR x 1 KiB of LDS
+// (GR = 10: 40 KiB per block, 4 blocks per CU).
+template <int D, int P, int NTS = 0, int GR = D>
+__global__ __launch_bounds__(256) void k_encode_g(Batch a) {
+  __shared__ u32x4 stage[4][GR][64];
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const Loc l = locate(a, item);
+#pragma unroll
+  for (int k = 0; k < GR; ++k) lds_dma16(l.gp + static_cast<uint64_t>(k) * a.rstride, &stage[w][k][0]);
+  V4 x[D];
+#pragma unroll
+  for (int k = GR; k < D; ++k) x[k] = load16<1>(l.gp + static_cast<uint64_t>(k) * a.rstride);
+  lds_dma_wait();
+#pragma unroll
+  for (int k = 0; k < GR; ++k) x[k] = lds16(&stage[w][k][lane]);
+  cparity_store<D, P, NTS>(l.gp, a.rstride, l.nb, x, std::make_integer_sequence<int, P>{});
+}
+
 // ----------------------------------------------- descriptor-driven kernels
 // Descriptor, byte offsets:
 //   [0] e_total  [1] e_data  [2] status  [3] reserved
@@ -377,6 +398,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
   const uint32_t nb = a.S - c * 16u;
   V4 x[DMAX];
+  // (survivor loads by LDS-DMA, as k_encode_g does, measured 34% slower here:
+  // DESIGN.md §3.4)
 #pragma unroll
   for (int k = 0; k < DMAX; ++k) {
     if (k < static_cast<int>(a.d)) {
@@ -685,7 +708,9 @@ static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
 
 // Launch policy (tuned with tools/kvariants.hip on MI355X)
 constexpr int kEncNT = 1;    // nontemporal loads, plain stores
+constexpr int kEncLdsRows = 8;  // (10,3): rows 0-7 by LDS-DMA nt, 8-9 to registers (182.6 vs 188.6 us)
 constexpr int kEncJumboNT = 3;  // (32,8): NT loads and stores (578 vs 615 us, tools/jvariants.hip)
+constexpr int kEncJumboLdsRows = 16;  // (32,8): rows 0-15 by LDS-DMA nt (557 vs 571 us)
 constexpr int kApplyNT = 3;  // nontemporal loads and stores
 constexpr int kApplyPNT = 1; // k_apply_p: nontemporal loads, plain stores (-6% vs 3)
 constexpr int kApplyQNT = 3; // k_apply_q (jumbo): NT loads and stores (548 vs 572 us)
@@ -706,9 +731,9 @@ bool has_const_encode(int d, int p) { return (d == 10 && p == 3) || (d == 32 && 
 hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   const dim3 grid(blocks_for(a.items, 256)), block(256);
   if (d == 10 && p == 3)
-    launch(kKEncode, k_encode_c<10, 3, kEncNT>, grid, block, 0, s, a);
+    launch(kKEncode, k_encode_g<10, 3, kEncNT & 2, kEncLdsRows>, grid, block, 0, s, a);
   else if (d == 32 && p == 8)
-    launch(kKEncode, k_encode_c<32, 8, kEncJumboNT>, grid, block, 0, s, a);
+    launch(kKEncode, k_encode_g<32, 8, kEncJumboNT & 2, kEncJumboLdsRows>, grid, block, 0, s, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
