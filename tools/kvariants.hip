@@ -60,8 +60,9 @@ static void build_table(int d, int p, uint32_t dpad, uint32_t epad, uint32_t str
 // Memory-pattern ceiling of the reconstruct: the wave-scalar descriptor
 // prologue, survivor loads and erased-row stores of k_apply_p, with the GF
 // arithmetic replaced by a plain XOR of the survivors (wrong values, same bytes).
-template <int NT>
+template <int NT, bool GL = false>
 __global__ __launch_bounds__(256) void k_pattern_rec(Batch a) {
+  __shared__ u32x4 stage[GL ? 4 : 1][GL ? 10 : 1][64];
   const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
   if (wfirst >= a.items) return;
@@ -81,11 +82,24 @@ __global__ __launch_bounds__(256) void k_pattern_rec(Batch a) {
   uint8_t* gp = a.base + (a.g0 + gl) * a.gstride + static_cast<uint64_t>(c) * 16u;
   const uint32_t nb = a.S - c * 16u;
   V4 y{{0u, 0u, 0u, 0u}};
+  if constexpr (GL) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
 #pragma unroll
-  for (int k = 0; k < 10; ++k) {
-    const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
-    const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
-    xor4(y, load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride));
+    for (int k = 0; k < 10; ++k) {
+      const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
+      const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
+      lds_dma16(gp + static_cast<uint64_t>(r) * a.rstride, &stage[w][k][0]);
+    }
+    lds_dma_wait();
+#pragma unroll
+    for (int k = 0; k < 10; ++k) xor4(y, lds16(&stage[w][k][lane]));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
+      const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
+      xor4(y, load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride));
+    }
   }
   const uint32_t orows = inB ? oB : oA;
   for (int i = 0; i < 4; ++i) {
@@ -204,11 +218,12 @@ int main(int argc, char** argv) {
   add(k_encode_g<10, 3, 0, 6>, pl, enc_bytes, "enc planar lds-dma nt 6 rows + 4 reg");
   add(k_encode_g<10, 3, 0, 5>, pl, enc_bytes, "enc planar lds-dma nt 5 rows + 5 reg");
   add(k_encode_g<10, 3, 0, 3>, pl, enc_bytes, "enc planar lds-dma nt 3 rows + 7 reg");
-  add(k_apply_p<10, 1, 0, 1, 1, 4, true, 0, 10>, pl, dec_bytes, "dec planar perm lds-dma nt");
-  add(k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 4>, pl, dec_bytes, "dec planar perm lds-dma 4 rows + 6 reg");
-  add(k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 2>, pl, dec_bytes, "dec planar perm lds-dma 2 rows + 8 reg");
+  add(k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 10>, pl, dec_bytes, "dec planar perm lds-dma asm-collect");
+  add(k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 8>, pl, dec_bytes, "dec planar perm lds-dma asm-collect 8 rows + 2 reg");
+  pair(k_encode_g<10, 3, 0, 8>, k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 8>, pl, "pair planar lds-dma enc 8 + perm lds-dma 8");
+  pair(k_encode_g<10, 3, 0, 8>, k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 10>, pl, "pair planar lds-dma enc 8 + perm lds-dma 10");
+  add(k_pattern_rec<1, true>, pl, dec_bytes, "dec planar MEMORY PATTERN ONLY lds-dma nt (xor, no GF)");
   pair(k_encode_g<10, 3, 0, 8>, k_apply_p<10, 1, 1>, pl, "pair planar lds-dma enc 8 rows + perm-nt1");
-  pair(k_encode_g<10, 3, 0>, k_apply_p<10, 1, 0, 1, 1, 4, true, 0, 10>, pl, "pair planar lds-dma enc + perm");
 
   {  // LDS-DMA variants must reproduce the register-load kernels bit for bit
     const uint32_t grid = (pl.items + 255) / 256;
@@ -229,8 +244,8 @@ int main(int argc, char** argv) {
     };
     run_cmp("k_encode_g == k_encode_c", k_encode_c<10, 3, 1>, k_encode_g<10, 3, 0>);
     run_cmp("k_encode_g<8> == k_encode_c", k_encode_c<10, 3, 1>, k_encode_g<10, 3, 0, 8>);
-    run_cmp("k_apply_p lds-dma 4 == k_apply_p", k_apply_p<10, 1, 1>, k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 4>);
-    run_cmp("k_apply_p lds-dma == k_apply_p", k_apply_p<10, 1, 1>, k_apply_p<10, 1, 0, 1, 1, 4, true, 0, 10>);
+    run_cmp("k_apply_p lds-dma asm-collect == k_apply_p", k_apply_p<10, 1, 1>, k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 10>);
+    run_cmp("k_apply_p lds-dma 8 == k_apply_p", k_apply_p<10, 1, 1>, k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 8>);
     CK(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
   }
 

@@ -353,8 +353,14 @@ __device__ __forceinline__ void p_accum(V4* acc, const V4* x, const Batch& a, co
   }
 }
 
-template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1, int EMAX = 4, bool PAIR = true, int SWZ = 0>
+template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1, int EMAX = 4, bool PAIR = true, int SWZ = 0,
+          int GLR = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_p(Batch a) {
+  // GLR > 0 (A/B only, tools/kvariants.hip): survivors 0..GLR-1 by LDS-DMA.  It
+  // lifts the compute-free pattern 186.7 -> 181.6 us but not this kernel
+  // (187.3 / 191.0 us at GLR 10 / 8 vs 188.0): DESIGN.md §3.4.
+  static_assert(GLR == 0 || (DMAX == 10 && (GLR == 8 || GLR == 10)), "LDS-DMA survivor staging: d = 10");
+  __shared__ u32x4 stage[GLR ? 4 : 1][GLR ? GLR : 1][64];
   const uint32_t bid = block_id<SWZ>();
   const uint32_t wfirst = bid * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
   const uint32_t item = bid * 256u + threadIdx.x;
@@ -398,16 +404,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
   const uint32_t nb = a.S - c * 16u;
   V4 x[DMAX];
-  // (survivor loads by LDS-DMA, as k_encode_g does, measured 34% slower here:
-  // DESIGN.md §3.4)
+  if constexpr (GLR > 0) {  // survivors 0..GLR-1 by LDS-DMA nt, the rest to registers (host: d == 10)
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t sbase = lds_addr(&stage[w][0][0]);
+    uint32_t tok = 0;
 #pragma unroll
-  for (int k = 0; k < DMAX; ++k) {
-    if (k < static_cast<int>(a.d)) {
+    for (int k = 0; k < DMAX; ++k) {
       const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
       const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
-      x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
-    } else {
-      x[k] = V4{{0u, 0u, 0u, 0u}};
+      if (k < GLR)
+        lds_dma16_nt_asm(gp + static_cast<uint64_t>(r) * a.rstride, sbase + 1024u * k, tok);
+      else
+        x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
+    }
+    lds_collect<GLR>(x, &stage[w][0][lane], tok);
+  } else {
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) {
+      if (k < static_cast<int>(a.d)) {
+        const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
+        const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
+        x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
+      } else {
+        x[k] = V4{{0u, 0u, 0u, 0u}};
+      }
     }
   }
   V4 acc[EMAX];

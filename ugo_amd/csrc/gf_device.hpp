@@ -97,6 +97,71 @@ __device__ __forceinline__ V4 lds16(const u32x4* stage_lane) {
   return V4{{v.x, v.y, v.z, v.w}};
 }
 
+// The same LDS-DMA as a NON-volatile inline asm with no memory clobber.  The
+// builtin, and any volatile asm, counts as a write to memory the compiler
+// cannot place, so every uniform load after it loses its no-clobber proof and
+// becomes a per-lane vector load instead of a scalar load (k_apply_p's
+// coefficient tables: 290 vector loads, 34% slower).  Order comes from data
+// instead: each DMA threads `tok` through, and lds_collect consumes it.
+// lds_base: the row's stage address in LDS (wave-uniform), for M0.
+__device__ __forceinline__ void lds_dma16_nt_asm(const uint8_t* p, uint32_t lds_base, uint32_t& tok) {
+  uint32_t keep;
+  asm("s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep), "+s"(tok)
+      : "v"(p), "s"(lds_base));
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p));
+}
+
+// Wait for the wave's LDS-DMA (tok: the last lds_dma16_nt_asm's) and read N
+// staged rows (1 KiB apart, this lane's 16 B each) in ONE asm unit ending in
+// lgkmcnt(0): its outputs are ready when it ends, as the compiler assumes.
+template <int N>
+__device__ __forceinline__ void lds_collect(V4* x, const u32x4* stage_lane, uint32_t tok) {
+  static_assert(N == 8 || N == 10, "lds_collect: 8 or 10 rows");
+  const uint32_t ad = lds_addr(stage_lane);
+  u32x4 v[10];
+  if constexpr (N == 10) {
+    asm("s_waitcnt vmcnt(0)\n\t"
+        "ds_read_b128 %0, %10\n\t"
+        "ds_read_b128 %1, %10 offset:1024\n\t"
+        "ds_read_b128 %2, %10 offset:2048\n\t"
+        "ds_read_b128 %3, %10 offset:3072\n\t"
+        "ds_read_b128 %4, %10 offset:4096\n\t"
+        "ds_read_b128 %5, %10 offset:5120\n\t"
+        "ds_read_b128 %6, %10 offset:6144\n\t"
+        "ds_read_b128 %7, %10 offset:7168\n\t"
+        "ds_read_b128 %8, %10 offset:8192\n\t"
+        "ds_read_b128 %9, %10 offset:9216\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+          "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9])
+        : "v"(ad), "s"(tok));
+  } else {
+    asm("s_waitcnt vmcnt(0)\n\t"
+        "ds_read_b128 %0, %8\n\t"
+        "ds_read_b128 %1, %8 offset:1024\n\t"
+        "ds_read_b128 %2, %8 offset:2048\n\t"
+        "ds_read_b128 %3, %8 offset:3072\n\t"
+        "ds_read_b128 %4, %8 offset:4096\n\t"
+        "ds_read_b128 %5, %8 offset:5120\n\t"
+        "ds_read_b128 %6, %8 offset:6144\n\t"
+        "ds_read_b128 %7, %8 offset:7168\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+          "=&v"(v[7])
+        : "v"(ad), "s"(tok));
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) x[k] = V4{{v[k].x, v[k].y, v[k].z, v[k].w}};
+}
+
 // store the first nb (1..16) bytes of a chunk
 template <int NT>
 __device__ __forceinline__ void store16(uint8_t* p, const V4& y, uint32_t nb) {
