@@ -281,6 +281,48 @@ def test_host_api_pipelined(gpu):
         fec.host_free(buf)
 
 
+@pytest.mark.parametrize("offset,pitch,data_only", [(256, 1360, False), (3, 1353, False), (16, 1360, True)])
+def test_host_reconstruct_pinned_erased_rows_only(gpu, offset, pitch, data_only):
+    """Pinned host batches get only their erased rows back, written by the
+    device through the batch's mapping (k_erased_out) -- at an interior
+    pointer of the allocation, 16-B aligned (vector form) or not (byte form),
+    with failing groups left untouched and DATA_ONLY leaving parity rows."""
+    d, p, n, S, G = 10, 3, 13, 1350, 700
+    host = _rand(G, n, pitch, 91 + offset).numpy()
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    rng = np.random.default_rng(offset)
+    masks = []
+    for g in range(G):
+        k = int(rng.integers(0, p + 2)) if g % 50 else p + 1  # every 50th group: too few shards
+        masks.append(((1 << n) - 1) & ~int(sum(1 << int(r) for r in rng.choice(n, k, replace=False))))
+    masks = np.array(masks, dtype=np.uint64)
+    inp = want.copy()
+    for g, m in enumerate(masks):
+        for r in range(n):
+            if not (int(m) >> r) & 1:
+                inp[g, r, :S] = rng.integers(0, 256, S, dtype=np.uint8)  # garbage in erased rows
+    enc = fec.New(d, p)
+    buf = fec.host_alloc(G * n * pitch + 4096)
+    try:
+        arr = buf[offset:offset + G * n * pitch].reshape(G, n, pitch)
+        arr[:] = inp
+        st = np.full(G, -1, np.int8)
+        agg = enc.reconstruct_host(arr, masks, S, data_only=data_only, status=st)
+        ok = np.array([bin(int(m)).count("1") >= d for m in masks])
+        assert (st[ok] == 0).all() and (st[~ok] != 0).all() and agg == st[~ok][0]
+        got = arr.copy()
+    finally:
+        fec.host_free(buf)
+    assert np.array_equal(got[~ok], inp[~ok]), "failing groups must be untouched"
+    assert np.array_equal(got[:, :, S:], inp[:, :, S:]), "padding bytes must be untouched"
+    if data_only:
+        assert np.array_equal(got[ok][:, :d, :S], want[ok][:, :d, :S])
+        assert np.array_equal(got[ok][:, d:, :S], inp[ok][:, d:, :S]), "DATA_ONLY must leave parity rows"
+    else:
+        assert np.array_equal(got[ok][:, :, :S], want[ok][:, :, :S])
+
+
 @pytest.mark.parametrize("d,p,S,pitch", [(10, 3, 1350, 1360), (32, 8, 9000, 9008), (6, 2, 77, 80)])
 def test_shard_major_layout(gpu, d, p, S, pitch):
     """Planar [d+p][G][pitch] batches (ugo_fec_*_strided) give the same bytes."""

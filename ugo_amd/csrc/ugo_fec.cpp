@@ -324,6 +324,21 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
     tmp_status.resize(groups);
     status = tmp_status.data();
   }
+  // Reconstruct into pinned host memory: only the erased rows come back, written
+  // by k_erased_out through the batch's device mapping (2 of 13 rows for the
+  // headline (10,3) case instead of all 13).  Pageable memory: every row.
+  uint8_t* mapped = nullptr;
+  if (recon) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, shards) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer) {
+      mapped = static_cast<uint8_t*>(at.devicePointer);
+      if (at.hostPointer) mapped += shards - static_cast<uint8_t*>(at.hostPointer);  // interior pointer
+    }
+    else
+      (void)hipGetLastError();  // pageable: clear the sticky lookup error
+  }
+  const uint64_t outmask = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? ((uint64_t(1) << c->d) - 1)
+                                                                   : (c->n >= 64 ? ~uint64_t(0) : ((uint64_t(1) << c->n) - 1));
   size_t chunk = 0;
   for (size_t g0 = 0; g0 < groups; g0 += per, ++chunk) {
     const int si = static_cast<int>(chunk % kStreams);
@@ -355,9 +370,23 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
       st = reconstruct_dev(c, dev, c->d_mask[si], gn, S, interleaved(c, pitch), flags, c->d_status[si], s);
       if (st) return st;
-      // all rows back: present rows and padding come back byte-identical (they
-      // were copied in above and the kernels write only erased rows' [0, S))
-      e = hipMemcpyAsync(host, dev, gn * gbytes, hipMemcpyDeviceToHost, s);
+      if (mapped) {
+        ugo::kern::ErasedOut o{};
+        o.src = dev;
+        o.dst = mapped + g0 * gbytes;
+        o.present = c->d_mask[si];
+        o.status = c->d_status[si];
+        o.groups = gn;
+        o.pitch = pitch;
+        o.outmask = outmask;
+        o.n = static_cast<uint32_t>(c->n);
+        o.S = static_cast<uint32_t>(S);
+        e = ugo::kern::launch_erased_out(o, s);
+      } else {
+        // all rows back: present rows and padding come back byte-identical (they
+        // were copied in above and the kernels write only erased rows' [0, S))
+        e = hipMemcpyAsync(host, dev, gn * gbytes, hipMemcpyDeviceToHost, s);
+      }
       if (e == hipSuccess) e = hipMemcpyAsync(status + g0, c->d_status[si], gn, hipMemcpyDeviceToHost, s);
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
     }
