@@ -91,9 +91,9 @@ int main(int argc, char** argv) {
   add(k_encode_g<32, 8, 0, 8>, a, enc_bytes, "enc const-network lds-dma 8 rows");
   add(k_apply_q<8, 0, 1, 1, 4>, ae, enc_bytes, "enc perm-tables streaming ring4 nt1");
   add(k_apply_q<8, 0, 1, 1, 8>, ae, enc_bytes, "enc perm-tables streaming ring8 nt1");
-  add(k_apply_q<8, 2, 1, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt1 (production)");
+  add(k_apply_q<8, 2, 1, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt1");
   add(k_apply_q<8, 2, 1, 1, 8>, ar, dec_bytes, "dec perm streaming ring8 nt1");
-  add(k_apply_q<8, 2, 3, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt3");
+  add(k_apply_q<8, 2, 3, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt3 (production)");
   add(k_apply_q<8, 2, 0, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt0");
   add(k_apply<32, 2, 3>, ar, dec_bytes, "dec masked-horner k_apply nt3 (before)");
   vars.push_back({"k_prepare (8192 groups)", 0.0, [=]() { launch_prepare(pr, G, 0); }, {}});
