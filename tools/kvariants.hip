@@ -110,6 +110,31 @@ __global__ __launch_bounds__(256) void k_pattern_rec(Batch a) {
   }
 }
 
+// Memory-pattern probes for the random-erasure reconstruct: READS 0 = the
+// first 10 present rows (the real survivor set), 1 = every present row (11 of
+// 13: no read gaps), 2 = all 13 rows; then the erased rows are written.
+template <int READS>
+__global__ __launch_bounds__(256) void k_pattern_probe(Batch a) {
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t gl = item / a.chunks;
+  const uint32_t c = item - gl * a.chunks;
+  const uint64_t m = a.present[a.g0 + gl];
+  uint8_t* gp = a.base + (a.g0 + gl) * a.gstride + static_cast<uint64_t>(c) * 16u;
+  V4 y{{0u, 0u, 0u, 0u}};
+  int taken = 0;
+#pragma unroll
+  for (int r = 0; r < 13; ++r) {
+    const bool pres = (m >> r) & 1u;
+    const bool rd = READS == 2 ? true : (READS == 1 ? pres : (pres && taken < 10));
+    taken += pres;
+    if (rd) xor4(y, load16<1>(gp + static_cast<uint64_t>(r) * a.rstride));
+  }
+#pragma unroll
+  for (int r = 0; r < 13; ++r)
+    if (!((m >> r) & 1u)) { y.v[0] += r; store16<0>(gp + static_cast<uint64_t>(r) * a.rstride, y, 16); }
+}
+
 int main(int argc, char** argv) {
   const int d = 10, p = 3, n = 13;
   const uint32_t S = 1350, pitch = 1360;
@@ -194,6 +219,17 @@ int main(int argc, char** argv) {
     Batch bu = b;
     bu.desc = dtab + hf[0] * stride;
     add(k_apply<10, 0, 3>, bu, dec_bytes, "dec " + L + " nt3 fixed-pattern uniform-desc");
+    // fixed pattern: every wave takes k_apply_p's uniform path (dA == dB, no
+    // per-lane table pick); against the compute-free pattern of the same rows
+    add(k_apply_p<10, 1, 1>, bf, dec_bytes, "dec " + L + " perm nt1 fixed-pattern (no picks)");
+    add(k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 10>, bf, dec_bytes, "dec " + L + " perm lds-dma fixed-pattern (no picks)");
+    add(k_pattern_rec<1>, bf, dec_bytes, "dec " + L + " MEMORY PATTERN ONLY nt1 fixed-pattern");
+    add(k_pattern_rec<1, true>, bf, dec_bytes, "dec " + L + " MEMORY PATTERN ONLY lds-dma fixed-pattern");
+    add(k_pattern_probe<0>, b, dec_bytes, "dec " + L + " PROBE read first-10-present, write erased");
+    add(k_pattern_probe<1>, b, dec_bytes, "dec " + L + " PROBE read all 11 present, write erased");
+    add(k_pattern_probe<2>, b, dec_bytes, "dec " + L + " PROBE read all 13, write erased");
+    add(k_pattern_probe<0>, bf, dec_bytes, "dec " + L + " PROBE fixed-pattern first-10");
+    add(k_pattern_probe<1>, bf, dec_bytes, "dec " + L + " PROBE fixed-pattern all 11 present");
   }
 
   // encode -> reconstruct back-to-back (the bench step): the encode's store
