@@ -8,7 +8,9 @@ groups; %HBM roofline".  One step = one pass of the hot path over one batch:
                              with exactly 2 distinct erased shards (uniform over
                              the 78 patterns, BASELINE configs[2])
 Inputs are resident in HBM before the timed region (synthetic, device-generated
-random bytes).  Algorithmic bytes per group: encode (d+p)*S,
+random bytes).  Steps alternate between 2 independent batches (--batches), so
+every step works on a batch none of whose lines sit in the Infinity Cache --
+the state a fresh batch of packets arrives in.  Algorithmic bytes per group: encode (d+p)*S,
 reconstruct (d+e)*S; value = sum over ranks / max-over-ranks time, in GiB/s.
 
 Multi-GPU (torchrun, one process per GPU): packet groups are independent, so
@@ -53,6 +55,11 @@ def parse():
     ap.add_argument("--shard-size", type=int, default=1350)
     ap.add_argument("--pitch", type=int, default=0, help="row pitch in HBM (default: shard size rounded to 16)")
     ap.add_argument("--erasures", type=int, default=2)
+    ap.add_argument("--batches", type=int, default=2,
+                    help="rotate the steps over this many independent batches per GPU (step k works on batch "
+                         "k mod B). With B >= 2 every step meets a cold batch, as a fresh batch of packets is: "
+                         "none of its lines are in the 256-MB Infinity Cache. B = 1 re-runs one batch, and the "
+                         "cache then absorbs part of the rewritten parity (DESIGN.md §4)")
     ap.add_argument("--layout", choices=["planar", "interleaved"], default="planar",
                     help="planar = shard-major [d+p][G][pitch] batch; interleaved = [G][d+p][pitch]")
     ap.add_argument("--seed", type=int, default=0x5EED)
@@ -141,13 +148,18 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(args.seed + rank)
     planar = args.layout == "planar"
     shape = (n, G, pitch) if planar else (G, n, pitch)
-    shards = torch.randint(0, 256, shape, dtype=torch.uint8, device=dev, generator=gen)
+    nb = max(1, args.batches)
+    batches = [torch.randint(0, 256, shape, dtype=torch.uint8, device=dev, generator=gen) for _ in range(nb)]
+    shards = batches[0]
     masks, erased = make_masks(G, n, e, args.seed + 1000 + rank, dev)
     stream = torch.cuda.current_stream()
+    cur = [0]
 
     def step():
-        enc.encode_batch(shards, shard_size=S, stream=stream, shard_major=planar)
-        enc.reconstruct_batch(shards, masks, shard_size=S, stream=stream, shard_major=planar)
+        b = batches[cur[0] % nb]
+        cur[0] += 1
+        enc.encode_batch(b, shard_size=S, stream=stream, shard_major=planar)
+        enc.reconstruct_batch(b, masks, shard_size=S, stream=stream, shard_major=planar)
 
     for _ in range(args.warmup):
         step()
@@ -220,11 +232,14 @@ def main():
         verify["all_ranks_ok"] = bool(okt.item())
 
     if rank == 0:
+        payload = G * d * S  # klauspost's convention: data bytes per call (BASELINE.md secondary column)
         kern = {
             "encode": {"avg_ms": round(enc_ms, 5), "bytes_per_launch": enc_bytes,
-                       "GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1)},
+                       "GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),
+                       "payload_GBps": round(payload / (enc_ms * 1e-3) / 1e9, 1)},
             "reconstruct": {"avg_ms": round(dec_ms, 5), "bytes_per_launch": dec_bytes,
-                            "GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1)},
+                            "GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
+                            "payload_GBps": round(payload / (dec_ms * 1e-3) / 1e9, 1)},
         }
         dom = "encode" if enc_ms >= dec_ms else "reconstruct"
         traffic = None
@@ -252,6 +267,7 @@ def main():
                                    f"{G} groups/GPU", "groups_per_gpu": G, "total_groups": total_groups,
                        "data_shards": d, "parity_shards": p, "shard_size": S, "pitch": pitch, "erasures": e,
                        "layout": "shard-major [d+p][G][pitch]" if planar else "group-major [G][d+p][pitch]",
+                       "batches_per_gpu": nb,
                        "parallelism": f"dp{world} (independent packet groups, no collective)"},
             "pct_hbm_roofline": round(step_bytes_all / world * args.steps / elapsed / (HBM_PEAK_GBS * 1e9), 4),
             "roofline": roof, "kernels": kern, "verify": verify,

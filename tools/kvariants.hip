@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -135,6 +136,96 @@ __global__ __launch_bounds__(256) void k_pattern_probe(Batch a) {
     if (!((m >> r) & 1u)) { y.v[0] += r; store16<0>(gp + static_cast<uint64_t>(r) * a.rstride, y, 16); }
 }
 
+// Compute-free encode pattern: the 10 data rows in (GR of them by LDS-DMA nt,
+// the rest nt register loads), 3 XOR "parity" rows out.
+template <int GR, int NTS>
+__global__ __launch_bounds__(256) void k_pattern_enc(Batch a) {
+  __shared__ u32x4 stage[4][GR ? GR : 1][64];
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const Loc l = locate(a, item);
+  V4 x[10];
+#pragma unroll
+  for (int k = 0; k < GR; ++k) lds_dma16(l.gp + static_cast<uint64_t>(k) * a.rstride, &stage[w][k][0]);
+#pragma unroll
+  for (int k = GR; k < 10; ++k) x[k] = load16<1>(l.gp + static_cast<uint64_t>(k) * a.rstride);
+  if constexpr (GR > 0) {
+    lds_dma_wait();
+#pragma unroll
+    for (int k = 0; k < GR; ++k) x[k] = lds16(&stage[w][k][lane]);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    V4 y = x[i];
+#pragma unroll
+    for (int k = 3; k < 10; ++k)
+      if ((k + i) & 1) xor4(y, x[k]);
+    store16<NTS>(l.gp + static_cast<uint64_t>(10 + i) * a.rstride, y, 16);
+  }
+}
+
+// Persistent, pipelined k_encode_g (A/B only): a wave walks 64-item steps at a
+// grid stride; once step t's rows are in registers, step t+1's row loads are
+// issued into the same stage, streaming while step t is computed and stored.
+template <int D, int P, int NTS, int GR>
+__global__ __launch_bounds__(256) void k_encode_gp(Batch a) {
+  __shared__ u32x4 stage[4][GR][64];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t nsteps = (a.items + 63u) / 64u, stride = gridDim.x * 4u;
+  uint32_t step = blockIdx.x * 4u + w;
+  if (step >= nsteps) return;
+  uint32_t item = step * 64u + lane;
+  Loc l = locate(a, min(item, a.items - 1u));
+  V4 x[D];
+#pragma unroll
+  for (int k = 0; k < GR; ++k) lds_dma16(l.gp + static_cast<uint64_t>(k) * a.rstride, &stage[w][k][0]);
+#pragma unroll
+  for (int k = GR; k < D; ++k) x[k] = load16<1>(l.gp + static_cast<uint64_t>(k) * a.rstride);
+  for (;;) {
+    lds_dma_wait();
+#pragma unroll
+    for (int k = 0; k < GR; ++k) x[k] = lds16(&stage[w][k][lane]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    V4 xc[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) xc[k] = x[k];
+    const uint32_t cur = item;
+    const Loc lc = l;
+    step += stride;
+    const bool more = step < nsteps;
+    if (more) {
+      item = step * 64u + lane;
+      l = locate(a, min(item, a.items - 1u));
+#pragma unroll
+      for (int k = 0; k < GR; ++k) lds_dma16(l.gp + static_cast<uint64_t>(k) * a.rstride, &stage[w][k][0]);
+#pragma unroll
+      for (int k = GR; k < D; ++k) x[k] = load16<1>(l.gp + static_cast<uint64_t>(k) * a.rstride);
+    }
+    if (cur < a.items) cparity_store<D, P, NTS>(lc.gp, a.rstride, lc.nb, xc, std::make_integer_sequence<int, P>{});
+    if (!more) break;
+  }
+}
+
+// Cold-regime ceilings: write-only and copy streams over a whole batch buffer.
+template <int NTS>
+__global__ __launch_bounds__(256) void k_write_stream(Batch a, uint64_t n16) {
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  if (i >= n16) return;
+  const u32x4 v = {static_cast<uint32_t>(i), 1u, 2u, 3u};
+  u32x4* q = reinterpret_cast<u32x4*>(a.base) + i;
+  if constexpr (NTS) __builtin_nontemporal_store(v, q); else *q = v;
+}
+template <int NTS>
+__global__ __launch_bounds__(256) void k_copy_stream(Batch a, uint64_t n16) {
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  if (i >= n16) return;
+  const u32x4* src = reinterpret_cast<const u32x4*>(a.base) + i;
+  u32x4* dst = reinterpret_cast<u32x4*>(a.base) + n16 + i;
+  const u32x4 v = __builtin_nontemporal_load(src);
+  if constexpr (NTS) __builtin_nontemporal_store(v, dst); else *dst = v;
+}
+
 int main(int argc, char** argv) {
   const int d = 10, p = 3, n = 13;
   const uint32_t S = 1350, pitch = 1360;
@@ -247,10 +338,93 @@ int main(int argc, char** argv) {
   pair(k_encode_c<10, 3, 1>, k_apply_p<10, 1, 3>, pl, "pair planar enc-nt1 perm-nt3");
   pair(k_encode_c<10, 3, 3>, k_apply_p<10, 1, 3>, pl, "pair planar enc-nt3 perm-nt3");
   pair(k_encode_c<10, 3, 1>, k_apply_p<10, 1, 0>, pl, "pair planar enc-nt1 perm-nt0");
+  // Cold-HBM regime (argv[3] == "cold"): every launch works on the next of 4
+  // independent batches, so no launch finds its batch's lines in the 256-MB
+  // Infinity Cache.  Only these variants run in that mode.
+  const bool cold = argc > 3 && std::string(argv[3]) == "cold";
+  if (cold) {
+    vars.clear();
+    std::vector<Batch> rot(4, pl);
+    for (int r = 1; r < 4; ++r) {
+      uint8_t* nb;
+      CK(hipMalloc(&nb, G * n * pitch));
+      CK(hipMemcpy(nb, buf, G * n * pitch, hipMemcpyDeviceToDevice));
+      rot[r].base = nb;
+    }
+    auto cnt = std::make_shared<int>(0);
+    auto addr = [&](auto kern, double bytes, std::string nm) {
+      const uint32_t grid = (pl.items + 255) / 256;
+      vars.push_back({nm, bytes, [=]() { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+    };
+    auto pairr = [&](auto ke, auto kd, std::string nm) {
+      const uint32_t grid = (pl.items + 255) / 256;
+      vars.push_back({nm, enc_bytes + dec_bytes, [=]() {
+        const Batch& b = rot[(*cnt)++ & 3];
+        hipLaunchKernelGGL(ke, dim3(grid), dim3(256), 0, 0, b);
+        hipLaunchKernelGGL(kd, dim3(grid), dim3(256), 0, 0, b);
+      }, {}});
+    };
+    addr(k_encode_g<10, 3, 0, 8>, enc_bytes, "COLD enc lds-dma 8");
+    addr(k_encode_g<10, 3, 2, 8>, enc_bytes, "COLD enc lds-dma 8, nt stores (production)");
+    addr(k_encode_g<10, 3, 0, 10>, enc_bytes, "COLD enc lds-dma 10");
+    addr(k_encode_g<10, 3, 2, 10>, enc_bytes, "COLD enc lds-dma 10, nt stores");
+    addr(k_encode_c<10, 3, 1>, enc_bytes, "COLD enc nt1");
+    addr(k_encode_c<10, 3, 3>, enc_bytes, "COLD enc nt3");
+    addr(k_encode_c<10, 3, 0>, enc_bytes, "COLD enc nt0");
+    addr(k_apply_p<10, 1, 1>, dec_bytes, "COLD dec perm nt1");
+    addr(k_apply_p<10, 1, 3>, dec_bytes, "COLD dec perm nt3 (production)");
+    addr(k_apply_p<10, 1, 0>, dec_bytes, "COLD dec perm nt0");
+    addr(k_apply_p<10, 1, 2>, dec_bytes, "COLD dec perm nt stores only");
+    addr(k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>, dec_bytes, "COLD dec perm lds-dma, nt stores");
+    addr(k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 10>, dec_bytes, "COLD dec perm lds-dma");
+    addr(k_pattern_rec<3>, dec_bytes, "COLD dec MEMORY PATTERN ONLY nt3");
+    addr(k_pattern_rec<3, true>, dec_bytes, "COLD dec MEMORY PATTERN ONLY lds-dma, nt stores");
+    addr(k_apply_p<10, 1, 3, 1, 1, 3, true, 0, 10>, dec_bytes, "COLD dec perm lds-dma, nt stores, emax3");
+    addr(k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 8>, dec_bytes, "COLD dec perm lds-dma 8, nt stores");
+    {
+      const uint64_t bytes = G * n * pitch, n16w = bytes / 16, n16c = bytes / 32;
+      vars.push_back({"COLD CEILING write-only stream nt", double(bytes), [=]() {
+        hipLaunchKernelGGL(k_write_stream<1>, dim3((n16w + 255) / 256), dim3(256), 0, 0, rot[(*cnt)++ & 3], n16w); }, {}});
+      vars.push_back({"COLD CEILING write-only stream plain", double(bytes), [=]() {
+        hipLaunchKernelGGL(k_write_stream<0>, dim3((n16w + 255) / 256), dim3(256), 0, 0, rot[(*cnt)++ & 3], n16w); }, {}});
+      vars.push_back({"COLD CEILING copy (half buffer -> other half) nt", double(bytes), [=]() {
+        hipLaunchKernelGGL(k_copy_stream<1>, dim3((n16c + 255) / 256), dim3(256), 0, 0, rot[(*cnt)++ & 3], n16c); }, {}});
+      vars.push_back({"COLD CEILING copy (half buffer -> other half) nt loads, plain stores", double(bytes), [=]() {
+        hipLaunchKernelGGL(k_copy_stream<0>, dim3((n16c + 255) / 256), dim3(256), 0, 0, rot[(*cnt)++ & 3], n16c); }, {}});
+    }
+    addr(k_pattern_enc<0, 2>, enc_bytes, "COLD enc MEMORY PATTERN ONLY nt loads+stores");
+    addr(k_pattern_enc<8, 2>, enc_bytes, "COLD enc MEMORY PATTERN ONLY lds-dma 8, nt stores");
+    addr(k_pattern_enc<10, 2>, enc_bytes, "COLD enc MEMORY PATTERN ONLY lds-dma 10, nt stores");
+    for (uint32_t gp : {1280u, 2560u}) {
+      vars.push_back({"COLD enc lds-dma 10 pipelined persistent, nt stores, grid " + std::to_string(gp), enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_gp<10, 3, 2, 10>), dim3(gp), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD enc lds-dma 6 pipelined persistent, nt stores, grid " + std::to_string(gp), enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_gp<10, 3, 2, 6>), dim3(gp), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+    }
+    pairr(k_encode_g<10, 3, 2, 10>, k_apply_p<10, 1, 3>, "COLD pair enc lds-dma 10 + dec nt3 reg");
+    pairr(k_encode_c<10, 3, 3>, k_apply_p<10, 1, 3>, "COLD pair enc nt3 reg + dec nt3 reg");
+    pairr(k_encode_c<10, 3, 3>, k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>, "COLD pair enc nt3 reg + dec lds-dma");
+    pairr(k_encode_g<10, 3, 0, 8>, k_apply_p<10, 1, 1>, "COLD pair old production");
+    pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>, "COLD pair enc lds-dma 8 + dec lds-dma");
+    pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 3>, "COLD pair production (enc lds-dma 8 + dec nt3 reg, nt stores both)");
+    pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 1>, "COLD pair nt stores encode");
+  }
+  if (!cold) {
   // LDS-DMA (global_load_lds_dwordx4 nt) row loads; profiles/r1/kvariants_xcd_rstride.jsonl
   // holds the row-stride sweep (+-2%, kept at G * pitch)
   add(k_encode_g<10, 3, 0>, pl, enc_bytes, "enc planar lds-dma nt");
   add(k_encode_g<10, 3, 0, 8>, pl, enc_bytes, "enc planar lds-dma nt 8 rows + 2 reg");
+  add(k_encode_g<10, 3, 0, 9>, pl, enc_bytes, "enc planar lds-dma nt 9 rows + 1 reg");
+  add(k_encode_g<10, 3, 0, 7>, pl, enc_bytes, "enc planar lds-dma nt 7 rows + 3 reg");
+  {
+    const uint32_t g128 = (pl.items + 127) / 128, g512 = (pl.items + 511) / 512;
+    vars.push_back({"enc planar lds-dma nt 8 rows, block 128", enc_bytes,
+                    [=]() { hipLaunchKernelGGL((k_encode_g<10, 3, 0, 8, 128>), dim3(g128), dim3(128), 0, 0, pl); }, {}});
+    vars.push_back({"enc planar lds-dma nt 8 rows, block 512", enc_bytes,
+                    [=]() { hipLaunchKernelGGL((k_encode_g<10, 3, 0, 8, 512>), dim3(g512), dim3(512), 0, 0, pl); }, {}});
+    vars.push_back({"enc planar lds-dma nt 8 rows, block 64", enc_bytes,
+                    [=]() { hipLaunchKernelGGL((k_encode_g<10, 3, 0, 8, 64>), dim3((pl.items + 63) / 64), dim3(64), 0, 0, pl); }, {}});
+  }
   add(k_encode_g<10, 3, 0, 6>, pl, enc_bytes, "enc planar lds-dma nt 6 rows + 4 reg");
   add(k_encode_g<10, 3, 0, 5>, pl, enc_bytes, "enc planar lds-dma nt 5 rows + 5 reg");
   add(k_encode_g<10, 3, 0, 3>, pl, enc_bytes, "enc planar lds-dma nt 3 rows + 7 reg");
@@ -260,6 +434,8 @@ int main(int argc, char** argv) {
   pair(k_encode_g<10, 3, 0, 8>, k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 10>, pl, "pair planar lds-dma enc 8 + perm lds-dma 10");
   add(k_pattern_rec<1, true>, pl, dec_bytes, "dec planar MEMORY PATTERN ONLY lds-dma nt (xor, no GF)");
   pair(k_encode_g<10, 3, 0, 8>, k_apply_p<10, 1, 1>, pl, "pair planar lds-dma enc 8 rows + perm-nt1");
+
+  }  // !cold
 
   {  // LDS-DMA variants must reproduce the register-load kernels bit for bit
     const uint32_t grid = (pl.items + 255) / 256;
