@@ -183,7 +183,6 @@ int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size
 #define UGO_FEC_KERNEL_RX 5          /* ugo_fec_rx_assemble                     */
 #define UGO_FEC_KERNEL_TX 6          /* ugo_fec_tx_assemble                     */
 #define UGO_FEC_KERNEL_PACKET 7      /* ugo_fec_packet_decode                   */
-#define UGO_FEC_KERNEL_HOST_OUT 8    /* host path: erased rows -> pinned host   */
 
 typedef struct ugo_fec_launch_time {
   uint32_t kernel; /* UGO_FEC_KERNEL_* */

@@ -282,9 +282,9 @@ def test_host_api_pipelined(gpu):
 
 
 @pytest.mark.parametrize("offset,pitch,data_only", [(256, 1360, False), (3, 1353, False), (16, 1360, True)])
-def test_host_reconstruct_pinned_erased_rows_only(gpu, offset, pitch, data_only):
-    """Pinned host batches get only their erased rows back, written by the
-    device through the batch's mapping (k_erased_out) -- at an interior
+def test_host_reconstruct_pinned_zero_copy(gpu, offset, pitch, data_only):
+    """Pinned host batches are reconstructed zero-copy: the kernels read the
+    survivors and write only the erased rows through the batch's mapping -- at an interior
     pointer of the allocation, 16-B aligned (vector form) or not (byte form),
     with failing groups left untouched and DATA_ONLY leaving parity rows."""
     d, p, n, S, G = 10, 3, 13, 1350, 700

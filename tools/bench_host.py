@@ -74,8 +74,10 @@ def host_case(d, p, S, G, emax, reps, pinned=True):
     ok = bool(np.array_equal(arr[:, :, :S], keep[:, :, :S])) and not st.any()
     alg_enc = G * n * S
     alg_dec = int(sum(d + int(e) for e in es) * S)
-    # in: whole groups + masks; out: pinned -> erased rows only (k_erased_out), pageable -> every row; + status
-    dec_pcie = G * n * pitch + 9 * G + (int(sum(int(e) for e in es)) * S if pinned else G * n * pitch)
+    # pinned: zero-copy -- the kernels read d survivor rows per group and write the erased rows over PCIe;
+    # pageable: staged -- whole groups in, whole groups out; + masks and statuses either way
+    e_rows = int(sum(int(e) for e in es))
+    dec_pcie = (G * d * S + e_rows * S if pinned else 2 * G * n * pitch) + 9 * G
     out = [
         {"case": f"host encode ({d}+{p})x{S}", "groups": G, "pinned": pinned, "ms": t_enc * 1e3,
          "alg_GBps": alg_enc / t_enc / 1e9, "pcie_bytes": G * (d * pitch + p * S),

@@ -828,47 +828,6 @@ hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// One wave per group (grid-stride): for each erased row the reconstruct wrote,
-// lanes copy bytes [0, S) in 16-B pieces (VEC: pitch and both bases 16-B
-// aligned, so the piece covering S stays inside the row's pitch and carries
-// the row's own padding bytes back unchanged) or byte by byte otherwise.
-// The stores go over PCIe to pinned host memory; 1 KiB per wave-instruction.
-template <bool VEC>
-__global__ __launch_bounds__(256) void k_erased_out(ErasedOut a) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t nw = (gridDim.x * 256ull) >> 6;
-  for (uint64_t g = (blockIdx.x * 256ull + threadIdx.x) >> 6; g < a.groups; g += nw) {
-    if (a.status[g] != 0) continue;
-    uint64_t m = ~a.present[g] & a.outmask;
-    const uint8_t* sg = a.src + g * a.n * a.pitch;
-    uint8_t* dg = a.dst + g * a.n * a.pitch;
-    while (m) {
-      const uint32_t r = static_cast<uint32_t>(__builtin_ctzll(m));
-      m &= m - 1;
-      const uint8_t* sr = sg + r * a.pitch;
-      uint8_t* dr = dg + r * a.pitch;
-      if constexpr (VEC) {
-        for (uint32_t o = 16u * lane; o < a.S; o += 1024u)
-          *reinterpret_cast<u32x4*>(dr + o) = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sr + o));
-      } else {
-        for (uint32_t o = lane; o < a.S; o += 64u) dr[o] = sr[o];
-      }
-    }
-  }
-}
-
-hipError_t launch_erased_out(const ErasedOut& a, hipStream_t s) {
-  if (a.groups == 0) return hipSuccess;
-  const bool vec = a.pitch % 16 == 0 && reinterpret_cast<uintptr_t>(a.src) % 16 == 0 &&
-                   reinterpret_cast<uintptr_t>(a.dst) % 16 == 0;
-  const uint64_t blocks = std::min<uint64_t>((a.groups + 3) / 4, 2048);
-  if (vec)
-    launch(kKHostOut, k_erased_out<true>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a);
-  else
-    launch(kKHostOut, k_erased_out<false>, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
 hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s) {
   launch(kKPrepare, k_prepare, dim3(groups), dim3(64), 0, s, a);
   return hipGetLastError();

@@ -54,21 +54,6 @@ hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s);
 hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s);
 hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s);
 
-// Host path: copy the rows a reconstruct wrote (erased rows within `outmask`,
-// groups with status 0) from the device stage to the caller's host rows
-// through their device mapping -- instead of copying every row back.
-struct ErasedOut {
-  const uint8_t* src;       // device stage, interleaved [G][n][pitch]
-  uint8_t* dst;             // device-mapped pinned host batch, same layout
-  const uint64_t* present;  // device presence masks
-  const int8_t* status;     // device per-group status
-  uint64_t groups;
-  uint64_t pitch;
-  uint64_t outmask;         // rows the reconstruct writes: (1 << n) - 1, or data rows only
-  uint32_t n;
-  uint32_t S;
-};
-hipError_t launch_erased_out(const ErasedOut& a, hipStream_t s);
 
 }  // namespace kern
 }  // namespace ugo

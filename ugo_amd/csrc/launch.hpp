@@ -25,7 +25,6 @@ enum KernelId : uint32_t {
   kKRx = 5,           // RX group assembly
   kKTx = 6,           // TX group assembly
   kKPacket = 7,       // packet wire decode
-  kKHostOut = 8,      // host path: erased rows written to pinned host memory
 };
 
 struct LaunchTimer {
