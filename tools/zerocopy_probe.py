@@ -2,7 +2,8 @@
 """Host-path probe: reconstruct a pinned HOST batch in place with the device
 kernels reading survivors and writing erased rows straight through PCIe
 (zero-copy: the batch's device mapping), against the staged host path
-(ugo_fec_reconstruct_host: H2D of whole groups -> kernel -> erased rows back).
+(before zero-copy became ugo_fec_reconstruct_host's pinned path: H2D of whole
+groups -> kernel -> erased rows back).
 The zero-copy form moves d survivor rows in per group instead of all d+p.
 Not product code."""
 import ctypes
