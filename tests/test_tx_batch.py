@@ -85,6 +85,7 @@ def test_oracle_tx_group_matches_reused_buffer_loop_on_full_packets():
 @pytest.mark.parametrize("d,p,max_len,G,key,wrap", [
     (10, 3, 1476, 96, KEY, False),   # headline geometry, compile-time network
     (10, 3, 1476, 40, None, True),   # seqids wrap at paws mid-batch (markFEC)
+    (10, 3, 500, 64, KEY, False),    # < 64 chunks per packet: per-lane lengths (a wave spans > 2 groups)
     (5, 3, 1476, 40, KEY, False),    # descriptor kernel
     (12, 4, 700, 24, KEY, False),
     (32, 8, 9006, 6, KEY, False),    # jumbo network

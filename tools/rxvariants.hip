@@ -115,6 +115,32 @@ int main(int argc, char** argv) {
   vs.push_back({"PATTERN: aligned scatter copy, wave/packet", [&] { k_copy_scatter<<<2048, 256>>>(a, d_row); }, {}});
   vs.push_back({"PATTERN: linear copy of the same bytes",
                 [&] { k_copy_linear<<<4096, 256>>>(reinterpret_cast<const u32x4*>(d_wire), reinterpret_cast<u32x4*>(d_lin), npk * 1480 / 16); }, {}});
+  // Cold regime (argv[2] == "cold"): every launch takes the next of 3 wire
+  // rings and 3 batches, so none of its lines are in the Infinity Cache.
+  std::vector<RxArgs> rot(3, a);
+  std::vector<uint8_t*> lin(3, d_lin);
+  int cnt = 0;
+  auto nx = [&]() -> const RxArgs& { return rot[cnt++ % 3]; };
+  if (argc > 2 && std::string(argv[2]) == "cold") {
+    vs.clear();
+    for (int r = 1; r < 3; ++r) {
+      uint8_t *w2, *s2, *l2;
+      CK(hipMalloc(&w2, wire.size()));
+      CK(hipMalloc(&s2, n * G * pitch + 64));
+      CK(hipMalloc(&l2, npk * slot));
+      CK(hipMemcpy(w2, d_wire, wire.size(), hipMemcpyDeviceToDevice));
+      rot[r].wire = w2;
+      rot[r].shards = s2;
+      lin[r] = l2;
+    }
+    vs.push_back({"COLD k_rx_place<3> plain loads + stores", [&] { k_rx_place<3, 0, 0><<<blocks, 256>>>(nx()); }, {}});
+    vs.push_back({"COLD k_rx_place<3> nt loads", [&] { k_rx_place<3, 0, 1><<<blocks, 256>>>(nx()); }, {}});
+    vs.push_back({"COLD k_rx_place<3> nt stores", [&] { k_rx_place<3, 0, 2><<<blocks, 256>>>(nx()); }, {}});
+    vs.push_back({"COLD k_rx_place<3> nt loads + stores", [&] { k_rx_place<3, 0, 3><<<blocks, 256>>>(nx()); }, {}});
+    vs.push_back({"COLD PATTERN: linear copy of the same bytes", [&] {
+      const int r = cnt++ % 3;
+      k_copy_linear<<<4096, 256>>>(reinterpret_cast<const u32x4*>(rot[r].wire), reinterpret_cast<u32x4*>(lin[r]), npk * 1480 / 16); }, {}});
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

@@ -12,6 +12,40 @@
 
 using namespace ugo::kern;
 
+// Compute-free TX pattern: the same 10 packet-chunk loads and 13 wire-chunk
+// stores per thread as k_tx_c (full-length packets), parity = plain XORs.
+template <int NTS>
+__global__ __launch_bounds__(256) void k_tx_pattern(TxArgs a) {
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.groups * a.chunks) return;
+  const uint64_t g = item / a.chunks;
+  const uint32_t o = 16u * (item - static_cast<uint32_t>(g) * a.chunks);
+  const uint8_t* src = a.pkts + g * 10 * a.slot_in + o;
+  uint8_t* dst = a.wire + g * 13 * a.slot_out + o;
+  V4 x[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) x[k] = load16<1>(src + static_cast<uint64_t>(k) * a.slot_in);
+#pragma unroll
+  for (int k = 0; k < 10; ++k) store16<NTS>(dst + static_cast<uint64_t>(k) * a.slot_out, x[k], 16u);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    V4 y = x[i];
+#pragma unroll
+    for (int k = 3; k < 10; ++k)
+      if ((k + i) & 1) xor4(y, x[k]);
+    store16<NTS>(dst + static_cast<uint64_t>(10 + i) * a.slot_out, y, 16u);
+  }
+}
+
+namespace ugo {
+namespace kern {
+LaunchTimer*& current_timer() {
+  static thread_local LaunchTimer* t = nullptr;
+  return t;
+}
+}  // namespace kern
+}  // namespace ugo
+
 int main(int argc, char** argv) {
   const uint64_t G = argc > 1 ? atoll(argv[1]) : 65536;
   const int rounds = argc > 2 ? atoi(argv[2]) : 11;
@@ -43,9 +77,28 @@ int main(int argc, char** argv) {
   add(k_tx_c<10, 3, 3, false>, "tx nt3 vector-lens");
   add(k_tx_c<10, 3, 3, true>, "tx nt3 scalar-lens");
   add(k_tx_c<10, 3, 0, true>, "tx nt0 scalar-lens");
+  // cold regime (argv[3] == "cold"): each launch on the next of 3 packet / wire buffer pairs
+  std::vector<TxArgs> rot(3, a);
+  int cnt = 0;
+  if (argc > 3 && std::string(argv[3]) == "cold") {
+    for (int r = 1; r < 3; ++r) {
+      CK(hipMalloc(&rot[r].pkts, G * d * slot));
+      CK(hipMemset(const_cast<uint8_t*>(rot[r].pkts), 0x3c, G * d * slot));
+      CK(hipMalloc(&rot[r].wire, G * n * slot));
+    }
+    auto addc = [&](auto k, std::string nm) {
+      vars.push_back({nm, [=, &rot, &cnt]() { hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, rot[cnt++ % 3]); }, {}});
+    };
+    addc(k_tx_c<10, 3, 0, false>, "COLD tx nt0");
+    addc(k_tx_c<10, 3, 1, false>, "COLD tx nt1 (nt loads)");
+    addc(k_tx_c<10, 3, 2, false>, "COLD tx nt2 (nt stores)");
+    addc(k_tx_c<10, 3, 3, false>, "COLD tx nt3 (nt loads + stores)");
+    addc(k_tx_pattern<0>, "COLD TX MEMORY PATTERN ONLY (nt loads, plain stores)");
+    addc(k_tx_pattern<2>, "COLD TX MEMORY PATTERN ONLY (nt loads + stores)");
+  }
   // correctness: every variant writes the same wire bytes
   std::vector<uint8_t> ref(G * n * slot), got(G * n * slot);
-  for (size_t v = 0; v < vars.size(); ++v) {
+  for (size_t v = 0; v < 5; ++v) {
     CK(hipMemset(wire, 0, G * n * slot));
     vars[v].go();
     CK(hipMemcpy(v ? got.data() : ref.data(), wire, ref.size(), hipMemcpyDeviceToHost));

@@ -145,7 +145,8 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 //  * lengths are clamped to the slot.
 // MODE (A/B timing only, tools/rxvariants.hip): 0 = production, 1 = without
 // the presence atomics, 2 = the same loads and stores without the realignment.
-template <int NP, int MODE = 0>
+// NT: bit 0 nontemporal payload loads, bit 1 nontemporal stores.
+template <int NP, int MODE = 0, int NT = 0>
 __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
   __shared__ uint32_t bstats[4];
   if (threadIdx.x < 4) bstats[threadIdx.x] = 0;
@@ -203,7 +204,8 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const uint32_t o = 16u * (32u * q + hl);
-      A[q] = o < lim ? ld16(pk + o) : zero;
+      A[q] = o < lim ? ((NT & 1) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + o)) : ld16(pk + o))
+                     : zero;
       bx[q] = by[q] = 0u;
       if (hl == 31u && o + 16u < lim) {
         const u32x4 B = ld16(pk + o + 16u);
@@ -241,7 +243,11 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
       }
       const uint32_t nb = a.S - o;
       if (nb >= 16u) {
-        *reinterpret_cast<u32x4*>(dst + o) = u32x4{w[0], w[1], w[2], w[3]};
+        const u32x4 v = {w[0], w[1], w[2], w[3]};
+        if constexpr (NT & 2)
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + o));
+        else
+          *reinterpret_cast<u32x4*>(dst + o) = v;
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -276,11 +282,13 @@ hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
   const uint32_t blocks = rx_blocks(a);
   if (blocks == 0) return hipSuccess;
   const uint32_t passes = ((a.S + 15u) / 16u + 31u) / 32u;
+  // nt loads + stores: on a cold ring and batch 493 vs 552 us with plain ones
+  // (a linear copy of the same bytes: 487 us; tools/rxvariants 15 cold)
   switch (passes) {
-    case 1: launch(kKRx, k_rx_place<1>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 2: launch(kKRx, k_rx_place<2>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 3: launch(kKRx, k_rx_place<3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 4: launch(kKRx, k_rx_place<4>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 1: launch(kKRx, k_rx_place<1, 0, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 2: launch(kKRx, k_rx_place<2, 0, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 3: launch(kKRx, k_rx_place<3, 0, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 4: launch(kKRx, k_rx_place<4, 0, 3>, dim3(blocks), dim3(256), 0, s, a); break;
     default: launch(kKRx, k_rx_scatter, dim3(blocks), dim3(256), 0, s, a); break;
   }
   return hipGetLastError();

@@ -55,10 +55,12 @@ __device__ __forceinline__ void put_header(V4& x, uint32_t seq, uint32_t flag) {
   x.v[1] = (x.v[1] & 0xffff0000u) | flag;        // LE16 flag
 }
 
-// launch policy (tools/txvariants.hip A/B): nontemporal loads of the packet
-// stream; store policy / scalar lengths as measured
-constexpr int kTxNT = 1;
-constexpr bool kTxSL = false;
+// launch policy (tools/txvariants.hip A/B, after the loads-first change):
+// nontemporal loads and stores, lengths by scalar loads -- warm 484 us, cold
+// 500 us (plain stores / vector lengths 490-507 us); the compute-free pattern
+// of the same accesses is 454 us cold
+constexpr int kTxNT = 3;
+constexpr bool kTxSL = true;
 
 struct TxItem {
   uint64_t g;        // absolute group
@@ -128,13 +130,18 @@ __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x)
   t.padc = a.pad ? load16<0>(a.pad + t.o) : V4{{0u, 0u, 0u, 0u}};
   const uint8_t* src = a.pkts + t.g * a.d * a.slot_in + t.o;
   uint8_t* dst = a.wire + t.g * n * a.slot_out + t.o;
+  // all loads first: the stores below may alias the packets as far as the
+  // compiler knows, so a load placed after a store waits for it
+#pragma unroll
+  for (int k = 0; k < DN; ++k) {
+    x[k] = V4{{0u, 0u, 0u, 0u}};
+    if (k < static_cast<int>(a.d) && t.o < Ls[k]) x[k] = load16<1>(src + static_cast<uint64_t>(k) * a.slot_in);
+  }
 #pragma unroll
   for (int k = 0; k < DN; ++k) {
     if (k < static_cast<int>(a.d)) {
       const uint32_t Lk = Ls[k];
-      V4 v{{0u, 0u, 0u, 0u}};
-      if (t.o < Lk) v = load16<1>(src + static_cast<uint64_t>(k) * a.slot_in);
-      v = keep_bytes(v, Lk - min(Lk, t.o));
+      V4 v = keep_bytes(x[k], Lk - min(Lk, t.o));
       if (t.o < Lk) {
         V4 w = v;
         if (m == 0) put_header(w, t.seq0 + k, kTypeData);
@@ -208,14 +215,21 @@ hipError_t launch_tx_assemble(int dmax, const TxArgs& a, hipStream_t s) {
   if (items == 0) return hipSuccess;
   const dim3 grid(static_cast<uint32_t>((items + 255) / 256)), block(256);
   switch (dmax) {
-    case 0:
-      if (a.d == 10 && a.p == 3)
-        launch(kKTx, k_tx_c<10, 3>, grid, block, 0, s, a);
+    case 0: {
+      // scalar lengths need a wave to span at most 2 groups: >= 64 chunks per packet
+      const bool sl = kTxSL && a.chunks >= 64;
+      if (a.d == 10 && a.p == 3 && sl)
+        launch(kKTx, k_tx_c<10, 3, kTxNT, true>, grid, block, 0, s, a);
+      else if (a.d == 10 && a.p == 3)
+        launch(kKTx, k_tx_c<10, 3, kTxNT, false>, grid, block, 0, s, a);
+      else if (a.d == 32 && a.p == 8 && sl)
+        launch(kKTx, k_tx_c<32, 8, kTxNT, true>, grid, block, 0, s, a);
       else if (a.d == 32 && a.p == 8)
-        launch(kKTx, k_tx_c<32, 8>, grid, block, 0, s, a);
+        launch(kKTx, k_tx_c<32, 8, kTxNT, false>, grid, block, 0, s, a);
       else
         return hipErrorInvalidValue;
       break;
+    }
     case 4: launch(kKTx, k_tx_var<4>, grid, block, 0, s, a); break;
     case 8: launch(kKTx, k_tx_var<8>, grid, block, 0, s, a); break;
     case 10: launch(kKTx, k_tx_var<10>, grid, block, 0, s, a); break;
