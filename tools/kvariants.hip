@@ -373,6 +373,9 @@ int main(int argc, char** argv) {
     addr(k_encode_c<10, 3, 0>, enc_bytes, "COLD enc nt0");
     addr(k_apply_p<10, 1, 1>, dec_bytes, "COLD dec perm nt1");
     addr(k_apply_p<10, 1, 3>, dec_bytes, "COLD dec perm nt3 (production)");
+    addr(k_apply_p<10, 1, 3, 0>, dec_bytes, "COLD dec perm nt3 TSEL0 (probe: no per-lane pick, B lanes wrong)");
+    addr(k_apply_p<10, 1, 3, 1, 1, 3>, dec_bytes, "COLD dec perm nt3 emax3");
+    addr(k_apply_p<10, 1, 3, 1, 1, 4, false>, dec_bytes, "COLD dec perm nt3 unpaired");
     addr(k_apply_p<10, 1, 0>, dec_bytes, "COLD dec perm nt0");
     addr(k_apply_p<10, 1, 2>, dec_bytes, "COLD dec perm nt stores only");
     addr(k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>, dec_bytes, "COLD dec perm lds-dma, nt stores");
