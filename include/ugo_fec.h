@@ -129,9 +129,13 @@ int ugo_fec_check_shards(int n, const size_t* lens, int nil_ok, size_t* shard_si
  * XOR with one keystream prefix, `pad`), decode (ugo/fec.go:78-89: LE32 seqid,
  * LE16 flag, payload data[6:]) and the group/slot choice of input
  * (ugo/fec.go:145,175: group = seqid / (d+p), slot = seqid % (d+p)).
- *   wire     device; packet i at wire + i*slot_stride (slot_stride % 16 == 0,
- *            shards 16-B aligned), lens[i] bytes (device uint16).
- *   pad      device keystream >= slot_stride bytes, or NULL (no decryption).
+ *   wire     packet i at wire + i*slot_stride (slot_stride % 16 == 0,
+ *            shards 16-B aligned), lens[i] bytes (uint16).
+ *   pad      keystream >= slot_stride bytes, or NULL (no decryption).
+ * Every buffer may be device memory or pinned host memory (ugo_fec_host_alloc
+ * or registered): pinned buffers are used through their device mapping, so a
+ * recvmmsg ring is read over PCIe by the kernel itself (zero-copy) with no
+ * separate H2D.  Pageable host memory is rejected (UGO_FEC_ERR_INVALID_ARG).
  * A packet whose flag is typeData (0xf1) or typeFEC (0xf2) and whose group is
  * in [first_group, first_group + groups) is written to row seqid % (d+p) of
  * group seqid/(d+p) - first_group of the strided batch: its payload bytes
@@ -144,8 +148,8 @@ int ugo_fec_rx_assemble(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, c
                         uint8_t* shards, size_t shard_size, size_t row_stride, size_t group_stride,
                         uint64_t* present, uint32_t* stats, void* stream);
 
-/* TX group assembly for a batch of `groups` outgoing groups (device memory,
- * stream-ordered, asynchronous) -- replaces the sender loop ugo/conn.go:643-685
+/* TX group assembly for a batch of `groups` outgoing groups (device or pinned
+ * host memory, as for RX; stream-ordered, asynchronous) -- replaces the sender loop ugo/conn.go:643-685
  * (markData, copy into the group buffers, calcECC(group, 6, maxsize),
  * markFEC, ecc[k][:maxsize]) plus crypt.Encrypt (ugo/conn.go:634) per packet:
  *   pkts:   data packet k of group g at pkts + (g*d + k)*slot_in, lens[g*d + k]

@@ -69,7 +69,8 @@ typedef struct ugo_pkt_segment {
 #define UGO_PKT_FEC_FRAMED 1u
 
 /* Decode npackets received packets: packet i is at pkts + i*slot (16-B aligned
- * slots), lens[i] bytes.  pad (nullable, >= slot bytes) is XORed over each
+ * slots), lens[i] bytes.  Buffers: device or pinned host memory (zero-copy,
+ * as for ugo_fec_rx_assemble); pageable host memory is rejected.  pad (nullable, >= slot bytes) is XORed over each
  * packet from byte 0 first (the fixed-key RC4 Decrypt, ugo/conn.go:390).
  * info[npackets]; ranges[npackets][max_ranges][2] = {first, last} packet
  * numbers, highest range first; segs[npackets][max_segments].  A packet that

@@ -50,8 +50,12 @@ def _packets(groups, seed, full_len):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("full_len,encrypt,first_group", [(True, True, 0), (False, True, 5), (False, False, 0)])
-def test_rx_assemble_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_group):
+@pytest.mark.parametrize("full_len,encrypt,first_group,ring", [(True, True, 0, "device"), (False, True, 5, "device"),
+                                                               (False, False, 0, "device"),
+                                                               (False, True, 5, "pinned")])
+def test_rx_assemble_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_group, ring):
+    """ring = "pinned": the packet ring, lengths and pad stay in pinned host
+    memory and the kernel reads them over PCIe (zero-copy)."""
     d, p, n, S, pitch, slot = 10, 3, 13, 1470, 1472, 1488
     total_groups, G = 300, 256
     pk = _packets(total_groups, 11, full_len)
@@ -107,8 +111,12 @@ def test_rx_assemble_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_gro
     sh = torch.full((n, G, pitch), 0xAB, dtype=torch.uint8, device="cuda")  # garbage in unwritten rows
     present = torch.zeros(G, dtype=torch.int64, device="cuda")
     st = torch.zeros(4, dtype=torch.int32, device="cuda")
-    pad = torch.frombuffer(bytearray(ks), dtype=torch.uint8).cuda() if encrypt else None
-    codec.rx_assemble(torch.from_numpy(slots).cuda(), torch.from_numpy(lens.view(np.int16)).cuda(), sh, present,
+    if ring == "pinned":
+        put = lambda t: t.pin_memory()  # noqa: E731
+    else:
+        put = lambda t: t.cuda()  # noqa: E731
+    pad = put(torch.frombuffer(bytearray(ks), dtype=torch.uint8)) if encrypt else None
+    codec.rx_assemble(put(torch.from_numpy(slots)), put(torch.from_numpy(lens.view(np.int16))), sh, present,
                       first_group=first_group, shard_size=S, pad=pad, stats=st)
     assert np.array_equal(present.cpu().numpy().view(np.uint64), masks)
     assert st.cpu().tolist() == stats
@@ -136,3 +144,15 @@ def test_rx_assemble_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_gro
                     assert bytes(got[g, r]) == orig, (g, r)
                     nrec += 1
         assert nrec > 0
+
+
+@pytest.mark.gpu
+def test_rx_assemble_rejects_pageable_host_memory(gpu):
+    """A ring the GPU cannot reach is refused up front, not faulted on."""
+    codec = fec.New(10, 3)
+    ring = torch.zeros((64, 1488), dtype=torch.uint8)  # pageable
+    lens = torch.full((64,), 1476, dtype=torch.int16, device="cuda")
+    sh = torch.zeros((13, 8, 1472), dtype=torch.uint8, device="cuda")
+    present = torch.zeros(8, dtype=torch.int64, device="cuda")
+    with pytest.raises(fec.ErrInvalidArg):
+        codec.rx_assemble(ring, lens, sh, present, shard_size=1470)

@@ -315,6 +315,27 @@ int ensure_stage(ugo_fec* c, size_t pitch) {
   return UGO_FEC_OK;
 }
 
+// Device view of a buffer a kernel will touch: device (or managed) memory as
+// is, pinned host memory through its device mapping (the kernel then reads or
+// writes it over PCIe: zero-copy, e.g. a recvmmsg ring), anything else --
+// pageable host memory the GPU cannot reach -- rejected instead of faulting.
+template <typename T>
+bool device_view(T*& p) {
+  if (!p) return true;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged || at.type == hipMemoryTypeUnified)
+    return true;
+  if (at.type != hipMemoryTypeHost || !at.devicePointer) return false;  // unregistered (pageable) memory
+  auto* base = static_cast<uint8_t*>(at.devicePointer);
+  if (at.hostPointer) base += reinterpret_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(at.hostPointer);
+  p = reinterpret_cast<T*>(base);
+  return true;
+}
+
 // Zero-copy reconstruct of a pinned host batch (see host_path).
 int host_reconstruct_mapped(ugo_fec* c, uint8_t* mapped, const uint64_t* present, size_t groups, size_t S,
                             size_t pitch, unsigned flags, int8_t* status) {
@@ -628,6 +649,9 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   if ((c->n > 1 && row_stride < S) || (groups > 1 && group_stride < S)) return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(wire) || !device_view(lens) || !device_view(pad) || !device_view(shards) ||
+      !device_view(present) || !device_view(stats))
+    return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
   ugo::kern::RxArgs a{};
   a.wire = wire;
@@ -662,6 +686,9 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
     return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(pkts) || !device_view(lens) || !device_view(pad) || !device_view(wire) ||
+      !device_view(wire_lens) || !device_view(status))
+    return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
   ugo::kern::TxArgs a{};
   a.pkts = pkts;
@@ -706,6 +733,9 @@ int ugo_fec_packet_decode(ugo_fec* c, const uint8_t* pkts, size_t slot, const ui
     return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(pkts) || !device_view(lens) || !device_view(pad) || !device_view(info) ||
+      !device_view(ranges) || !device_view(segs))
+    return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
   ugo::kern::PktArgs a{};
   a.pkts = pkts;
