@@ -330,6 +330,7 @@ bool device_view(T*& p) {
   if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged || at.type == hipMemoryTypeUnified)
     return true;
   if (at.type != hipMemoryTypeHost || !at.devicePointer) return false;  // unregistered (pageable) memory
+  if (at.devicePointer == at.hostPointer) return true;  // one address for host and device (ROCm)
   auto* base = static_cast<uint8_t*>(at.devicePointer);
   if (at.hostPointer) base += reinterpret_cast<const uint8_t*>(p) - static_cast<const uint8_t*>(at.hostPointer);
   p = reinterpret_cast<T*>(base);
@@ -393,7 +394,10 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
     uint8_t* mapped = nullptr;
     if (hipPointerGetAttributes(&at, shards) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer) {
       mapped = static_cast<uint8_t*>(at.devicePointer);
-      if (at.hostPointer) mapped += shards - static_cast<uint8_t*>(at.hostPointer);  // interior pointer
+      if (at.hostPointer && at.hostPointer != at.devicePointer)
+        mapped += shards - static_cast<uint8_t*>(at.hostPointer);  // interior pointer
+      else
+        mapped = shards;
     } else {
       (void)hipGetLastError();  // pageable: clear the sticky lookup error
     }
@@ -579,6 +583,7 @@ int ugo_fec_encode_strided(ugo_fec* c, uint8_t* shards, size_t groups, size_t S,
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(shards)) return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
   return encode_dev(c, shards, groups, S, L, static_cast<hipStream_t>(stream));
 }
@@ -597,6 +602,7 @@ int ugo_fec_reconstruct_strided(ugo_fec* c, uint8_t* shards, const uint64_t* pre
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(shards) || !device_view(present) || !device_view(status)) return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
   return reconstruct_dev(c, shards, present, groups, S, L, flags, status, static_cast<hipStream_t>(stream));
 }
