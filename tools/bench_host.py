@@ -73,11 +73,13 @@ def host_case(d, p, S, G, emax, reps, pinned=True):
     t_dec = (time.perf_counter() - t0) / reps
     ok = bool(np.array_equal(arr[:, :, :S], keep[:, :, :S])) and not st.any()
     alg_enc = G * n * S
-    alg_dec = int(sum(d + int(e) for e in es) * S)
+    alg_dec = int(sum(d + int(e) for e in es if int(e) > 0) * S)  # a group with no erasure moves nothing
     # pinned: zero-copy -- the kernels read d survivor rows per group and write the erased rows over PCIe;
     # pageable: staged -- whole groups in, whole groups out; + masks and statuses either way
+    # (zero-copy reads nothing for a group with no erasure)
     e_rows = int(sum(int(e) for e in es))
-    dec_pcie = (G * d * S + e_rows * S if pinned else 2 * G * n * pitch) + 9 * G
+    lossy = int(sum(1 for e in es if int(e) > 0))
+    dec_pcie = (lossy * d * S + e_rows * S if pinned else 2 * G * n * pitch) + 9 * G
     out = [
         {"case": f"host encode ({d}+{p})x{S}", "groups": G, "pinned": pinned, "ms": t_enc * 1e3,
          "alg_GBps": alg_enc / t_enc / 1e9, "pcie_bytes": G * (d * pitch + p * S),
@@ -115,7 +117,7 @@ def device_case(d, p, S, G, emax, reps):
     torch.cuda.synchronize()
     te = e[0].elapsed_time(e[1]) / reps * 1e-3
     td = e[1].elapsed_time(e[2]) / reps * 1e-3
-    alg_dec = int(sum(d + int(x) for x in es) * S)
+    alg_dec = int(sum(d + int(x) for x in es if int(x) > 0) * S)  # a group with no erasure moves nothing
     return [{"case": f"device encode ({d}+{p})x{S}", "groups": G, "us": te * 1e6, "alg_GBps": G * n * S / te / 1e9},
             {"case": f"device reconstruct ({d}+{p})x{S} e~U[0,{emax}]", "groups": G, "us": td * 1e6,
              "alg_GBps": alg_dec / td / 1e9}]
