@@ -236,10 +236,12 @@ def main():
         kern = {
             "encode": {"avg_ms": round(enc_ms, 5), "bytes_per_launch": enc_bytes,
                        "GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),
-                       "payload_GBps": round(payload / (enc_ms * 1e-3) / 1e9, 1)},
+                       "payload_GBps": round(payload / (enc_ms * 1e-3) / 1e9, 1),
+                       "frac": round(enc_bytes / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "reconstruct": {"avg_ms": round(dec_ms, 5), "bytes_per_launch": dec_bytes,
                             "GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
-                            "payload_GBps": round(payload / (dec_ms * 1e-3) / 1e9, 1)},
+                            "payload_GBps": round(payload / (dec_ms * 1e-3) / 1e9, 1),
+                            "frac": round(dec_bytes / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
         }
         dom = "encode" if enc_ms >= dec_ms else "reconstruct"
         traffic = None
