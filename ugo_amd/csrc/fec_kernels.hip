@@ -8,7 +8,10 @@
 // chunks, so a wave's load of one row is 1 KiB contiguous), computes every
 // output row's chunk in registers and stores it.  Each input byte is read from
 // HBM exactly once and each output byte written once: the kernels are
-// HBM-bound byte-field codecs, no MFMA, no LDS on the streaming path.
+// HBM-bound byte-field codecs, no MFMA.  The headline encode (k_encode_g)
+// stages most of its row loads through LDS by LDS-DMA (global_load_lds_dwordx4
+// nt, 1 KiB per row per wave); loads and stores are nontemporal, the policy
+// that wins on a batch that is not in the Infinity Cache.
 //
 // GF(2^8) multiply-accumulate on 4 packed bytes per dword uses Horner's rule
 // over the coefficient bits (bit 7 first):
@@ -20,9 +23,12 @@
 //            y << 8)
 //     xt   = ((y & 0x7f7f7f7f) << 1) ^ (mask & 0x1d1d1d1d)
 //
-//  * k_encode_c<D,P>: coefficients are compile-time (gf::Code<D,P>), so the
-//    XOR network is fixed at compile time -- used for the (10,3) headline and
-//    the (32,8) jumbo geometry.
+//  * k_encode_c<D,P> / k_encode_g<D,P>: coefficients are compile-time
+//    (gf::Code<D,P>), so the XOR network is fixed at compile time -- the (10,3)
+//    headline and the (32,8) jumbo geometry (k_encode_g in production).
+//  * k_apply_p<DMAX,MODE>: runtime coefficients through split v_perm_b32
+//    tables (the headline reconstruct), k_apply_q its streaming form for wide
+//    codes.
 //  * k_apply<DMAX,MODE>: coefficients come from a *descriptor* (input rows,
 //    output rows, e x d coefficient matrix).  MODE 0: one descriptor for all
 //    groups (generic encode); MODE 1: descriptor table indexed by the group's
