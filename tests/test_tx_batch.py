@@ -159,3 +159,47 @@ def test_tx_lossy_rx_reconstruct_round_trip(gpu):
             want = np.zeros(S, np.uint8)
             want[:len(b) - 6] = np.frombuffer(b[6:], np.uint8)
             assert np.array_equal(got[k, g, :S], want), f"group {g} row {k}"
+
+
+@pytest.mark.gpu
+def test_tx_rx_round_trip_full_size(gpu):
+    """BASELINE size (65,536 groups of (10+3), 1476-B packets), all on the
+    device: TX assemble -> lose 0..3 packets per group -> shuffle -> RX
+    assemble -> data-only Reconstruct.  Size-independent property: every data
+    payload comes back bit for bit (zero-padded past its length), and every
+    group is recoverable."""
+    d, p, n, S, pitch, slot, G = 10, 3, 13, 1470, 1472, 1488, 65536
+    dev = "cuda"
+    gen = torch.Generator(device=dev).manual_seed(21)
+    enc = fec.New(d, p)
+    pk = torch.randint(0, 256, (G * d, slot), dtype=torch.uint8, device=dev, generator=gen)
+    lens = torch.randint(7, 1477, (G * d,), dtype=torch.int16, device=dev, generator=gen)
+    lens[torch.rand(G * d, device=dev, generator=gen) < 0.5] = 1476
+    wire = torch.empty((G * n, slot), dtype=torch.uint8, device=dev)
+    wl = torch.empty(G * n, dtype=torch.int16, device=dev)
+    pad = torch.frombuffer(bytearray(fec.rc4_keystream(KEY, slot)), dtype=torch.uint8).to(dev)
+    st = torch.full((G,), -1, dtype=torch.int8, device=dev)
+    enc.tx_assemble(pk, lens, wire, wl, pad=pad, status=st)
+    assert bool((st == 0).all())
+    # lose e ~ U[0, 3] distinct packets per group: rank random keys within each group
+    e = torch.randint(0, p + 1, (G, 1), device=dev, generator=gen)
+    rank = torch.rand((G, n), device=dev, generator=gen).argsort(dim=1).argsort(dim=1)
+    keep = (rank >= e).reshape(-1).nonzero().squeeze(1)
+    keep = keep[torch.randperm(keep.numel(), device=dev, generator=gen)]
+    rx, rl = wire[keep].contiguous(), wl[keep].contiguous()
+    del wire
+    sh = torch.zeros((n, G, pitch), dtype=torch.uint8, device=dev)
+    present = torch.zeros(G, dtype=torch.int64, device=dev)
+    stats = torch.zeros(4, dtype=torch.int32, device=dev)
+    enc.rx_assemble(rx, rl, sh, present, shard_size=S, pad=pad, stats=stats)
+    assert stats.tolist() == [keep.numel(), 0, 0, 0]
+    status = torch.full((G,), -1, dtype=torch.int8, device=dev)
+    enc.reconstruct_batch(sh, present, shard_size=S, data_only=True, status=status, shard_major=True)
+    assert bool((status == 0).all())
+    # expected rows: payload bytes [6, len) of each data packet, zero past it
+    col = torch.arange(S, device=dev)
+    for k in range(d):  # one data row at a time keeps the temporaries small
+        pkt = pk.view(G, d, slot)[:, k, 6:6 + S]
+        L = (lens.view(G, d)[:, k].to(torch.int64) - 6).unsqueeze(1)
+        want = torch.where(col.unsqueeze(0) < L, pkt, torch.zeros_like(pkt))
+        assert torch.equal(sh[k, :, :S], want), f"data row {k}"
