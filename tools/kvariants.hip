@@ -207,6 +207,41 @@ __global__ __launch_bounds__(256) void k_encode_gp(Batch a) {
   }
 }
 
+// Encode with CPT chunks per lane, wave-contiguous: lane l of wave w takes
+// chunks 64*CPT*w + 64*j + l (j < CPT), so each wave covers CPT KiB of every
+// row (A/B: does per-wave contiguity beyond 1 KiB help the cold pattern?).
+template <int CPT, int NT, int GR = 0>
+__global__ __launch_bounds__(256) void k_encode_cpt(Batch a) {
+  __shared__ u32x4 stage[GR ? 4 : 1][GR ? GR : 1][CPT][64];
+  const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) >> 6, lane = threadIdx.x & 63u;
+  const uint32_t w = threadIdx.x >> 6;
+  V4 x[CPT][10];
+  Loc l[CPT];
+  bool ok[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const uint32_t item = wave * 64u * CPT + 64u * j + lane;
+    ok[j] = item < a.items;
+    l[j] = locate(a, ok[j] ? item : 0u);
+    if (ok[j]) {
+#pragma unroll
+      for (int k = 0; k < GR; ++k) lds_dma16(l[j].gp + static_cast<uint64_t>(k) * a.rstride, &stage[w][k][j][0]);
+#pragma unroll
+      for (int k = GR; k < 10; ++k) x[j][k] = load16<NT>(l[j].gp + static_cast<uint64_t>(k) * a.rstride);
+    }
+  }
+  if constexpr (GR > 0) {
+    lds_dma_wait();
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+#pragma unroll
+      for (int k = 0; k < GR; ++k) x[j][k] = lds16(&stage[w][k][j][lane]);
+  }
+#pragma unroll
+  for (int j = 0; j < CPT; ++j)
+    if (ok[j]) cparity_store<10, 3, NT>(l[j].gp, a.rstride, l[j].nb, x[j], std::make_integer_sequence<int, 3>{});
+}
+
 // Cold-regime ceilings: write-only and copy streams over a whole batch buffer.
 template <int NTS>
 __global__ __launch_bounds__(256) void k_write_stream(Batch a, uint64_t n16) {
@@ -370,10 +405,28 @@ int main(int argc, char** argv) {
     addr(k_encode_g<10, 3, 2, 10>, enc_bytes, "COLD enc lds-dma 10, nt stores");
     addr(k_encode_c<10, 3, 1>, enc_bytes, "COLD enc nt1");
     addr(k_encode_c<10, 3, 3>, enc_bytes, "COLD enc nt3");
+    {
+      const uint32_t g2 = (pl.items + 511) / 512, g4 = (pl.items + 1023) / 1024;
+      vars.push_back({"COLD enc nt3, 2 chunks per lane (2 KiB per wave per row)", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_cpt<2, 3>), dim3(g2), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      const uint32_t g3 = (pl.items + 767) / 768;
+      vars.push_back({"COLD enc nt3, 3 chunks per lane", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_cpt<3, 3>), dim3(g3), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD enc nt3, 2 chunks per lane, 4 rows by LDS-DMA", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_cpt<2, 3, 4>), dim3(g2), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD enc nt3, 2 chunks per lane, 2 rows by LDS-DMA", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_cpt<2, 3, 2>), dim3(g2), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD enc nt1, 2 chunks per lane", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_cpt<2, 1>), dim3(g2), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+    }
     addr(k_encode_c<10, 3, 0>, enc_bytes, "COLD enc nt0");
     addr(k_apply_p<10, 1, 1>, dec_bytes, "COLD dec perm nt1");
     addr(k_apply_p<10, 1, 3>, dec_bytes, "COLD dec perm nt3 (production)");
     addr(k_apply_p<10, 1, 3, 0>, dec_bytes, "COLD dec perm nt3 TSEL0 (probe: no per-lane pick, B lanes wrong)");
+    vars.push_back({"COLD pair enc nt3 2-chunk + dec nt3 reg", enc_bytes + dec_bytes, [=]() {
+      const Batch& b = rot[(*cnt)++ & 3];
+      hipLaunchKernelGGL((k_encode_cpt<2, 3>), dim3((pl.items + 511) / 512), dim3(256), 0, 0, b);
+      hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3((pl.items + 255) / 256), dim3(256), 0, 0, b); }, {}});
     addr(k_apply_p<10, 1, 3, 1, 1, 3>, dec_bytes, "COLD dec perm nt3 emax3");
     addr(k_apply_p<10, 1, 3, 1, 1, 4, false>, dec_bytes, "COLD dec perm nt3 unpaired");
     addr(k_apply_p<10, 1, 0>, dec_bytes, "COLD dec perm nt0");
@@ -417,6 +470,10 @@ int main(int argc, char** argv) {
   // holds the row-stride sweep (+-2%, kept at G * pitch)
   add(k_encode_g<10, 3, 0>, pl, enc_bytes, "enc planar lds-dma nt");
   add(k_encode_g<10, 3, 0, 8>, pl, enc_bytes, "enc planar lds-dma nt 8 rows + 2 reg");
+  add(k_encode_g<10, 3, 2, 8>, pl, enc_bytes, "enc planar lds-dma nt 8 rows + 2 reg, nt stores (production)");
+  vars.push_back({"enc planar nt3, 2 chunks per lane", enc_bytes, [=]() {
+    hipLaunchKernelGGL((k_encode_cpt<2, 3>), dim3((pl.items + 511) / 512), dim3(256), 0, 0, pl); }, {}});
+  add(k_apply_p<10, 1, 3>, pl, dec_bytes, "dec planar perm nt3 (production)");
   add(k_encode_g<10, 3, 0, 9>, pl, enc_bytes, "enc planar lds-dma nt 9 rows + 1 reg");
   add(k_encode_g<10, 3, 0, 7>, pl, enc_bytes, "enc planar lds-dma nt 7 rows + 3 reg");
   {
@@ -459,6 +516,15 @@ int main(int argc, char** argv) {
     };
     run_cmp("k_encode_g == k_encode_c", k_encode_c<10, 3, 1>, k_encode_g<10, 3, 0>);
     run_cmp("k_encode_g<8> == k_encode_c", k_encode_c<10, 3, 1>, k_encode_g<10, 3, 0, 8>);
+    {
+      CK(hipMemcpy(buf, hc.data(), hc.size(), hipMemcpyHostToDevice));
+      hipLaunchKernelGGL((k_encode_c<10, 3, 1>), dim3(grid), dim3(256), 0, 0, pl);
+      CK(hipMemcpy(h1.data(), buf, h1.size(), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(buf, hc.data(), hc.size(), hipMemcpyHostToDevice));
+      hipLaunchKernelGGL((k_encode_cpt<2, 3>), dim3((pl.items + 511) / 512), dim3(256), 0, 0, pl);
+      CK(hipMemcpy(h2.data(), buf, h2.size(), hipMemcpyDeviceToHost));
+      printf("{\"check\":\"k_encode_cpt<2> == k_encode_c\",\"equal\":%s}\n", h1 == h2 ? "true" : "false");
+    }
     run_cmp("k_apply_p lds-dma asm-collect == k_apply_p", k_apply_p<10, 1, 1>, k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 10>);
     run_cmp("k_apply_p lds-dma 8 == k_apply_p", k_apply_p<10, 1, 1>, k_apply_p<10, 1, 1, 1, 1, 4, true, 0, 8>);
     CK(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
