@@ -362,10 +362,9 @@ __device__ __forceinline__ void p_accum(V4* acc, const V4* x, const Batch& a, co
 template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1, int EMAX = 4, bool PAIR = true, int SWZ = 0,
           int GLR = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_p(Batch a) {
-  // GLR > 0 (A/B only): survivors 0..GLR-1 by LDS-DMA nt.  Alone on a cold
-  // batch it beats register loads (197 vs 204 us), but the encode -> reconstruct
-  // step is 1.5-2.5% slower with it (390 vs 385 us), and in a warm loop it ties
-  // them (187.3 vs 188.0 us): DESIGN.md §3.4.
+  // GLR > 0 (A/B only): survivors 0..GLR-1 by LDS-DMA nt.  It ties register
+  // loads on a cold batch (201.0 vs 201.0 us) and in a warm loop (187.3 vs
+  // 188.0 us): DESIGN.md §3.4.
   static_assert(GLR == 0 || (DMAX == 10 && (GLR == 8 || GLR == 10)), "LDS-DMA survivor staging: d = 10");
   __shared__ u32x4 stage[GLR ? 4 : 1][GLR ? GLR : 1][64];
   const uint32_t bid = block_id<SWZ>();
@@ -736,8 +735,9 @@ static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
 // Launch policy (tuned with tools/kvariants.hip on MI355X).
 // Store policy is chosen for the cold-HBM regime -- a batch whose lines are
 // not in the 256-MB Infinity Cache, as every fresh batch of packets is
-// (`kvariants 65536 25 cold`): nontemporal stores there take the (10,3) encode
-// from 227-244 to 195-207 us and the reconstruct from 224-236 to 204 us.  Re-running
+// (`kvariants 65536 21 cold`, each sample after a cache-evicting sweep):
+// nontemporal stores there take the (10,3) encode from 217.9 to 197.3 us and
+// the reconstruct from 228.4 to 201.0 us.  Re-running
 // ONE batch back to back instead (a warm loop) favours plain stores by 3-5%,
 // because the Infinity Cache then absorbs the rewritten parity lines.
 constexpr int kEncNT = 3;    // nontemporal loads and stores
@@ -745,7 +745,7 @@ constexpr int kEncLdsRows = 8;  // (10,3): rows 0-7 by LDS-DMA nt, 8-9 to regist
 constexpr int kEncJumboNT = 3;  // (32,8): NT loads and stores (578 vs 615 us, tools/jvariants.hip)
 constexpr int kEncJumboLdsRows = 16;  // (32,8): rows 0-15 by LDS-DMA nt (557 vs 571 us)
 constexpr int kApplyNT = 3;  // nontemporal loads and stores
-constexpr int kApplyPNT = 3; // k_apply_p: nontemporal loads and stores (cold: 204 vs 236 us)
+constexpr int kApplyPNT = 3; // k_apply_p: nontemporal loads and stores (cold: 201.0 vs 228.4 us)
 constexpr int kApplyQNT = 3; // k_apply_q (jumbo): NT loads and stores (548 vs 572 us)
 
 int apply_dmax(int d) {
