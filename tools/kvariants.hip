@@ -571,6 +571,7 @@ int main(int argc, char** argv) {
     run_cmp("k_encode_g == k_encode_c", k_encode_c<10, 3, 1>, k_encode_g<10, 3, 0>);
     run_cmp("k_encode_g<8> == k_encode_c", k_encode_c<10, 3, 1>, k_encode_g<10, 3, 0, 8>);
 
+
     {
       CK(hipMemcpy(buf, hc.data(), hc.size(), hipMemcpyHostToDevice));
       hipLaunchKernelGGL((k_encode_c<10, 3, 1>), dim3(grid), dim3(256), 0, 0, pl);
