@@ -347,3 +347,29 @@ def test_shard_major_layout(gpu, d, p, S, pitch):
     enc.reconstruct_batch(t, _masks_to_dev(masks), shard_size=S, status=st, shard_major=True)
     assert np.array_equal(st.cpu().numpy(), want_st)
     assert np.array_equal(t.cpu().numpy().transpose(1, 0, 2), want2)
+
+
+def test_empty_batches_are_noops(gpu):
+    """Zero groups / zero packets: every entry point returns OK and touches nothing
+    (upstream Encode/Reconstruct on an empty batch is never reached by ugo, but
+    a batch API must accept it)."""
+    enc = fec.New(10, 3)
+    for shard_major in (False, True):
+        shape = (13, 0, 1360) if shard_major else (0, 13, 1360)
+        t = torch.empty(shape, dtype=torch.uint8, device="cuda")
+        enc.encode_batch(t, shard_size=1350, shard_major=shard_major)
+        enc.reconstruct_batch(t, torch.empty(0, dtype=torch.int64, device="cuda"), shard_size=1350,
+                              shard_major=shard_major)
+    host = np.empty((0, 13, 1360), np.uint8)
+    enc.encode_host(host, 1350)
+    assert enc.reconstruct_host(host, np.empty(0, np.uint64), 1350) == 0
+    sh = torch.zeros((13, 4, 1472), dtype=torch.uint8, device="cuda")
+    present = torch.zeros(4, dtype=torch.int64, device="cuda")
+    enc.rx_assemble(torch.empty((0, 1488), dtype=torch.uint8, device="cuda"),
+                    torch.empty(0, dtype=torch.int16, device="cuda"), sh, present, shard_size=1470)
+    assert not present.any() and not sh.any()
+    enc.tx_assemble(torch.empty((0, 1488), dtype=torch.uint8, device="cuda"),
+                    torch.empty(0, dtype=torch.int16, device="cuda"),
+                    torch.empty((0, 1488), dtype=torch.uint8, device="cuda"),
+                    torch.empty(0, dtype=torch.int16, device="cuda"))
+    torch.cuda.synchronize()

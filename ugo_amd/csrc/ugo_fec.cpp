@@ -200,6 +200,7 @@ int check_batch(const ugo_fec* c, const void* shards, size_t groups, size_t S, c
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;  // checkShards: all shards empty
   if (S > 0xffffffffu) return UGO_FEC_ERR_INVALID_ARG;
+  if (groups == 0) return UGO_FEC_OK;  // an empty batch has no layout to check
   if (c->n > 1 && L.rstride < S) return UGO_FEC_ERR_INVALID_ARG;   // rows would overlap
   if (groups > 1 && L.gstride < S) return UGO_FEC_ERR_INVALID_ARG;
   if (groups && !shards) return UGO_FEC_ERR_INVALID_ARG;
@@ -583,6 +584,7 @@ int ugo_fec_encode_strided(ugo_fec* c, uint8_t* shards, size_t groups, size_t S,
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (groups == 0) return UGO_FEC_OK;  // nothing is touched (an empty tensor's pointer may be anything)
   if (!device_view(shards)) return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
   return encode_dev(c, shards, groups, S, L, static_cast<hipStream_t>(stream));
@@ -602,6 +604,7 @@ int ugo_fec_reconstruct_strided(ugo_fec* c, uint8_t* shards, const uint64_t* pre
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (groups == 0) return UGO_FEC_OK;
   if (!device_view(shards) || !device_view(present) || !device_view(status)) return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
   return reconstruct_dev(c, shards, present, groups, S, L, flags, status, static_cast<hipStream_t>(stream));
