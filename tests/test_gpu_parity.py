@@ -150,7 +150,8 @@ def test_reconstruct_inconsistent_inputs(gpu, table_max, monkeypatch):
 @pytest.mark.parametrize("d,p,S,pitch", [(4, 2, 100, 112), (5, 5, 64, 64), (12, 4, 333, 336),
                                          (20, 4, 200, 208), (32, 8, 9000, 9008), (3, 1, 50, 50),
                                          (40, 6, 70, 80), (1, 1, 7, 16), (7, 0, 32, 32),
-                                         (5, 3, 1500, 1504), (8, 4, 4096, 4096), (16, 4, 1030, 1040)])
+                                         (5, 3, 1500, 1504), (8, 4, 4096, 4096), (16, 4, 1030, 1040),
+                                         (56, 8, 256, 256)])  # d+p = 64: the widest presence mask
 def test_generic_geometries(gpu, d, p, S, pitch):
     n = d + p
     G = 300
@@ -373,3 +374,20 @@ def test_empty_batches_are_noops(gpu):
                     torch.empty((0, 1488), dtype=torch.uint8, device="cuda"),
                     torch.empty(0, dtype=torch.int16, device="cuda"))
     torch.cuda.synchronize()
+
+
+def test_more_than_64_shards_encode_only(gpu):
+    """Upstream allows 256 shards; presence masks are 64-bit, so a batch
+    reconstruct with d+p > 64 is refused (documented in include/ugo_fec.h)
+    while encode works."""
+    d, p, S, G = 100, 20, 64, 8
+    n = d + p
+    host = _rand(G, n, S, 7).numpy()
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    enc = fec.New(d, p)
+    t = _dev(host)
+    enc.encode_batch(t, shard_size=S)
+    assert np.array_equal(t.cpu().numpy(), want)
+    with pytest.raises(fec.ErrInvalidArg):
+        enc.reconstruct_batch(t, torch.full((G,), -1, dtype=torch.int64, device="cuda"), shard_size=S)
