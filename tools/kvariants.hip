@@ -288,6 +288,30 @@ __global__ __launch_bounds__(256) void k_flush_read(const u32x4* __restrict__ a,
   if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9e3779b9u) out[0] = v.x;
 }
 
+// Layout probe (A/B only): compute-free encode pattern over a TILED planar
+// layout [G/T][13][T][pitch] -- each tile of T groups is planar, tiles follow
+// each other -- instead of one planar [13][G][pitch].
+template <int T>
+__global__ __launch_bounds__(256) void k_pattern_tiled(Batch a) {
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t g = item / a.chunks, c = item - g * a.chunks;
+  const uint64_t tile = g / T, gi = g % T;
+  const uint64_t rs = static_cast<uint64_t>(T) * a.gstride;  // row stride inside a tile
+  uint8_t* gp = a.base + tile * 13ull * rs + gi * a.gstride + c * 16ull;
+  V4 x[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) x[k] = load16<1>(gp + k * rs);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    V4 y = x[i];
+#pragma unroll
+    for (int k = 3; k < 10; ++k)
+      if ((k + i) & 1) xor4(y, x[k]);
+    store16<2>(gp + (10 + i) * rs, y, 16);
+  }
+}
+
 // Cold-regime ceilings: write-only and copy streams over a whole batch buffer.
 template <int NTS>
 __global__ __launch_bounds__(256) void k_write_stream(Batch a, uint64_t n16) {
@@ -447,6 +471,10 @@ int main(int argc, char** argv) {
     };
     addr(k_encode_g<10, 3, 0, 8>, enc_bytes, "COLD enc lds-dma 8");
     addr(k_encode_g<10, 3, 2, 8>, enc_bytes, "COLD enc lds-dma 8, nt stores (production)");
+    addr(k_pattern_tiled<512>, enc_bytes, "COLD enc PATTERN tiled planar T=512");
+    addr(k_pattern_tiled<4096>, enc_bytes, "COLD enc PATTERN tiled planar T=4096");
+    addr(k_pattern_tiled<16384>, enc_bytes, "COLD enc PATTERN tiled planar T=16384");
+    addr(k_pattern_tiled<65536>, enc_bytes, "COLD enc PATTERN tiled planar T=65536 (= planar)");
     addr(k_encode_pol<0>, enc_bytes, "COLD enc POL store (plain)");
     addr(k_encode_pol<1>, enc_bytes, "COLD enc POL store nt");
     addr(k_encode_pol<2>, enc_bytes, "COLD enc POL store sc1");
