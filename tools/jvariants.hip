@@ -116,6 +116,18 @@ int main(int argc, char** argv) {
     vars[4].go();  // reconstruct of a consistent batch rewrites erased rows with the same bytes
     CK(hipMemcpy(h3.data(), buf, h.size(), hipMemcpyDeviceToHost));
     printf("{\"check\":\"reconstruct of codewords is idempotent\",\"equal\":%s}\n", same_rows(h3, h1) ? "true" : "false");
+    // every decode variant recovers garbage-filled erased rows to the codewords
+    std::vector<uint8_t> hc = h1;
+    for (uint64_t g = 0; g < G; ++g)
+      for (int r = 0; r < n; ++r)
+        if (!((hm[g] >> r) & 1)) memset(&hc[r * a.rstride + g * pitch], 0xA5, S);
+    for (auto& v : vars) {
+      if (v.name.rfind("dec", 0) != 0) continue;
+      CK(hipMemcpy(buf, hc.data(), hc.size(), hipMemcpyHostToDevice));
+      v.go();
+      CK(hipMemcpy(h3.data(), buf, h.size(), hipMemcpyDeviceToHost));
+      printf("{\"check\":\"%s recovers erased rows\",\"equal\":%s}\n", v.name.c_str(), same_rows(h3, h1) ? "true" : "false");
+    }
     fflush(stdout);
   }
   hipEvent_t e0, e1;
