@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -546,6 +547,17 @@ int main(int argc, char** argv) {
     pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>, "COLD pair enc lds-dma 8 + dec lds-dma");
     pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 3>, "COLD pair production (enc lds-dma 8 + dec nt3 reg, nt stores both)");
     pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 1>, "COLD pair nt stores encode");
+    {  // PROBE (timing only; writes the pitch padding): S = pitch, so every row's
+       // tail chunk is a full 16-B store and no 128-B line is partially written
+       // by a group's row end.  Same chunks, items and grid as production.
+      std::vector<Batch> rotf(rot);
+      for (auto& b : rotf) b.S = static_cast<uint32_t>(pitch);
+      const uint32_t grid = (pl.items + 255) / 256;
+      vars.push_back({"COLD enc production, PROBE full tail chunks (S=pitch)", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8>), dim3(grid), dim3(256), 0, 0, rotf[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD dec production, PROBE full tail chunks (S=pitch)", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotf[(*cnt)++ & 3]); }, {}});
+    }
   }
   if (!cold) {
   // LDS-DMA (global_load_lds_dwordx4 nt) row loads; profiles/r1/kvariants_xcd_rstride.jsonl
@@ -637,6 +649,19 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(h2.data(), buf, h.size(), hipMemcpyDeviceToHost));
     printf("{\"check\":\"k_apply_p<2> == k_apply_w\",\"equal\":%s}\n", h1 == h2 ? "true" : "false");
     fflush(stdout);
+  }
+  if (const char* f = getenv("KVAR_FILTER")) {  // '|'-separated substrings; keep matching variants
+    std::vector<Var> kept;
+    std::string fs(f);
+    for (auto& v : vars) {
+      size_t a = 0;
+      while (a <= fs.size()) {
+        const size_t b = std::min(fs.find('|', a), fs.size());
+        if (b > a && v.name.find(fs.substr(a, b - a)) != std::string::npos) { kept.push_back(v); break; }
+        a = b + 1;
+      }
+    }
+    vars.swap(kept);
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
