@@ -25,7 +25,11 @@ using namespace ugo::kern;
     }                                                                              \
   } while (0)
 
-static void build_table(int d, int p, uint32_t dpad, uint32_t epad, uint32_t stride, std::vector<uint8_t>& tab) {
+// canon: survivor slots aligned to row indices -- present data row r in slot r,
+// the parity survivors in the erased data rows' slots (in order) -- so two
+// groups sharing a wave load the same row in most slots.
+static void build_table(int d, int p, uint32_t dpad, uint32_t epad, uint32_t stride, std::vector<uint8_t>& tab,
+                        bool canon = false) {
   const int n = d + p;
   std::vector<uint8_t> M(n * d), scratch(n * d + 3 * d * d);
   gf::build_matrix(d, p, M.data(), scratch.data());
@@ -45,7 +49,15 @@ static void build_table(int d, int p, uint32_t dpad, uint32_t epad, uint32_t str
     int ed = 0;
     for (int r : outr) ed += r < d;
     out[0] = outr.size(); out[1] = ed;
-    for (int i = 0; i < d; ++i) out[4 + i] = surv[i];
+    std::vector<int> slot(d);
+    for (int k = 0; k < d; ++k) slot[k] = k;
+    if (canon) {
+      int nx = 0;
+      std::vector<int> freeslots;
+      for (int r = 0; r < d; ++r) if (!((m >> r) & 1)) freeslots.push_back(r);
+      for (int k = 0; k < d; ++k) slot[k] = surv[k] < d ? surv[k] : freeslots[nx++];
+    }
+    for (int i = 0; i < d; ++i) out[4 + slot[i]] = surv[i];
     for (size_t i = 0; i < outr.size(); ++i) out[4 + dpad + i] = outr[i];
     uint8_t* coef = out + 4 + dpad + epad;
     for (size_t i = 0; i < outr.size(); ++i)
@@ -54,7 +66,7 @@ static void build_table(int d, int p, uint32_t dpad, uint32_t epad, uint32_t str
         uint8_t v = 0;
         if (r < d) v = inv[r * d + k];
         else for (int j = 0; j < d; ++j) v ^= gf::mul(M[r * d + j], inv[j * d + k]);
-        coef[i * dpad + k] = v;
+        coef[i * dpad + slot[k]] = v;
       }
   }
 }
@@ -358,6 +370,11 @@ int main(int argc, char** argv) {
   uint8_t* dtab;
   CK(hipMalloc(&dtab, tab.size()));
   CK(hipMemcpy(dtab, tab.data(), tab.size(), hipMemcpyHostToDevice));
+  std::vector<uint8_t> tabc;
+  build_table(d, p, dpad, epad, stride, tabc, true);
+  uint8_t* dtabc;
+  CK(hipMalloc(&dtabc, tabc.size()));
+  CK(hipMemcpy(dtabc, tabc.data(), tabc.size(), hipMemcpyHostToDevice));
 
   std::vector<uint8_t> hmul(256 * 32);
   ugo::gf::perm_tables(hmul.data());
@@ -547,6 +564,41 @@ int main(int argc, char** argv) {
     pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>, "COLD pair enc lds-dma 8 + dec lds-dma");
     pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 3>, "COLD pair production (enc lds-dma 8 + dec nt3 reg, nt stores both)");
     pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 1>, "COLD pair nt stores encode");
+    {  // canonical survivor slots (same kernels, descriptor table with slot r = row r)
+      std::vector<Batch> rotc(rot);
+      for (auto& b : rotc) b.desc = dtabc;
+      const uint32_t grid = (pl.items + 255) / 256;
+      vars.push_back({"COLD dec perm nt3 (production kernel), CANON slots", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotc[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD dec MEMORY PATTERN ONLY nt3, CANON slots", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_pattern_rec<3>), dim3(grid), dim3(256), 0, 0, rotc[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD dec perm lds-dma, nt stores, CANON slots", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>), dim3(grid), dim3(256), 0, 0, rotc[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD pair production, CANON slots", enc_bytes + dec_bytes, [=]() {
+        const Batch& b = rotc[(*cnt)++ & 3];
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8>), dim3(grid), dim3(256), 0, 0, b);
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, b); }, {}});
+      // bit-exact check: canonical-slot table == first-d table, erased rows clobbered before each run
+      std::vector<uint8_t> h1(G * n * pitch), h2(G * n * pitch);
+      auto clob_run = [&](const Batch& b, std::vector<uint8_t>& out) {
+        CK(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL((k_encode_c<10, 3, 1>), dim3(grid), dim3(256), 0, 0, pl);
+        for (uint64_t g = 0; g < G; g += 97)  // a sample of groups gets garbage in its erased rows
+          for (int r = 0; r < n; ++r)
+            if (!(hm[g] >> r & 1)) CK(hipMemset(buf + r * pl.rstride + g * pl.gstride, 0xee, S));
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, b);
+        CK(hipMemcpy(out.data(), buf, out.size(), hipMemcpyDeviceToHost));
+      };
+      Batch bc = pl; bc.desc = dtabc;
+      clob_run(pl, h1);
+      clob_run(bc, h2);
+      CK(hipMemcpy(buf, h.data(), h.size(), hipMemcpyHostToDevice));
+      size_t ndiff = 0;
+      for (size_t i = 0; i < h1.size(); ++i) ndiff += h1[i] != h2[i];
+      printf("{\"check\":\"k_apply_p CANON slots == first-d slots\",\"equal\":%s,\"diff_bytes\":%zu}\n",
+             ndiff ? "false" : "true", ndiff);
+      fflush(stdout);
+    }
     {  // PROBE (timing only; writes the pitch padding): S = pitch, so every row's
        // tail chunk is a full 16-B store and no 128-B line is partially written
        // by a group's row end.  Same chunks, items and grid as production.
