@@ -62,6 +62,10 @@ def parse():
                          "cache then absorbs part of the rewritten parity (DESIGN.md §4)")
     ap.add_argument("--layout", choices=["planar", "interleaved"], default="planar",
                     help="planar = shard-major [d+p][G][pitch] batch; interleaved = [G][d+p][pitch]")
+    ap.add_argument("--decode", choices=["inplace", "into"], default="into",
+                    help="inplace = ugo_fec_reconstruct_strided (erased rows rebuilt inside the batch); into = "
+                         "ugo_fec_reconstruct_into (erased rows written to a separate [p][G][pitch] output batch, "
+                         "the fresh buffers klauspost's Reconstruct gives ugo's nil shards)")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16,
@@ -152,14 +156,21 @@ def main():
     batches = [torch.randint(0, 256, shape, dtype=torch.uint8, device=dev, generator=gen) for _ in range(nb)]
     shards = batches[0]
     masks, erased = make_masks(G, n, e, args.seed + 1000 + rank, dev)
+    into = args.decode == "into"
+    # one output batch per input batch, so every step's outputs are cold too
+    outs = [torch.zeros((p, G, pitch), dtype=torch.uint8, device=dev) for _ in range(nb)] if into else None
     stream = torch.cuda.current_stream()
     cur = [0]
 
     def step():
-        b = batches[cur[0] % nb]
+        i = cur[0] % nb
+        b = batches[i]
         cur[0] += 1
         enc.encode_batch(b, shard_size=S, stream=stream, shard_major=planar)
-        enc.reconstruct_batch(b, masks, shard_size=S, stream=stream, shard_major=planar)
+        if into:
+            enc.reconstruct_into(b, masks, outs[i], shard_size=S, stream=stream, shard_major=planar)
+        else:
+            enc.reconstruct_batch(b, masks, shard_size=S, stream=stream, shard_major=planar)
 
     for _ in range(args.warmup):
         step()
@@ -218,11 +229,23 @@ def main():
         gi = torch.arange(G, device=dev)
         for j in range(e):
             view[gi, erased[:, j].to(dev)] = 0
-        enc.reconstruct_batch(shards, masks, shard_size=S, stream=stream, shard_major=planar)
-        ok_rt = bool(torch.equal(view[:, :, :S], ref[:, :, :S]))
+        if into:
+            o = torch.full((p, G, pitch), 0xA5, dtype=torch.uint8, device=dev)
+            enc.reconstruct_into(shards, masks, o, shard_size=S, stream=stream, shard_major=planar)
+            es = erased.sort(dim=1).values.to(dev)  # output j = j-th erased row, ascending
+            ok_rt = all(bool(torch.equal(o[j, :, :S], ref[gi, es[:, j], :S])) for j in range(e))
+            for j in range(e):  # the input keeps its erased (zeroed) rows
+                ok_rt = ok_rt and not bool(view[gi, es[:, j], :S].any())
+            del o
+        else:
+            enc.reconstruct_batch(shards, masks, shard_size=S, stream=stream, shard_major=planar)
+            ok_rt = bool(torch.equal(view[:, :, :S], ref[:, :, :S]))
         par = ref[:, d:, :S].clone()
         view[:, d:, :] = 0
         enc.encode_batch(shards, shard_size=S, stream=stream, shard_major=planar)
+        if into:  # restore the erased data rows so the parity check sees the full data
+            view[:, :d, :] = ref[:, :d, :]
+            enc.encode_batch(shards, shard_size=S, stream=stream, shard_major=planar)
         ok_idem = bool(torch.equal(view[:, d:, :S], par))
         del ref, par
         verify = {"round_trip_full_size": ok_rt, "encode_idempotent": ok_idem}
@@ -247,7 +270,7 @@ def main():
         traffic = None
         try:
             tj = json.load(open(args.traffic_json))
-            key = f"{dom}:{d}+{p}x{S}/{pitch}:G{G}"
+            key = f"{dom}:{d}+{p}x{S}/{pitch}:G{G}" + (":into" if into and dom == "reconstruct" else "")
             traffic = tj.get(key)
         except Exception:
             pass
@@ -269,7 +292,7 @@ def main():
                                    f"{G} groups/GPU", "groups_per_gpu": G, "total_groups": total_groups,
                        "data_shards": d, "parity_shards": p, "shard_size": S, "pitch": pitch, "erasures": e,
                        "layout": "shard-major [d+p][G][pitch]" if planar else "group-major [G][d+p][pitch]",
-                       "batches_per_gpu": nb,
+                       "batches_per_gpu": nb, "decode": args.decode,
                        "parallelism": f"dp{world} (independent packet groups, no collective)"},
             "pct_hbm_roofline": round(step_bytes_all / world * args.steps / elapsed / (HBM_PEAK_GBS * 1e9), 4),
             "roofline": roof, "kernels": kern, "verify": verify,

@@ -105,6 +105,22 @@ int ugo_fec_reconstruct_strided(ugo_fec* ctx, uint8_t* shards, const uint64_t* p
                                 size_t shard_size, size_t row_stride, size_t group_stride,
                                 unsigned flags, int8_t* status, void* stream);
 
+/* Reconstruct into a separate output batch (replaces the same
+ * reedsolomon.Encoder.Reconstruct, ugo/fec.go:202, in the form ugo calls it:
+ * erased shards are nil, ugo/fec.go:166-176, and klauspost hands them fresh
+ * buffers).  `shards` is only read.  Output i of group g -- the i-th erased row
+ * in ascending row order, i.e. erased data rows first, then erased parity rows
+ * (DATA_ONLY: the data rows only) -- is written, shard_size bytes, to
+ *     out + g*out_group_stride + i*out_row_stride,   i < p.
+ * Output slots past a group's erasure count, and every slot of a group that
+ * fails (status as ugo_fec_reconstruct), are left untouched.  The rows the
+ * recovered data lands in are the ones ugo appends to `recovered`
+ * (ugo/fec.go:203-207).  Fast path: out 16-B aligned, strides % 16 == 0. */
+int ugo_fec_reconstruct_into(ugo_fec* ctx, const uint8_t* shards, const uint64_t* present, size_t groups,
+                             size_t shard_size, size_t row_stride, size_t group_stride, uint8_t* out,
+                             size_t out_row_stride, size_t out_group_stride, unsigned flags,
+                             int8_t* status, void* stream);
+
 /* ---- host-buffer batch (synchronous) ------------------------------------
  * Same contracts with HOST pointers: the engine stages through its own device
  * buffers, pipelining H2D -> kernel -> D2H over chunks on internal streams.

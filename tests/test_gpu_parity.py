@@ -391,3 +391,72 @@ def test_more_than_64_shards_encode_only(gpu):
     assert np.array_equal(t.cpu().numpy(), want)
     with pytest.raises(fec.ErrInvalidArg):
         enc.reconstruct_batch(t, torch.full((G,), -1, dtype=torch.int64, device="cuda"), shard_size=S)
+
+
+@pytest.mark.parametrize("d,p,S,pitch,opitch,shard_major,table_max",
+                         [(10, 3, 1350, 1360, 1360, True, "16"),    # headline kernel (k_apply_p)
+                          (10, 3, 1350, 1360, 1360, False, "0"),    # k_prepare + per-group descriptors
+                          (32, 8, 9000, 9008, 9008, True, "16"),    # jumbo streaming kernel (k_apply_q)
+                          (10, 3, 1350, 1353, 1355, False, "16"),   # unaligned: byte kernel
+                          (6, 2, 77, 80, 96, True, "16"),           # rows < 64 chunks: k_apply
+                          (12, 4, 1030, 1040, 1040, False, "16"),   # p = 4
+                          (20, 9, 1100, 1104, 1104, True, "16")])   # p > 8 (k_prepare + k_apply)
+def test_reconstruct_into_vs_oracle(gpu, d, p, S, pitch, opitch, shard_major, table_max, monkeypatch):
+    """ugo_fec_reconstruct_into: shards only read; output i = i-th erased row
+    (ascending), bit-exact vs the oracle's in-place result; slots past e and
+    failing groups untouched; statuses as the in-place form."""
+    monkeypatch.setenv("UGO_FEC_TABLE_MAX_SHARDS", table_max)
+    n, G = d + p, 700
+    host = _rand(G, n, pitch, 77 + d + p).numpy()
+    rs_ref.c_encode(d, p, host, S=S)
+    rng = np.random.default_rng(d * 7 + p)
+    masks = np.zeros(G, np.uint64)
+    for g in range(G):
+        e = int(rng.integers(0, p + 2))  # includes e = 0 and too-few-shards groups
+        m = (1 << n) - 1
+        for r in rng.choice(n, size=min(e, n), replace=False):
+            m &= ~(1 << int(r))
+        masks[g] = m
+    inp = _erase(host, masks, n)
+    inp[:, :, S:] = 0x3C  # padding stays what it was in the input
+    enc = fec.New(d, p)
+    for data_only in (False, True):
+        want = inp.copy()
+        rc, want_st = rs_ref.c_reconstruct(d, p, want, masks, S=S, data_only=data_only)
+        exp = np.full((G, p, opitch), 0xA5, dtype=np.uint8)
+        for g in range(G):
+            if want_st[g] != 0:
+                continue
+            er = [r for r in range(n) if not (int(masks[g]) >> r) & 1 and (r < d or not data_only)]
+            for i, r in enumerate(er):
+                exp[g, i, :S] = want[g, r, :S]
+        t_in = _dev(np.ascontiguousarray(inp.transpose(1, 0, 2)) if shard_major else inp)
+        before = t_in.clone()
+        out = torch.full((p, G, opitch) if shard_major else (G, p, opitch), 0xA5, dtype=torch.uint8, device="cuda")
+        st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+        enc.reconstruct_into(t_in, _masks_to_dev(masks), out, shard_size=S, data_only=data_only, status=st,
+                             shard_major=shard_major, out_shard_major=shard_major)
+        torch.cuda.synchronize()
+        assert torch.equal(t_in, before), "reconstruct_into wrote its input"
+        assert np.array_equal(st.cpu().numpy(), want_st)
+        got = out.cpu().numpy()
+        if shard_major:
+            got = got.transpose(1, 0, 2)
+        assert np.array_equal(got, exp), (d, p, S, data_only)
+
+
+def test_reconstruct_into_rejects_bad_outputs(gpu):
+    d, p, S = 10, 3, 1350
+    enc = fec.New(d, p)
+    lib = fec.load_library()
+    t = torch.zeros((4, d + p, 1360), dtype=torch.uint8, device="cuda")
+    m = _masks_to_dev(np.full(4, (1 << (d + p)) - 2, np.uint64))
+    o = torch.zeros((4, p, 1360), dtype=torch.uint8, device="cuda")
+    pitch = 1360
+    args = (enc._h, t.data_ptr(), m.data_ptr(), 4, S, pitch, (d + p) * pitch)
+    assert lib.ugo_fec_reconstruct_into(*args, None, pitch, p * pitch, 0, None, None) == fec.ErrInvalidArg.code
+    assert lib.ugo_fec_reconstruct_into(*args, o.data_ptr(), S - 1, p * pitch, 0, None, None) == fec.ErrInvalidArg.code
+    assert lib.ugo_fec_reconstruct_into(*args, o.data_ptr(), pitch, S - 1, 0, None, None) == fec.ErrInvalidArg.code
+    assert lib.ugo_fec_reconstruct_into(*args, o.data_ptr(), pitch, p * pitch, 0, None, None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(o[:, 0, :S], torch.zeros_like(o[:, 0, :S]))  # all-zero codeword: row 0 rebuilt as zeros

@@ -74,7 +74,9 @@ static void build_table(int d, int p, uint32_t dpad, uint32_t epad, uint32_t str
 // Memory-pattern ceiling of the reconstruct: the wave-scalar descriptor
 // prologue, survivor loads and erased-row stores of k_apply_p, with the GF
 // arithmetic replaced by a plain XOR of the survivors (wrong values, same bytes).
-template <int NT, bool GL = false>
+// OOP (probe): erased row i goes to output slot i of a separate planar batch
+// [4][G][pitch] at a.status (reused as a byte pointer), not back in place.
+template <int NT, bool GL = false, bool OOP = false>
 __global__ __launch_bounds__(256) void k_pattern_rec(Batch a) {
   __shared__ u32x4 stage[GL ? 4 : 1][GL ? 10 : 1][64];
   const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
@@ -120,7 +122,11 @@ __global__ __launch_bounds__(256) void k_pattern_rec(Batch a) {
     if (i >= static_cast<int>(e)) continue;
     const uint32_t r = (orows >> (8 * i)) & 0xffu;
     y.v[0] += i;
-    store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, y, nb);
+    if constexpr (OOP)
+      store16<NT>(reinterpret_cast<uint8_t*>(a.status) + static_cast<uint64_t>(i) * a.rstride +
+                      (a.g0 + gl) * a.gstride + static_cast<uint64_t>(c) * 16u, y, nb);
+    else
+      store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, y, nb);
   }
 }
 
@@ -564,6 +570,20 @@ int main(int argc, char** argv) {
     pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>, "COLD pair enc lds-dma 8 + dec lds-dma");
     pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 3>, "COLD pair production (enc lds-dma 8 + dec nt3 reg, nt stores both)");
     pairr(k_encode_g<10, 3, 2, 8>, k_apply_p<10, 1, 1>, "COLD pair nt stores encode");
+    {  // out-of-place reconstruct pattern: erased rows to a separate [4][G][pitch] batch
+      std::vector<Batch> roto(rot);
+      for (auto& b : roto) {
+        uint8_t* ob;
+        CK(hipMalloc(&ob, 4 * G * pitch));
+        CK(hipMemset(ob, 0, 4 * G * pitch));
+        b.status = reinterpret_cast<int8_t*>(ob);
+      }
+      const uint32_t grid = (pl.items + 255) / 256;
+      vars.push_back({"COLD dec MEMORY PATTERN ONLY nt3, OUT-OF-PLACE outputs", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_pattern_rec<3, false, true>), dim3(grid), dim3(256), 0, 0, roto[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD dec MEMORY PATTERN ONLY lds-dma nt stores, OUT-OF-PLACE outputs", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_pattern_rec<3, true, true>), dim3(grid), dim3(256), 0, 0, roto[(*cnt)++ & 3]); }, {}});
+    }
     {  // canonical survivor slots (same kernels, descriptor table with slot r = row r)
       std::vector<Batch> rotc(rot);
       for (auto& b : rotc) b.desc = dtabc;

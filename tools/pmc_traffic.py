@@ -107,7 +107,8 @@ def main():
             if k in alg:
                 ent["algorithmic_bytes"] = alg[k]
                 ent["traffic_over_algorithmic"] = corr / alg[k]
-                traffic[f"{k}:{d}+{p}x{S}/{pitch}:G{G}"] = corr
+                into = ":into" if (k == "reconstruct" and cfg.get("decode") == "into") else ""
+                traffic[f"{k}:{d}+{p}x{S}/{pitch}:G{G}{into}"] = corr
         summary["kernels"][k] = ent
     json.dump(summary, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
     tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")

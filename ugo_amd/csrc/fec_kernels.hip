@@ -66,6 +66,17 @@ __device__ __forceinline__ Loc locate(const Batch& a, uint32_t item) {
   return Loc{a.base + (a.g0 + gl) * a.gstride + static_cast<uint64_t>(c) * 16u, a.S - c * 16u};
 }
 
+// Destination of reconstruct output i (erased row r) for the chunk at byte
+// offset `off` of group g: row r of the group itself (in place), or slot i of
+// the caller's output batch (a.out: klauspost's Reconstruct hands erased, nil
+// shards fresh buffers, ugo/fec.go:198-202).  a.out is a kernel argument, so
+// the choice is a scalar branch.
+__device__ __forceinline__ uint8_t* out_row(const Batch& a, uint8_t* gp, uint64_t g, uint32_t off, uint32_t r,
+                                            uint32_t i) {
+  return a.out ? a.out + g * a.ogstride + static_cast<uint64_t>(i) * a.orstride + off
+               : gp + static_cast<uint64_t>(r) * a.rstride;
+}
+
 template <int D, int NT>
 __device__ __forceinline__ void load_rows(V4* x, const uint8_t* gp, uint64_t rstride) {
 #pragma unroll
@@ -166,7 +177,7 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
 #pragma unroll
     for (int w = 0; w < NW; ++w) cw[w] = ld32(coef + i * a.dpad + 4 * w);
     const V4 y = horner_var<DMAX>(x, cw);
-    store16<NT>(gp + static_cast<uint64_t>(orow[i]) * a.rstride, y, nb);
+    store16<NT>(out_row(a, gp, g, c * 16u, orow[i], i), y, nb);
   }
 }
 
@@ -186,7 +197,8 @@ struct WItem {
   const uint8_t* dA;
   const uint8_t* dB;
   uint8_t* gp;
-  uint32_t nb, e, orows;
+  uint64_t g;
+  uint32_t c, nb, e, orows;
   bool inB, live;
   V4 x[DMAX];
 };
@@ -221,6 +233,8 @@ __device__ __forceinline__ void witem_issue(WItem<DMAX>& it, const Batch& a, uin
   if (st != 0 || it.e == 0) return;
   it.live = true;
   it.gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
+  it.g = g;
+  it.c = c;
   it.nb = a.S - c * 16u;
   it.orows = it.inB ? oB : oA;
 #pragma unroll
@@ -250,7 +264,7 @@ __device__ __forceinline__ void witem_finish(const WItem<DMAX>& it, const Batch&
     }
     const V4 y = horner_var<DMAX>(it.x, cw);
     const uint32_t r = (it.orows >> (8 * i)) & 0xffu;
-    store16<NT>(it.gp + static_cast<uint64_t>(r) * a.rstride, y, it.nb);
+    store16<NT>(out_row(a, it.gp, it.g, it.c * 16u, r, i), y, it.nb);
   }
 }
 
@@ -446,7 +460,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (int i = 0; i < EMAX; ++i) {
     if (i >= static_cast<int>(e)) continue;
     const uint32_t r = (orows >> (8 * i)) & 0xffu;
-    store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, acc[i], nb);
+    store16<NT>(out_row(a, gp, g, c * 16u, r, i), acc[i], nb);
   }
   if (wst) a.status[g] = 0;
 }
@@ -544,7 +558,7 @@ __global__ __launch_bounds__(256) void k_apply_q(Batch a) {
   for (int i = 0; i < EMAX; ++i) {
     if (i >= static_cast<int>(e)) continue;
     const uint32_t r = (orw[i >> 2] >> (8 * (i & 3))) & 0xffu;
-    store16<NT>(gp + static_cast<uint64_t>(r) * a.rstride, acc[i], nb);
+    store16<NT>(out_row(a, gp, g, c * 16u, r, i), acc[i], nb);
   }
   if (wst) a.status[g] = 0;
 }
@@ -587,7 +601,7 @@ __global__ __launch_bounds__(256) void k_apply_bytes(Batch a) {
       for (uint32_t j = 0; j < nb; ++j) x |= static_cast<uint32_t>(src[j]) << (8 * j);
       acc ^= gfmul_var(coef[i * a.dpad + k], x);
     }
-    uint8_t* dst = gp + static_cast<uint64_t>(orow[i]) * a.rstride;
+    uint8_t* dst = out_row(a, gp, g, c * 4u, orow[i], i);
     for (uint32_t j = 0; j < nb; ++j) dst[j] = static_cast<uint8_t>(acc >> (8 * j));
   }
 }

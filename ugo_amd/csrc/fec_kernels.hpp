@@ -29,6 +29,9 @@ struct Batch {
   uint32_t data_only;
   uint32_t pass;            // k_apply_w with CPT > 1: item distance between a thread's chunks
   const uint32_t* mult;     // gf::perm_tables (256 x 8 dwords, device) for k_apply_p
+  uint8_t* out;             // reconstruct: null = erased rows rebuilt in place; else output i
+  uint64_t ogstride;        //   (i-th erased row, ascending) of group g at out + g*ogstride + i*orstride
+  uint64_t orstride;
 };
 
 struct Prep {

@@ -181,6 +181,12 @@ bool fast_layout(const ugo_fec* c, const uint8_t* shards, const Layout& L) {
          ugo::kern::apply_dmax(c->d) != 0;
 }
 
+// Separate output batch of a reconstruct (ugo_fec_reconstruct_into); none = in place.
+struct OutBatch {
+  uint8_t* base = nullptr;
+  Layout L{0, 0};
+};
+
 ugo::kern::Batch base_batch(const ugo_fec* c, uint8_t* shards, size_t S, const Layout& L) {
   ugo::kern::Batch a{};
   a.base = shards;
@@ -241,13 +247,18 @@ int ensure_work(ugo_fec* c, size_t groups) {
 }
 
 int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
-                    const Layout& L, unsigned flags, int8_t* status, hipStream_t s) {
+                    const Layout& L, unsigned flags, int8_t* status, hipStream_t s, const OutBatch& O = {}) {
   if (groups == 0) return UGO_FEC_OK;
   if (!present) return UGO_FEC_ERR_INVALID_ARG;
   if (c->n > 64) return UGO_FEC_ERR_INVALID_ARG;  // 64-bit presence masks
-  const bool fast = fast_layout(c, shards, L);
+  const bool fast = fast_layout(c, shards, L) &&
+                    (!O.base || (reinterpret_cast<uintptr_t>(O.base) % 16 == 0 && O.L.rstride % 16 == 0 &&
+                                 O.L.gstride % 16 == 0));
   const int mode = c->d_table ? 1 : 2;
   ugo::kern::Batch a = base_batch(c, shards, S, L);
+  a.out = O.base;
+  a.ogstride = O.L.gstride;
+  a.orstride = O.L.rstride;
   a.present = present;
   a.status = status;
   a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
@@ -608,6 +619,27 @@ int ugo_fec_reconstruct_strided(ugo_fec* c, uint8_t* shards, const uint64_t* pre
   if (!device_view(shards) || !device_view(present) || !device_view(status)) return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
   return reconstruct_dev(c, shards, present, groups, S, L, flags, status, static_cast<hipStream_t>(stream));
+}
+
+int ugo_fec_reconstruct_into(ugo_fec* c, const uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
+                             size_t row_stride, size_t group_stride, uint8_t* out, size_t out_row_stride,
+                             size_t out_group_stride, unsigned flags, int8_t* status, void* stream) {
+  const Layout L{row_stride, group_stride};
+  int st = check_batch(c, shards, groups, S, L);
+  if (st) return st;
+  if (groups == 0) return UGO_FEC_OK;
+  // p output slots of S bytes per group: slots must not overlap each other or the next group's
+  if (!out || (c->p > 1 && out_row_stride < S) || (groups > 1 && out_group_stride < S)) return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(shards) || !device_view(present) || !device_view(status) || !device_view(out))
+    return UGO_FEC_ERR_INVALID_ARG;
+  TimerScope ts(c);
+  OutBatch O;
+  O.base = out;
+  O.L = Layout{out_row_stride, out_group_stride};
+  return reconstruct_dev(c, const_cast<uint8_t*>(shards), present, groups, S, L, flags, status,
+                         static_cast<hipStream_t>(stream), O);
 }
 
 int ugo_fec_reconstruct(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,

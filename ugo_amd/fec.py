@@ -122,6 +122,7 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_reconstruct.argtypes = [vp, vp, vp, sz, sz, sz, u, vp, vp]
     lib.ugo_fec_encode_strided.argtypes = [vp, vp, sz, sz, sz, sz, vp]
     lib.ugo_fec_reconstruct_strided.argtypes = [vp, vp, vp, sz, sz, sz, sz, u, vp, vp]
+    lib.ugo_fec_reconstruct_into.argtypes = [vp, vp, vp, sz, sz, sz, sz, vp, sz, sz, u, vp, vp]
     lib.ugo_fec_encode_host.argtypes = [vp, vp, sz, sz, sz]
     lib.ugo_fec_reconstruct_host.argtypes = [vp, vp, vp, sz, sz, sz, u, vp]
     lib.ugo_fec_check_shards.argtypes = [i, vp, i, ctypes.POINTER(sz)]
@@ -239,6 +240,32 @@ class Encoder:
         _raise(load_library().ugo_fec_reconstruct_strided(self._h, shards.data_ptr(), present.data_ptr(), G, S, rs,
                                                           gs, RECONSTRUCT_DATA_ONLY if data_only else 0, st,
                                                           _stream_handle(stream)))
+
+    def reconstruct_into(self, shards, present, out, shard_size: Optional[int] = None, data_only=False,
+                         status=None, stream=None, shard_major: bool = False, out_shard_major: bool = True):
+        """Reconstruct with a separate output batch (include/ugo_fec.h
+        ugo_fec_reconstruct_into): `shards` is only read; output i of group g (the
+        i-th erased row, ascending) goes to `out`, a contiguous uint8 CUDA tensor
+        [p][G][opitch] (out_shard_major) or [G][p][opitch]."""
+        G, pitch, rs, gs = self._geom(shards, shard_major)
+        assert present.is_contiguous() and present.numel() == G and present.element_size() == 8
+        assert out.is_contiguous() and out.element_size() == 1 and out.dim() == 3
+        p = self.ParityShards
+        if out_shard_major:
+            assert out.shape[0] == p and out.shape[1] == G
+            opitch = out.shape[2]
+            ors, ogs = G * opitch, opitch
+        else:
+            assert out.shape[0] == G and out.shape[1] == p
+            opitch = out.shape[2]
+            ors, ogs = opitch, p * opitch
+        S = pitch if shard_size is None else shard_size
+        assert opitch >= S
+        st = None if status is None else status.data_ptr()
+        _raise(load_library().ugo_fec_reconstruct_into(self._h, shards.data_ptr(), present.data_ptr(), G, S, rs, gs,
+                                                       out.data_ptr(), ors, ogs,
+                                                       RECONSTRUCT_DATA_ONLY if data_only else 0, st,
+                                                       _stream_handle(stream)))
 
     def rx_assemble(self, wire, lens, shards, present, first_group: int = 0, shard_size: Optional[int] = None,
                     pad=None, stats=None, stream=None, shard_major: bool = True):
