@@ -579,6 +579,23 @@ int main(int argc, char** argv) {
         b.status = reinterpret_cast<int8_t*>(ob);
       }
       const uint32_t grid = (pl.items + 255) / 256;
+      std::vector<Batch> rotk(roto);  // the product kernels' own out-of-place form (Batch::out)
+      for (auto& b : rotk) {
+        b.out = reinterpret_cast<uint8_t*>(b.status);
+        b.status = nullptr;
+        b.ogstride = pitch;
+        b.orstride = G * pitch;
+      }
+      vars.push_back({"COLD dec INTO production k_apply_p nt3", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD dec INTO k_apply_p lds-dma 10", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>), dim3(grid), dim3(256), 0, 0, rotk[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD dec INTO k_apply_p lds-dma 8", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 8>), dim3(grid), dim3(256), 0, 0, rotk[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD dec INTO k_apply_p nt1 (plain stores)", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 1>), dim3(grid), dim3(256), 0, 0, rotk[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD dec INTO k_apply_p emax3", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3, 1, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[(*cnt)++ & 3]); }, {}});
       vars.push_back({"COLD dec MEMORY PATTERN ONLY nt3, OUT-OF-PLACE outputs", dec_bytes, [=]() {
         hipLaunchKernelGGL((k_pattern_rec<3, false, true>), dim3(grid), dim3(256), 0, 0, roto[(*cnt)++ & 3]); }, {}});
       vars.push_back({"COLD dec MEMORY PATTERN ONLY lds-dma nt stores, OUT-OF-PLACE outputs", dec_bytes, [=]() {
