@@ -50,3 +50,6 @@ def test_null_arguments_rejected():
     assert lib.ugo_fec_encode(None, None, 1, 16, 16, None) == 6
     assert lib.ugo_fec_reconstruct(None, None, None, 1, 16, 16, 0, None, None) == 6
     assert lib.ugo_fec_check_shards(0, None, 1, None) == 6
+    # reconstruct_into: no context, then an empty batch (a no-op whatever the pointers)
+    assert lib.ugo_fec_reconstruct_into(None, None, None, 1, 16, 16, 208, None, 16, 48, 0, None, None) == 6
+    assert lib.ugo_fec_reconstruct_into(None, None, None, 0, 16, 16, 208, None, 16, 48, 0, None, None) == 6
