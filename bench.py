@@ -10,44 +10,58 @@ groups; %HBM roofline".  One step = one pass of the hot path over one batch:
 Inputs are resident in HBM before the timed region (synthetic, device-generated
 random bytes).  Steps alternate between 2 independent batches (--batches), so
 every step works on a batch none of whose lines sit in the Infinity Cache --
-the state a fresh batch of packets arrives in.  Algorithmic bytes per group: encode (d+p)*S,
-reconstruct (d+e)*S; value = sum over ranks / max-over-ranks time, in GiB/s.
+the state a fresh batch of packets arrives in.  Algorithmic bytes per group
+(BASELINE.md): encode (d+p)*S, reconstruct (d+e)*S; value = sum over ranks /
+max-over-ranks time, in GiB/s.
 
-Multi-GPU (torchrun, one process per GPU): packet groups are independent, so
-each rank owns its own batch (weak scaling) -- or a contiguous 1/N slice of
---total-groups (strong scaling) -- and no data-path collective runs; only the
-timing barrier and a max-reduction.
+Warm-up has two parts: a clock warm-up that runs untimed steps until at least
+--clock-warmup-ms of load has passed and the last chunks of steps agree within
+2 % (the clocks take ~20 ms of load to settle, so a step count alone is not a
+warm-up), then the --warmup steps the driver asks for.  The timed region is
+exactly --steps steps.
+
+Multi-GPU: `python bench.py --gpus N` (N > 1, no torchrun environment) starts
+N rank processes itself -- a child `torch.distributed.run` on 127.0.0.1, before
+anything in this process touches a GPU -- and forwards rank 0's JSON line.
+Packet groups are independent codewords (ugo/fec.go:145-146), so each rank
+owns its own batch (weak scaling, default) or a contiguous 1/N slice of
+--total-groups (strong scaling; BASELINE configs[3] is --total-groups 4194304),
+and no collective touches the data path.  The only cross-rank traffic is the
+timing barrier, one max-reduction and one all-ok reduction, which run over
+gloo on the host (--dist-backend): they are control, not data, so RCCL has
+nothing to carry.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--groups G]
+                       [--total-groups T]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from ugo_amd import fec  # noqa: E402
-from ugo_amd.shard import dist_env, partition  # noqa: E402
 
 METRIC = "FEC encode+decode GiB/s device-resident, (10+3)×1350B groups; %HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, GB/s (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); > 1 without a torchrun environment launches them")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=50,
-                    help="untimed steps; the clocks take ~20 ms of load to reach steady state")
+                    help="untimed steps after the clock warm-up")
+    ap.add_argument("--clock-warmup-ms", type=float, default=200.0,
+                    help="untimed load before the --warmup steps: at least this long, and until the last 3 "
+                         "chunks of steps agree within 2%% (capped at 10x this)")
     ap.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
     ap.add_argument("--total-groups", type=int, default=0, help="if set: strong scaling over this many groups")
     ap.add_argument("--data-shards", type=int, default=10)
@@ -67,20 +81,268 @@ def parse():
                          "ugo_fec_reconstruct_into (erased rows written to a separate [p][G][pitch] output batch, "
                          "the fresh buffers klauspost's Reconstruct gives ugo's nil shards)")
     ap.add_argument("--seed", type=int, default=0x5EED)
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--dist-backend", choices=["gloo", "nccl"], default="gloo",
+                    help="process group for the timing barrier and reductions (no data-path collective)")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=8.0,
+                    help="per leg of the CPU baseline (all cores, 1 core); the 2-erasure leg gets half")
     ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="CPU baseline threads (the GPU box's CPU share is 16; capped at os.cpu_count())")
+                    help="CPU baseline threads (the GPU box's CPU share is 16; capped at the affinity set)")
     ap.add_argument("--cpu-simd", type=int, default=-1,
                     help="CPU baseline SIMD level: -1 best available, 0 scalar, 1 AVX2, 2 AVX-512 GFNI")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
+# ------------------------------------------------------------------ launcher
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(argv, nproc: int, port: int, script: str = None):
+    """The child command `bench.py --gpus N` runs: one process per rank, the
+    rendezvous on 127.0.0.1 (the container hostname may not resolve)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)] + list(argv)
+
+
+def is_result_line(line: str) -> bool:
+    s = line.strip()
+    if not s.startswith("{"):
+        return False
+    try:
+        return "metric" in json.loads(s)
+    except ValueError:
+        return False
+
+
+def launch(argv, nproc: int, script: str = None, timeout: float = None) -> int:
+    """Runs the ranks as a child process (never exec: this process may not
+    replace itself) and forwards rank 0's JSON line as this process's only
+    stdout line; everything else the child prints goes to stderr.  Returns the
+    child's exit code."""
+    cmd = launcher_cmd(argv, nproc, free_port(), script)
+    print("bench.py: launching " + " ".join(cmd), file=sys.stderr, flush=True)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    n_lines = 0
+    try:
+        for line in proc.stdout:
+            if is_result_line(line) and n_lines == 0:
+                sys.stdout.write(line if line.endswith("\n") else line + "\n")
+                sys.stdout.flush()
+                n_lines += 1
+            else:
+                sys.stderr.write(line)
+        rc = proc.wait(timeout=timeout)
+    except BaseException:
+        proc.kill()
+        proc.wait()
+        raise
+    if rc == 0 and n_lines != 1:
+        print("bench.py: the ranks exited without a result line", file=sys.stderr)
+        return 1
+    return rc
+
+
+# ---------------------------------------------------- rank-side coordination
+def dist_setup(backend: str):
+    """(rank, local_rank, world) from the torchrun environment; joins the
+    process group when world > 1."""
+    from ugo_amd.shard import dist_env
+
+    rank, local_rank, world = dist_env()
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group(backend, init_method="env://")
+    return rank, local_rank, world
+
+
+def rank_groups(total_groups: int, groups: int, rank: int, world: int):
+    """(first group, groups on this rank, scaling, total groups).  Strong
+    scaling: a contiguous 1/world slice of total_groups; weak: `groups` each."""
+    from ugo_amd.shard import partition
+
+    if total_groups:
+        g0, g1 = partition(total_groups, world, rank)
+        return g0, g1 - g0, "strong", total_groups
+    return rank * groups, groups, "weak", groups * world
+
+
+def barrier(world: int):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def reduce_max(values, world: int):
+    """Element-wise max over ranks of a list of floats (host tensors, so any
+    backend carries it)."""
+    import torch
+
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
+def all_ranks_ok(ok: bool, world: int) -> bool:
+    import torch
+
+    t = torch.tensor([int(bool(ok))], dtype=torch.int64)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def timed_region(step, steps: int, sync, world: int) -> float:
+    """Exactly `steps` steps bracketed by barrier + device synchronize on both
+    sides; returns this rank's wall time (reduce_max gives the job's)."""
+    barrier(world)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier(world)
+    return time.perf_counter() - t0
+
+
+def clock_warmup(step, sync, min_ms: float, chunk: int = 5, tol: float = 0.02, max_ms: float = None):
+    """Untimed steps until at least min_ms of load has run and the last 3
+    chunks of `chunk` steps agree within `tol` (or max_ms has passed).
+    Returns (elapsed ms, steps run, settled)."""
+    max_ms = 10 * min_ms if max_ms is None else max_ms
+    times = []
+    n = 0
+    sync()
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        for _ in range(chunk):
+            step()
+        sync()
+        t1 = time.perf_counter()
+        n += chunk
+        times.append(t1 - t0)
+        el = (t1 - t_start) * 1e3
+        last = times[-3:]
+        settled = len(last) == 3 and max(last) <= (1 + tol) * min(last)
+        if (el >= min_ms and settled) or el >= max_ms:
+            return el, n, settled
+
+
+# ------------------------------------------------------------- CPU baseline
+def host_info():
+    """CPU model, machine CPU count, this process's CPU share and whether a Go
+    toolchain exists (the reference is Go; BASELINE.md's CPU plan)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        share = os.cpu_count() or 1
+    go = shutil.which("go")
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": share,
+            "go_toolchain": "present" if go else "absent"}
+
+
+def cpu_baseline(args, d, p, S, n):
+    """The CPU oracle timed on this host's cores (rank 0, N = 1, after the GPU
+    work).  Main figure: BASELINE configs[0] -- 1,024 groups of (10+3)x1350,
+    Encode of every group, then 1 uniformly random erased shard per group and
+    Reconstruct, each group one call as ugo/fec.go:196-217 (input) and
+    :228-243 (calcECC) make them -- on all cores of this process's share and
+    on 1 core.  Secondary: the bench's own 2-erasure workload on 4,096 groups.
+    oracle/rs_oracle.c restates the upstream algorithm with the upstream
+    library's SIMD strategy (AVX-512 GFNI affine or AVX2 nibble tables, per-
+    pattern inverse cache).  The Go reference needs a Go toolchain, which
+    the box lacks (host_info probes for one)."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import rs_ref  # checker / CPU baseline only
+
+    rs_ref.load_c_oracle()
+    info = host_info()
+    level = rs_ref.set_simd(args.cpu_simd)
+    threads = max(1, min(args.cpu_threads, info["affinity_cpus"]))
+    rng = np.random.default_rng(args.seed)
+
+    def sample(G, erasures):
+        sh = rng.integers(0, 256, size=(G, n, S), dtype=np.uint8)
+        masks = np.full(G, (1 << n) - 1, np.uint64)
+        for g in range(G):
+            for r in rng.choice(n, erasures, replace=False):
+                masks[g] &= ~np.uint64(1 << int(r))
+        return sh, masks
+
+    def leg(sh, masks, erasures, nthreads, seconds):
+        G = sh.shape[0]
+        passes = 0
+        t0 = time.perf_counter()
+        while True:
+            rs_ref.c_encode(d, p, sh, threads=nthreads)
+            rc, st = rs_ref.c_reconstruct(d, p, sh, masks, threads=nthreads)
+            assert rc == 0
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+        per_pass = G * ((d + p) * S + (d + erasures) * S)
+        return round(per_pass * passes / el / 2**30, 4), passes, el
+
+    try:
+        sh1, m1 = sample(1024, 1)
+        v_all, n_all, t_all = leg(sh1, m1, 1, threads, args.cpu_baseline_seconds)
+        v_one, n_one, t_one = leg(sh1, m1, 1, 1, args.cpu_baseline_seconds)
+        sh2, m2 = sample(4096, args.erasures)
+        v_two, n_two, t_two = leg(sh2, m2, args.erasures, threads, args.cpu_baseline_seconds / 2)
+    finally:
+        rs_ref.set_simd(0)
+    simd = rs_ref.SIMD_NAMES[level]
+    out = {"value": v_all, "unit": "GiB/s", "cores": threads, "kind": "port",
+           "sample": f"BASELINE configs[0]: 1024 groups ({d}+{p})x{S}B, Encode every group then 1 uniformly "
+                     f"random erased shard per group and Reconstruct, one group per call (ugo/fec.go:196-217, "
+                     f":228-243); {n_all} passes in {t_all:.1f}s on {threads} threads; oracle/rs_oracle.c "
+                     f"[{simd}], a C restatement of the klauspost algorithm and its SIMD strategy (the Go "
+                     f"reference cannot run: go toolchain {info['go_toolchain']})",
+           "single_core": {"value": v_one, "unit": "GiB/s", "cores": 1, "passes": n_one,
+                           "seconds": round(t_one, 2)},
+           "two_erasure_4096": {"value": v_two, "unit": "GiB/s", "cores": threads, "passes": n_two,
+                                "seconds": round(t_two, 2),
+                                "sample": f"4096 groups, encode + {args.erasures}-erasure reconstruct (the "
+                                          f"bench's own workload)"},
+           "simd": simd}
+    out.update(info)
+    return out
+
+
+# -------------------------------------------------------------- GPU ranks
 def make_masks(G, n, e, seed, device):
     """Presence masks with exactly e distinct erased shards per group."""
+    import torch
+
     gen = torch.Generator(device="cpu").manual_seed(seed)
     keys = torch.rand((G, n), generator=gen)
     erased = keys.argsort(dim=1)[:, :e]  # e distinct indices, uniform over C(n, e)
@@ -90,66 +352,30 @@ def make_masks(G, n, e, seed, device):
     return masks.to(device), erased
 
 
-def cpu_baseline(args, d, p, S, n, sample_groups=4096):
-    """The CPU oracle (oracle/rs_oracle.c: the upstream algorithm, with the
-    upstream library's SIMD strategy -- AVX-512 GFNI affine or AVX2 nibble
-    tables, fused multi-output column blocks, per-pattern inverse cache) timed
-    on this host's cores on a bounded sample of the same workload."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import rs_ref  # checker / CPU baseline only
+def run_rank(args):
+    import numpy as np
+    import torch
 
-    rs_ref.load_c_oracle()
-    level = rs_ref.set_simd(args.cpu_simd)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    rng = np.random.default_rng(args.seed)
-    sh = rng.integers(0, 256, size=(sample_groups, n, S), dtype=np.uint8)
-    masks = np.full(sample_groups, (1 << n) - 1, np.uint64)
-    for g in range(sample_groups):
-        for r in rng.choice(n, args.erasures, replace=False):
-            masks[g] &= ~np.uint64(1 << int(r))
-    t0 = time.perf_counter()
-    passes = 0
-    try:
-        while True:
-            rs_ref.c_encode(d, p, sh, threads=threads)
-            rs_ref.c_reconstruct(d, p, sh, masks, threads=threads)
-            passes += 1
-            el = time.perf_counter() - t0
-            if el >= args.cpu_baseline_seconds:
-                break
-    finally:
-        rs_ref.set_simd(0)
-    per_pass = sample_groups * ((d + p) * S + (d + args.erasures) * S)
-    return {"value": round(per_pass * passes / el / 2**30, 4), "unit": "GiB/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{sample_groups} groups ({d}+{p})x{S}B, encode + {args.erasures}-erasure reconstruct, "
-                      f"{passes} passes in {el:.1f}s on {threads} threads, oracle/rs_oracle.c "
-                      f"[{rs_ref.SIMD_NAMES[level]}] (C restatement of the klauspost algorithm and its SIMD "
-                      f"strategy; the Go reference cannot run: no Go toolchain)"}
+    from ugo_amd import fec
 
-
-def main():
-    args = parse()
-    rank, local_rank, world = dist_env()
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    rank, local_rank, world = dist_setup(args.dist_backend)
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible (the product path has no CPU fallback)")
+    dev_index = local_rank % ndev
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    ranks_per_device = -(-world // ndev) if world > ndev else 1
     d, p, S = args.data_shards, args.parity_shards, args.shard_size
     n = d + p
     pitch = args.pitch or (S + 15) // 16 * 16
-    if args.total_groups:
-        g0, g1 = partition(args.total_groups, world, rank)
-        G = g1 - g0
-        scaling = "strong"
-    else:
-        G = args.groups
-        g0 = rank * G
-        scaling = "weak"
+    g0, G, scaling, total_groups = rank_groups(args.total_groups, args.groups, rank, world)
     e = args.erasures
 
-    enc = fec.New(d, p, device=local_rank)
-    gen = torch.Generator(device=dev).manual_seed(args.seed + rank)
+    enc = fec.New(d, p, device=dev_index)
+    gen = torch.Generator(device=dev).manual_seed(args.seed + g0)
     planar = args.layout == "planar"
     shape = (n, G, pitch) if planar else (G, n, pitch)
     nb = max(1, args.batches)
@@ -172,22 +398,16 @@ def main():
         else:
             enc.reconstruct_batch(b, masks, shard_size=S, stream=stream, shard_major=planar)
 
+    sync = torch.cuda.synchronize
+    cw_ms, cw_steps, cw_settled = clock_warmup(step, sync, args.clock_warmup_ms)
+    barrier(world)  # ranks start the counted warm-up together, none idles after its clock warm-up
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
 
     # 1. The timed region (`value`): K steps of ordinary launches, barrier +
     #    synchronize on both sides, max over ranks.
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_region(step, args.steps, sync, world)
 
     # 2. Kernel-timing pass (`roofline`, `kernels`): the same K steps again with
     #    the library's launch timing on -- each launch issued with
@@ -196,11 +416,11 @@ def main():
     #    ~5 us per kernel boundary (tools/gap_probe.py: 374.8 vs 364.6 us per
     #    step), so the value pass above runs without them.
     enc.timing_begin(4 * args.steps + 16)
-    torch.cuda.synchronize()
+    sync()
     t1 = time.perf_counter()
-    for k in range(args.steps):
+    for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     elapsed_timing_pass = time.perf_counter() - t1
     recs, untimed = enc.timing_end()
     kid = recs["kernel"]
@@ -210,11 +430,7 @@ def main():
     enc_ms = float(recs["ms"][kid == 1].sum()) / args.steps
     dec_ms = float(recs["ms"][np.isin(kid, (2, 3))].sum()) / args.steps  # apply (+ k_prepare for d+p > 16)
 
-    t = torch.tensor([elapsed, enc_ms, dec_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, enc_ms_max, dec_ms_max = t.tolist()
-    total_groups = G * world if scaling == "weak" else args.total_groups
+    elapsed, enc_ms_max, dec_ms_max = reduce_max([elapsed, enc_ms, dec_ms], world)
 
     enc_bytes = G * n * S            # per launch, this rank
     dec_bytes = G * (d + e) * S
@@ -249,10 +465,7 @@ def main():
         ok_idem = bool(torch.equal(view[:, d:, :S], par))
         del ref, par
         verify = {"round_trip_full_size": ok_rt, "encode_idempotent": ok_idem}
-        okt = torch.tensor([int(ok_rt and ok_idem)], device=dev)
-        if world > 1:
-            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        verify["all_ranks_ok"] = bool(okt.item())
+        verify["all_ranks_ok"] = all_ranks_ok(ok_rt and ok_idem, world)
 
     if rank == 0:
         payload = G * d * S  # klauspost's convention: data bytes per call (BASELINE.md secondary column)
@@ -282,6 +495,10 @@ def main():
                         f"{args.steps} steps right after the timed region, from hipExtLaunchKernel start/stop "
                         f"events on the launch stream (ms_per_step of that pass: "
                         f"{elapsed_timing_pass / args.steps * 1e3:.4f})"}
+        if scaling == "strong":
+            workload = f"{total_groups} groups total, strong: {G} groups on rank 0"
+        else:
+            workload = f"{G} groups/GPU, weak: {total_groups} groups total"
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
@@ -289,19 +506,35 @@ def main():
             "data": "synthetic: device-generated uniform random bytes (seeded), "
                     f"{e} distinct uniformly random erased shards per group",
             "config": {"workload": f"({d}+{p})x{S}B groups, encode + {e}-erasure reconstruct, device-resident, "
-                                   f"{G} groups/GPU", "groups_per_gpu": G, "total_groups": total_groups,
+                                   + workload, "groups_per_gpu": G, "total_groups": total_groups,
                        "data_shards": d, "parity_shards": p, "shard_size": S, "pitch": pitch, "erasures": e,
                        "layout": "shard-major [d+p][G][pitch]" if planar else "group-major [G][d+p][pitch]",
                        "batches_per_gpu": nb, "decode": args.decode,
                        "parallelism": f"dp{world} (independent packet groups, no collective)"},
+            "clock_warmup_ms": round(cw_ms, 1), "clock_warmup_steps": cw_steps, "clock_settled": cw_settled,
             "pct_hbm_roofline": round(step_bytes_all / world * args.steps / elapsed / (HBM_PEAK_GBS * 1e9), 4),
             "roofline": roof, "kernels": kern, "verify": verify,
         }
+        if ranks_per_device > 1:
+            out["config"]["ranks_per_device"] = ranks_per_device
+            out["note"] = (f"{world} ranks on {ndev} device(s): a launcher rehearsal, not an {world}-GPU "
+                           f"measurement")
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, d, p, S, n)
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
+        import torch.distributed as dist
+
         dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # nothing here has touched a GPU yet: start the ranks as a child process
+        sys.exit(launch(argv, args.gpus))
+    run_rank(args)
 
 
 if __name__ == "__main__":

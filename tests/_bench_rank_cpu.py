@@ -1,0 +1,62 @@
+"""torchrun target for tests/test_bench_dist.py (CPU, gloo): one rank of
+bench.py's multi-GPU decomposition with the CPU oracle standing in for the
+rank's GPU (checker only).  It calls bench.py's own coordination functions --
+dist_setup, rank_groups, clock_warmup, timed_region, reduce_max, all_ranks_ok
+-- and rank 0 prints one JSON result line, as bench.py's ranks do."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+import rs_ref  # noqa: E402
+
+
+def main():
+    total = int(os.environ.get("BENCH_TEST_TOTAL", "1000"))
+    args = bench.parse(sys.argv[1:])
+    rank, local_rank, world = bench.dist_setup("gloo")
+    assert world == args.gpus, (world, args.gpus)
+    d, p, S = 10, 3, 64
+    n = d + p
+    g0, G, scaling, tot = bench.rank_groups(total, 0, rank, world)
+    rng = np.random.default_rng(123)
+    full = rng.integers(0, 256, (total, n, S), dtype=np.uint8)  # same synthetic batch on every rank
+    mine = np.ascontiguousarray(full[g0:g0 + G])
+    ref = full.copy()
+    rs_ref.c_encode(d, p, ref)
+
+    def step():
+        rs_ref.c_encode(d, p, mine)
+
+    cw_ms, cw_steps, settled = bench.clock_warmup(step, lambda: None, 5.0)
+    elapsed = bench.timed_region(step, 3, lambda: None, world)
+    ok = bool(np.array_equal(mine, ref[g0:g0 + G]))
+    erased = mine.copy()
+    erased[:, [2, 11]] = 0
+    masks = np.full(G, ((1 << n) - 1) & ~(1 << 2) & ~(1 << 11), np.uint64)
+    rs_ref.c_reconstruct(d, p, erased, masks)
+    ok = ok and bool(np.array_equal(erased, mine))
+    tmax, gmax, ranks = bench.reduce_max([0.5 + rank, G, rank], world)
+    covered = bench.reduce_max([g0 + G if rank == world - 1 else 0], world)[0]
+    all_ok = bench.all_ranks_ok(ok, world)
+    one_bad = bench.all_ranks_ok(ok and rank != world - 1, world)
+    if rank == 0:
+        print(json.dumps({"metric": "test", "n_gpus": world, "scaling": scaling, "total_groups": tot,
+                          "tmax": tmax, "gmax": gmax, "max_rank": ranks, "covered": covered, "all_ok": all_ok,
+                          "one_bad": one_bad, "elapsed_pos": elapsed > 0, "cw_steps": cw_steps}), flush=True)
+    else:
+        print("rank %d noise on stdout" % rank, flush=True)
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

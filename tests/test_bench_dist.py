@@ -1,0 +1,123 @@
+"""CPU tests of bench.py's N > 1 path (gloo, world_size 2).
+
+Packet groups are independent codewords (ugo/fec.go:145-146), so ranks own
+contiguous group ranges and nothing but the timing barrier and two scalar
+reductions crosses ranks.  These tests drive bench.py's own launcher
+(`bench.py --gpus N` starts the ranks as a child torch.distributed.run and
+forwards rank 0's line) and its own coordination code (dist_setup,
+rank_groups, clock_warmup, timed_region, reduce_max, all_ranks_ok) through
+tests/_bench_rank_cpu.py, a torchrun target that stands the CPU oracle in for
+each rank's GPU (checker only).
+"""
+import json
+import os
+import sys
+
+import pytest
+
+import bench
+from ugo_amd.shard import partition
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+RANK_SCRIPT = os.path.join(HERE, "_bench_rank_cpu.py")
+
+
+def test_launcher_command_shape():
+    cmd = bench.launcher_cmd(["--gpus", "4", "--steps", "20"], 4, 29512)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29512" in cmd
+    i = cmd.index(os.path.abspath(bench.__file__))
+    assert cmd[i + 1:] == ["--gpus", "4", "--steps", "20"], "the child gets the same arguments"
+
+
+def test_main_dispatch(monkeypatch):
+    calls = []
+    monkeypatch.setattr(bench, "launch", lambda argv, n, **k: calls.append(("launch", n, list(argv))) or 0)
+    monkeypatch.setattr(bench, "run_rank", lambda args: calls.append(("rank", args.gpus)))
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    bench.main(["--steps", "3"])  # --gpus 1: unchanged, runs in this process
+    assert calls[-1] == ("rank", 1)
+    with pytest.raises(SystemExit) as ex:
+        bench.main(["--gpus", "2", "--steps", "3"])  # no torchrun environment: launches
+    assert ex.value.code == 0 and calls[-1] == ("launch", 2, ["--gpus", "2", "--steps", "3"])
+    monkeypatch.setenv("WORLD_SIZE", "2")  # inside torchrun: this process is a rank
+    bench.main(["--gpus", "2"])
+    assert calls[-1] == ("rank", 2)
+
+
+def test_result_line_filter():
+    assert bench.is_result_line('{"metric": "x", "value": 1}\n')
+    assert not bench.is_result_line('{"other": 1}')
+    assert not bench.is_result_line("rank 1 noise on stdout")
+    assert not bench.is_result_line("{not json")
+
+
+@pytest.mark.parametrize("total", [1000, 7])
+def test_two_ranks_through_bench_launcher(total, capfd, monkeypatch):
+    """bench.launch starts 2 gloo ranks; rank 0's line is the only stdout line."""
+    monkeypatch.setenv("BENCH_TEST_TOTAL", str(total))
+    rc = bench.launch(["--gpus", "2"], 2, script=RANK_SCRIPT, timeout=240)
+    out, err = capfd.readouterr()
+    assert rc == 0, err[-2000:]
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1, out
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["scaling"] == "strong" and r["total_groups"] == total
+    assert r["tmax"] == 1.5, "max-over-ranks time reduction"
+    assert r["max_rank"] == 1.0
+    sizes = [partition(total, 2, k)[1] - partition(total, 2, k)[0] for k in range(2)]
+    assert r["gmax"] == max(sizes)
+    assert r["covered"] == total, "the last rank's range ends at the total"
+    assert r["all_ok"] is True, "every rank's slice equals the single-process result"
+    assert r["one_bad"] is False, "one failing rank makes all_ranks_ok false"
+    assert r["elapsed_pos"] and r["cw_steps"] >= 15
+    assert "rank 1 noise on stdout" in err, "other ranks' stdout goes to stderr"
+
+
+def test_rank_groups_weak_and_strong():
+    assert bench.rank_groups(0, 65536, 3, 8) == (3 * 65536, 65536, "weak", 8 * 65536)
+    g0, G, sc, tot = bench.rank_groups(4194304, 65536, 7, 8)
+    assert (g0, G, sc, tot) == (7 * 524288, 524288, "strong", 4194304)
+    spans = [bench.rank_groups(10, 0, r, 3)[:2] for r in range(3)]
+    assert spans == [(0, 3), (3, 3), (6, 4)]
+
+
+def test_clock_warmup_waits_for_settled_steps():
+    import itertools
+    import time
+
+    # step times fall for 6 chunks (the clock ramp), then settle
+    durs = itertools.chain([0.004, 0.003, 0.0025, 0.002, 0.0015, 0.0012], itertools.repeat(0.001))
+    cur = {"d": 0.0}
+
+    def step():
+        pass
+
+    def sync():
+        time.sleep(cur["d"])
+        cur["d"] = next(durs)
+
+    ms, steps, settled = bench.clock_warmup(step, sync, 1.0, chunk=1, max_ms=1000.0)
+    assert settled and steps >= 8, (ms, steps)
+    ms, steps, settled = bench.clock_warmup(step, lambda: time.sleep(0.002), 30.0, chunk=1)
+    assert ms >= 30.0 and settled
+
+
+def test_partition_covers_exactly_once():
+    for total in (0, 1, 7, 65536, 4194304):
+        for world in (1, 2, 3, 8):
+            ranges = [partition(total, world, r) for r in range(world)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == total
+            for (a0, a1), (b0, b1) in zip(ranges, ranges[1:]):
+                assert a1 == b0 and a0 <= a1
+            sizes = [b - a for a, b in ranges]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        partition(10, 2, 2)
+
+
+def test_host_info_fields():
+    info = bench.host_info()
+    assert set(info) == {"cpu_model", "nproc", "affinity_cpus", "go_toolchain"}
+    assert info["go_toolchain"] in ("present", "absent") and info["affinity_cpus"] >= 1
