@@ -39,7 +39,9 @@
 extern "C" {
 #endif
 
-#define UGO_FEC_ABI_VERSION 1
+/* 2: ugo_fec_rx_assemble keeps the first copy of a repeated seqid and its
+ *    stats grew a fifth counter (duplicates). */
+#define UGO_FEC_ABI_VERSION 2
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
  * that ugo/fec.go logs and swallows (ugo/fec.go:60-63, 208-210, 239-241). */
@@ -157,8 +159,26 @@ int ugo_fec_check_shards(int n, const size_t* lens, int nil_ok, size_t* shard_si
  * group seqid/(d+p) - first_group of the strided batch: its payload bytes
  * [0, min(len-6, shard_size)) then zeros up to shard_size; bit row of
  * present[group] is OR-ed (zero `present` before the first call of a batch).
- * stats (device u32[4], nullable) counts accepted / bad-flag / out-of-window /
- * too-short packets.  Then ugo_fec_reconstruct_strided recovers the batch. */
+ * stats (device u32[5], nullable) counts accepted / bad-flag / out-of-window /
+ * too-short / duplicate packets.  Then ugo_fec_reconstruct_strided recovers
+ * the batch.
+ *
+ * Batch-window rule (what replaces input's per-packet queue, ugo/fec.go:107-226):
+ *  - one call is one window of arrivals, in ring order (packet index order);
+ *  - dedupe (ugo/fec.go:123-129: a seqid already queued drops the new packet):
+ *    for each seqid the FIRST accepted packet in ring order is placed; later
+ *    copies -- whatever their payload or length -- count as duplicates and
+ *    write nothing.  Deterministic: the same ring gives the same batch;
+ *  - expiry (fecExpire, ugo/fec.go:109-121) and the rxlimit trim (:220-224)
+ *    bound how long a packet waits for its group.  Here the caller bounds it
+ *    by what it puts in a ring and by [first_group, first_group + groups):
+ *    packets of groups outside that window are counted out-of-window and
+ *    dropped, as a packet older than rxlimit arrivals or fecExpire is;
+ *  - duplicates are only detected within one call: a seqid placed by an
+ *    earlier call into the same batch is overwritten by a later call's copy
+ *    (give each window its own batch, or one call per batch).
+ * The engine takes (groups*(d+p)*4) bytes of stream-ordered scratch per call.
+ * npackets < 2^32 - 1. */
 int ugo_fec_rx_assemble(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, const uint16_t* lens,
                         size_t npackets, const uint8_t* pad, uint64_t first_group, size_t groups,
                         uint8_t* shards, size_t shard_size, size_t row_stride, size_t group_stride,

@@ -217,6 +217,56 @@ def test_full_size_round_trip_and_linearity(gpu):
     assert np.array_equal(sample[:, :, :S], want[:, :, :S])
 
 
+def test_full_size_timed_form_vs_oracle(gpu):
+    """The exact form bench.py times (BASELINE configs[1]+[2]): planar
+    [13][65536][1360] batch, encode, then reconstruct_into a separate
+    [3][65536][1360] output with 2 uniformly random erasures per group
+    (bench.make_masks).  Full-size round trip, plus 512 groups checked byte for
+    byte against the oracle (encode and reconstruct), the output slots past the
+    erasures untouched and the input never written."""
+    import bench
+
+    d, p, n, S, pitch, G = 10, 3, 13, 1350, 1360, 65536
+    enc = fec.New(d, p)
+    gen = torch.Generator(device="cuda").manual_seed(0x5EED)
+    sh = torch.randint(0, 256, (n, G, pitch), dtype=torch.uint8, device="cuda", generator=gen)
+    host0 = sh.cpu().numpy()
+    enc.encode_batch(sh, shard_size=S, shard_major=True)
+    masks, erased = bench.make_masks(G, n, 2, 0x5EED + 1000, "cuda")
+    view = sh.transpose(0, 1)
+    full = view.clone()
+    gi = torch.arange(G, device="cuda")
+    for j in range(2):
+        view[gi, erased[:, j].cuda()] = 0
+    before = sh.clone()
+    out = torch.full((p, G, pitch), 0xA5, dtype=torch.uint8, device="cuda")
+    st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    enc.reconstruct_into(sh, masks, out, shard_size=S, status=st, shard_major=True)
+    torch.cuda.synchronize()
+    assert torch.equal(sh, before), "reconstruct_into wrote its input"
+    assert bool((st == 0).all())
+    es = erased.sort(dim=1).values.cuda()
+    for j in range(2):  # the full round trip
+        assert torch.equal(out[j, :, :S], full[gi, es[:, j], :S])
+    assert bool((out[2] == 0xA5).all()), "slot past the erasures written"
+    # oracle sample: 512 groups spread over the batch
+    idx = np.sort(np.random.default_rng(3).choice(G, 512, replace=False))
+    smp = np.ascontiguousarray(host0.transpose(1, 0, 2)[idx][:, :, :S])
+    rs_ref.c_encode(d, p, smp)
+    got_full = full[torch.as_tensor(idx).cuda()].cpu().numpy()[:, :, :S]
+    assert np.array_equal(got_full, smp), "encode differs from the oracle"
+    m = masks.cpu().numpy().view(np.uint64)[idx]
+    inp = _erase(smp, m, n)
+    want = inp.copy()
+    rc, want_st = rs_ref.c_reconstruct(d, p, want, m)
+    assert rc == 0 and not want_st.any()
+    o = out.cpu().numpy()[:, idx, :S]
+    er = es.cpu().numpy()[idx]
+    for k in range(len(idx)):
+        for j in range(2):
+            assert np.array_equal(o[j, k], want[k, er[k, j]]), (idx[k], j)
+
+
 def test_go_shaped_api(gpu):
     enc = fec.New(10, 3)
     rng = np.random.default_rng(4)

@@ -44,6 +44,17 @@ def test_kat_galois(kat):
         assert [lib.oracle_gf_mul(int(c), x) for x in inp[: len(want)]] == want
 
 
+@pytest.mark.xfail(strict=True, reason="recalled upstream galMulSlice(177) tail disagrees with both restatements; "
+                                       "kept on record until a pinned fixture settles it")
+def test_kat_galois_disputed_tail(kat):
+    disp = kat["gal_mul_slice_disputed"]
+    c, inp = disp["coefficient"], disp["inputs"]
+    lib = rs_ref.load_c_oracle()
+    ours = [rs_ref.gf_mul(c, x) for x in inp]
+    assert ours == [lib.oracle_gf_mul(c, x) for x in inp] == disp["restatements"]  # the two restatements agree
+    assert ours == disp["recalled"]
+
+
 def test_kat_matrix(kat):
     mm = kat["matrix_multiply"]
     assert rs_ref.mat_mul(mm["a"], mm["b"]) == mm["out"]

@@ -28,6 +28,53 @@ def test_rc4_known_answers_and_product_keystream():
         assert fec.rc4_keystream(key, 1536) == rc4_ref.keystream(key, 1536)
 
 
+def _expected_placement(wire, G, n, S, pitch, first_group):
+    """The batch ugo's per-packet path builds from `wire` in ring order
+    (decrypted packets): FEC.decode (ugo/fec.go:78-89), the flag filter of
+    Conn.handlePacket (ugo/conn.go:395), the group/slot of input
+    (ugo/fec.go:145,175), and its dedupe -- a seqid already queued drops the
+    new packet, so the first copy stays (ugo/fec.go:123-129).  Returns the
+    group-major batch, presence masks and stats [accepted, bad flag, out of
+    window, too short, duplicate]."""
+    want = np.zeros((G, n, pitch), np.uint8)
+    masks = np.zeros(G, np.uint64)
+    stats = [0, 0, 0, 0, 0]
+    seen = set()
+    for w in wire:
+        if len(w) < 6:
+            stats[3] += 1
+            continue
+        seq = int.from_bytes(w[:4], "little")
+        flag = int.from_bytes(w[4:6], "little")
+        if flag not in (0xF1, 0xF2):
+            stats[1] += 1
+            continue
+        g = seq // n - first_group
+        if not 0 <= g < G:
+            stats[2] += 1
+            continue
+        if seq in seen:
+            stats[4] += 1
+            continue
+        seen.add(seq)
+        stats[0] += 1
+        pl = w[6:6 + S]
+        want[g, seq % n, :] = 0
+        want[g, seq % n, :len(pl)] = np.frombuffer(pl, np.uint8)
+        masks[g] |= np.uint64(1 << (seq % n))
+    return want, masks, stats
+
+
+def _ring(wire, slot):
+    npk = len(wire)
+    slots = np.zeros((npk, slot), np.uint8)
+    lens = np.zeros(npk, np.uint16)
+    for i, w in enumerate(wire):
+        slots[i, :len(w)] = np.frombuffer(w, np.uint8)
+        lens[i] = len(w)
+    return slots, lens
+
+
 def _packets(groups, seed, full_len):
     tx = fec_ref.FEC.new(128, 10, 3, clock=lambda: 0)
     rng = np.random.default_rng(seed)
@@ -83,34 +130,14 @@ def test_rx_assemble_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_gro
         lens[i] = len(w)
 
     # expected: decode each (decrypted) packet on the CPU, place, reconstruct (oracle)
-    want = np.zeros((G, n, pitch), np.uint8)
-    masks = np.zeros(G, np.uint64)
-    stats = [0, 0, 0, 0]
-    for w in wire:
-        if len(w) < 6:
-            stats[3] += 1
-            continue
-        seq = int.from_bytes(w[:4], "little")
-        flag = int.from_bytes(w[4:6], "little")
-        if flag not in (0xF1, 0xF2):
-            stats[1] += 1
-            continue
-        g = seq // n - first_group
-        if not 0 <= g < G:
-            stats[2] += 1
-            continue
-        stats[0] += 1
-        pl = w[6:6 + S]
-        want[g, seq % n, :] = 0
-        want[g, seq % n, :len(pl)] = np.frombuffer(pl, np.uint8)
-        masks[g] |= np.uint64(1 << (seq % n))
+    want, masks, stats = _expected_placement(wire, G, n, S, pitch, first_group)
     exp = np.ascontiguousarray(want[:, :, :S])
     rc, exp_st = rs_ref.c_reconstruct(d, p, exp, masks, data_only=True)
 
     codec = fec.New(d, p)
     sh = torch.full((n, G, pitch), 0xAB, dtype=torch.uint8, device="cuda")  # garbage in unwritten rows
     present = torch.zeros(G, dtype=torch.int64, device="cuda")
-    st = torch.zeros(4, dtype=torch.int32, device="cuda")
+    st = torch.zeros(5, dtype=torch.int32, device="cuda")
     if ring == "pinned":
         put = lambda t: t.pin_memory()  # noqa: E731
     else:
@@ -144,6 +171,76 @@ def test_rx_assemble_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_gro
                     assert bytes(got[g, r]) == orig, (g, r)
                     nrec += 1
         assert nrec > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("encrypt,S,slot", [(True, 1470, 1488), (False, 1470, 1488), (True, 3000, 3024)])
+def test_rx_assemble_first_copy_wins(gpu, encrypt, S, slot):
+    """Repeated seqids with DIFFERENT payloads and lengths (a replayed or
+    corrupted packet with a valid header): the first copy in ring order is the
+    one placed, as ugo's input keeps the queued packet and drops the new one
+    (ugo/fec.go:123-129).  Copies sit next to each other (same wave), a wave
+    apart and far apart; two runs in one process are identical.  S = 3000 runs
+    the per-pass kernel (rows of more than 128 chunks)."""
+    d, p, n = 10, 3, 13
+    pitch = (S + 15) // 16 * 16
+    G = 512
+    rng = np.random.default_rng(77)
+    maxlen = min(S + 6, slot)
+
+    def pkt(seq, flag):
+        L = int(rng.integers(6, maxlen + 1))
+        b = bytearray(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        b[0:4] = seq.to_bytes(4, "little")
+        b[4:6] = flag.to_bytes(2, "little")
+        return bytes(b)
+
+    wire = []
+    for g in range(G):
+        for r in range(n):
+            if rng.random() < 0.1:
+                continue
+            seq = g * n + r
+            flag = 0xF1 if r < d else 0xF2
+            copies = 1 + int(rng.integers(0, 4)) if rng.random() < 0.3 else 1
+            for _ in range(copies):
+                wire.append(pkt(seq, flag))
+    # ring order: mostly shuffled, with runs of adjacent copies kept together
+    order = list(range(len(wire)))
+    rng.shuffle(order)
+    wire = [wire[i] for i in order]
+    hot = pkt(5 * n + 2, 0xF1)
+    wire[100:100] = [hot[:6] + bytes(rng.integers(0, 256, len(hot) - 6, dtype=np.uint8)) for _ in range(8)]
+    wire.insert(0, pkt(7 * n + 12, 0xF2))
+    wire.append(pkt(7 * n + 12, 0xF2))  # last copy of the first packet's seqid: dropped
+    want, masks, stats = _expected_placement(wire, G, n, S, pitch, 0)
+    assert stats[4] > 50
+
+    ks = rc4_ref.keystream(KEY, slot)
+    enc = [rc4_ref.xor_stream(KEY, w) if encrypt else w for w in wire]
+    slots, lens = _ring(enc, slot)
+    codec = fec.New(d, p)
+    pad = torch.frombuffer(bytearray(ks), dtype=torch.uint8).cuda() if encrypt else None
+    ring = torch.from_numpy(slots).cuda()
+    tl = torch.from_numpy(lens.view(np.int16)).cuda()
+    runs = []
+    for _ in range(2):
+        sh = torch.full((n, G, pitch), 0xAB, dtype=torch.uint8, device="cuda")
+        present = torch.zeros(G, dtype=torch.int64, device="cuda")
+        st = torch.zeros(5, dtype=torch.int32, device="cuda")
+        codec.rx_assemble(ring, tl, sh, present, shard_size=S, pad=pad, stats=st)
+        runs.append((sh.cpu().numpy(), present.cpu().numpy().view(np.uint64), st.cpu().tolist()))
+    for got, pres, st in runs:
+        assert st == stats
+        assert np.array_equal(pres, masks)
+        g_major = got.transpose(1, 0, 2)
+        for g in range(G):
+            for r in range(n):
+                if (int(masks[g]) >> r) & 1:
+                    assert np.array_equal(g_major[g, r, :S], want[g, r, :S]), (g, r)
+                else:
+                    assert (g_major[g, r] == 0xAB).all(), (g, r)  # unclaimed rows untouched
+    assert np.array_equal(runs[0][0], runs[1][0])
 
 
 @pytest.mark.gpu

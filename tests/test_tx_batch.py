@@ -190,9 +190,9 @@ def test_tx_rx_round_trip_full_size(gpu):
     del wire
     sh = torch.zeros((n, G, pitch), dtype=torch.uint8, device=dev)
     present = torch.zeros(G, dtype=torch.int64, device=dev)
-    stats = torch.zeros(4, dtype=torch.int32, device=dev)
+    stats = torch.zeros(5, dtype=torch.int32, device=dev)
     enc.rx_assemble(rx, rl, sh, present, shard_size=S, pad=pad, stats=stats)
-    assert stats.tolist() == [keep.numel(), 0, 0, 0]
+    assert stats.tolist() == [keep.numel(), 0, 0, 0, 0]
     status = torch.full((G,), -1, dtype=torch.int8, device=dev)
     enc.reconstruct_batch(sh, present, shard_size=S, data_only=True, status=status, shard_major=True)
     assert bool((status == 0).all())

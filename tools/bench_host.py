@@ -157,7 +157,7 @@ def rx_case(G, loss, reps, encrypt=True):
     lens = torch.full((npk,), 1476, dtype=torch.int16, device="cuda")
     sh = torch.empty((n, G, pitch), dtype=torch.uint8, device="cuda")
     present = torch.zeros(G, dtype=torch.int64, device="cuda")
-    st = torch.zeros(4, dtype=torch.int32, device="cuda")
+    st = torch.zeros(5, dtype=torch.int32, device="cuda")
 
     def run():
         present.zero_()

@@ -13,6 +13,12 @@
 // payload, and its presence bit is OR-ed into present[group]; Reconstruct
 // (k_apply*) then runs over the batch.
 //
+// Duplicates: input drops a packet whose seqid is already queued, so the
+// first arrival of a seqid is the one kept (ugo/fec.go:123-129).  A batch is
+// one window of arrivals in ring order: k_rx_claim takes, per (group, row),
+// the smallest packet index of an accepted packet (atomicMin), and the place
+// kernels write only that packet; later copies count as duplicates.
+//
 // The packet sits at a 16-aligned slot, so its payload (offset 6) is
 // misaligned: each thread loads the two aligned chunks covering its 16 output
 // bytes, XORs the keystream chunks, and realigns with v_alignbyte.
@@ -47,8 +53,8 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
   // stats: summed per block in LDS, one atomic per block per counter (a device
   // counter hit once per packet serialises at ~11 ns per atomic:
   // MI355X_MICROARCH.md "fanin")
-  __shared__ uint32_t bstats[4];
-  if (threadIdx.x < 4) bstats[threadIdx.x] = 0;
+  __shared__ uint32_t bstats[5];
+  if (threadIdx.x < 5) bstats[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, hl = lane & 31u;
   const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
@@ -67,15 +73,16 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
     if (a.pad) h ^= ld16(a.pad);
     const uint32_t seqid = h.x;
     const uint32_t flag = h.y & 0xffffu;
-    uint32_t why = 0;  // 0 = accept, else stats slot
-    if (!have) why = 4;
+    uint32_t why = 0;  // 0 = accept, else stats slot (5: no packet)
+    if (!have) why = 5;
     else if (len < 6u) why = 3;
     else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
     const uint32_t row = seqid % a.n;
     const uint64_t grp = seqid / a.n;
     if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
-    const bool ok = why == 0;
     const uint64_t gs = grp - a.first_group;
+    if (!why && a.win && a.win[gs * a.n + row] != static_cast<uint32_t>(i)) why = 4;  // not the first copy
+    const bool ok = why == 0;
     uint8_t* dst = a.shards + row * a.rstride + gs * a.gstride;
     const uint32_t L = ok ? min(len - 6u, a.S) : 0u;  // copy(buf, data[6:]) bounded by the row
     for (uint32_t q0 = 0; q0 < nq; q0 += 32u) {
@@ -123,14 +130,14 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
         }
       }
     }
-    if (hl == 0 && why < 4) {
+    if (hl == 0 && why < 5) {
       if (ok) atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
       atomicAdd(&bstats[why], 1u);
     }
   }
   if (a.stats) {
     __syncthreads();
-    if (threadIdx.x < 4 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+    if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
   }
 }
 
@@ -148,8 +155,8 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 // NT: bit 0 nontemporal payload loads, bit 1 nontemporal stores.
 template <int NP, int MODE = 0, int NT = 0>
 __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
-  __shared__ uint32_t bstats[4];
-  if (threadIdx.x < 4) bstats[threadIdx.x] = 0;
+  __shared__ uint32_t bstats[5];
+  if (threadIdx.x < 5) bstats[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, hl = lane & 31u;
   const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
@@ -189,16 +196,20 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
     }
     const uint32_t seqid = h.x;
     const uint32_t flag = h.y & 0xffffu;
-    uint32_t why = 0;  // 0 = accept, else stats slot
-    if (!have) why = 4;
+    uint32_t why = 0;  // 0 = accept, else stats slot (5: no packet)
+    if (!have) why = 5;
     else if (len < 6u) why = 3;
     else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
     const uint32_t row = seqid % a.n;
     const uint64_t grp = seqid / a.n;
     if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
-    const bool ok = why == 0;
-    const uint32_t L = ok ? min(len - 6u, a.S) : 0u;  // payload bytes kept
-    const uint32_t lim = ok ? L + 6u : 0u;            // packet bytes [0, lim) are needed
+    const bool acc = why == 0;
+    // first copy in ring order?  The claim word is loaded before the payload and
+    // only waited for at the stores (a duplicate's payload is loaded, then dropped)
+    uint32_t claim = static_cast<uint32_t>(i);
+    if (acc && a.win) claim = a.win[(grp - a.first_group) * a.n + row];
+    const uint32_t L = acc ? min(len - 6u, a.S) : 0u;  // payload bytes kept
+    const uint32_t lim = acc ? L + 6u : 0u;            // packet bytes [0, lim) are needed
     u32x4 A[NP];
     uint32_t bx[NP], by[NP];
 #pragma unroll
@@ -213,6 +224,8 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
         by[q] = B.y;
       }
     }
+    if (acc && claim != static_cast<uint32_t>(i)) why = 4;  // a later copy of a claimed seqid
+    const bool ok = why == 0;
     uint8_t* dst = a.shards + row * a.rstride + (grp - a.first_group) * a.gstride;
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
@@ -260,14 +273,37 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
         }
       }
     }
-    if (hl == 0 && why < 4) {
+    if (hl == 0 && why < 5) {
       if (MODE == 0 && ok) atomicOr(reinterpret_cast<unsigned long long*>(&a.present[grp - a.first_group]), 1ull << row);
       atomicAdd(&bstats[why], 1u);
     }
   }
   if (a.stats) {
     __syncthreads();
-    if (threadIdx.x < 4 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+    if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+  }
+}
+
+// First-arrival claim: one thread per packet reads its 8 header bytes (seqid,
+// flag), classifies it exactly as the place kernels do, and takes the
+// smallest index per (group, row).  ~8 B read per 1.5-KB packet.
+__global__ __launch_bounds__(256) void k_rx_claim(RxArgs a) {
+  const uint64_t nthreads = gridDim.x * 256ull;
+  uint32_t k0 = 0u, k1 = 0u;
+  if (a.pad) {
+    k0 = reinterpret_cast<const uint32_t*>(a.pad)[0];
+    k1 = reinterpret_cast<const uint32_t*>(a.pad)[1];
+  }
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < a.npk; i += nthreads) {
+    const uint32_t len = a.lens[i];
+    if (len < 6u) continue;
+    const uint32_t* h = reinterpret_cast<const uint32_t*>(a.wire + i * a.slot);
+    const uint32_t seqid = h[0] ^ k0;
+    const uint32_t flag = (h[1] ^ k1) & 0xffffu;
+    if (flag != 0xf1u && flag != 0xf2u) continue;
+    const uint64_t grp = seqid / a.n;
+    if (grp < a.first_group || grp >= a.first_group + a.groups) continue;
+    atomicMin(&a.win[(grp - a.first_group) * a.n + seqid % a.n], static_cast<uint32_t>(i));
   }
 }
 
@@ -276,6 +312,14 @@ static inline uint32_t rx_blocks(const RxArgs& a) {
   uint64_t blocks = (waves + 3) / 4;
   if (blocks > 2048u) blocks = 2048u;  // 8 workgroups per CU, grid-stride over packet pairs
   return static_cast<uint32_t>(blocks);
+}
+
+hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s) {
+  uint64_t blocks = (a.npk + 255) / 256;
+  if (blocks == 0) return hipSuccess;
+  if (blocks > 4096u) blocks = 4096u;
+  launch(kKRx, k_rx_claim, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {

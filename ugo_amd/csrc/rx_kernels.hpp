@@ -13,7 +13,8 @@ struct RxArgs {
   const uint8_t* pad;      // keystream XORed over each packet from byte 0, >= slot bytes, or null
   uint8_t* shards;         // batch base (device)
   uint64_t* present;       // per-group presence masks (device, OR-ed)
-  uint32_t* stats;         // accepted, bad flag, out of window, too short (device, nullable)
+  uint32_t* stats;         // accepted, bad flag, out of window, too short, duplicate (device, nullable)
+  uint32_t* win;           // [groups][n] first packet index per (group, row) (k_rx_claim), or null
   uint64_t npk;
   uint64_t slot;
   uint64_t first_group;
@@ -24,6 +25,10 @@ struct RxArgs {
   uint32_t n;              // d + p
 };
 
+// Claims every (group, row) for its first packet in ring order (atomicMin of
+// the packet index into a.win, which the caller fills with 0xff bytes), then
+// places the winners.  a.win == null places every accepted packet.
+hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s);
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s);
 
 }  // namespace kern

@@ -57,8 +57,10 @@ struct ugo_fec {
   uint8_t* d_gf = nullptr;  // exp[512] | log[256] | pad | gf::perm_tables at +1024
   uint8_t* d_encdesc = nullptr;
   uint8_t* d_table = nullptr;
-  uint8_t* d_work = nullptr;  // MODE 2 per-group descriptors
-  size_t work_groups = 0;
+  // stream-ordered scratch (MODE 2 descriptors, RX claim words): allocated and
+  // freed on the call's own stream, so calls on different streams never share
+  // a workspace
+  hipMemPool_t pool = nullptr;
   // host-path staging
   hipStream_t streams[kStreams] = {};
   uint8_t* d_stage[kStreams] = {};
@@ -157,7 +159,6 @@ void free_ctx(ugo_fec* c) {
   (void)hipFree(c->d_gf);
   (void)hipFree(c->d_encdesc);
   (void)hipFree(c->d_table);
-  (void)hipFree(c->d_work);
   (void)hipFree(c->d_zc_mask);
   (void)hipFree(c->d_zc_status);
   for (int i = 0; i < kStreams; ++i) {
@@ -165,6 +166,10 @@ void free_ctx(ugo_fec* c) {
     (void)hipFree(c->d_mask[i]);
     (void)hipFree(c->d_status[i]);
     if (c->streams[i]) (void)hipStreamDestroy(c->streams[i]);
+  }
+  if (c->pool) {
+    (void)hipDeviceSynchronize();  // async frees still queued on user streams
+    (void)hipMemPoolDestroy(c->pool);
   }
   delete c;
 }
@@ -213,6 +218,26 @@ int check_batch(const ugo_fec* c, const void* shards, size_t groups, size_t S, c
   return UGO_FEC_OK;
 }
 
+// Bytes spanned by `rows` x `groups` slots of S bytes (row r of group g at
+// g*gstride + r*rstride).
+size_t extent(size_t S, size_t rstride, size_t rows, size_t gstride, size_t groups) {
+  if (rows == 0 || groups == 0) return 0;
+  return (groups - 1) * gstride + (rows - 1) * rstride + S;
+}
+
+// True if those slots are pairwise disjoint: sorted by stride, the smaller
+// stride is >= S and the larger one clears a whole run of the smaller.
+bool layout_disjoint(size_t S, size_t rstride, size_t rows, size_t gstride, size_t groups) {
+  size_t small = rstride, ns = rows, large = gstride, nl = groups;
+  if (ns <= 1 || (nl > 1 && gstride < rstride)) {
+    std::swap(small, large);
+    std::swap(ns, nl);
+  }
+  if (ns > 1 && small < S) return false;
+  if (nl > 1 && large < (ns - 1) * small + S) return false;
+  return true;
+}
+
 int encode_dev(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, const Layout& L, hipStream_t s) {
   if (c->p == 0 || groups == 0) return UGO_FEC_OK;
   const bool fast = fast_layout(c, shards, L);
@@ -236,15 +261,28 @@ int encode_dev(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, const Layou
   return UGO_FEC_OK;
 }
 
-int ensure_work(ugo_fec* c, size_t groups) {
-  if (c->work_groups >= groups) return UGO_FEC_OK;
-  (void)hipFree(c->d_work);
-  c->d_work = nullptr;
-  c->work_groups = 0;
-  if (hipMalloc(&c->d_work, groups * c->desc_stride + 64) != hipSuccess) return UGO_FEC_ERR_HIP;
-  c->work_groups = groups;
-  return UGO_FEC_OK;
+// Scratch of `bytes` on stream s, from the context's memory pool (created on
+// first use; memory is kept in the pool between calls, so after the first call
+// an allocation is a host-side bookkeeping step).  Free with scratch_free on
+// the same stream.
+int scratch_alloc(ugo_fec* c, size_t bytes, hipStream_t s, void** out) {
+  *out = nullptr;
+  if (!c->pool) {
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = c->device;
+    if (hipMemPoolCreate(&c->pool, &props) != hipSuccess) {
+      c->pool = nullptr;
+      return UGO_FEC_ERR_HIP;
+    }
+    uint64_t keep = ~0ull;
+    (void)hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
+  return hip_status(hipMallocFromPoolAsync(out, bytes ? bytes : 16, c->pool, s));
 }
+
+int scratch_free(void* ptr, hipStream_t s) { return ptr ? hip_status(hipFreeAsync(ptr, s)) : UGO_FEC_OK; }
 
 int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
                     const Layout& L, unsigned flags, int8_t* status, hipStream_t s, const OutBatch& O = {}) {
@@ -264,12 +302,18 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
   a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
   a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
   size_t per = std::max<size_t>(1, kMaxItems / a.chunks);
+  uint8_t* work = nullptr;
   if (mode == 2) {
     // per-group descriptors, bounded workspace (<= 64 Ki groups per slice)
     per = std::min<size_t>(per, 65536);
-    const int st = ensure_work(c, std::min(per, groups));
+    const int st = scratch_alloc(c, std::min(per, groups) * c->desc_stride + 64, s, reinterpret_cast<void**>(&work));
     if (st) return st;
   }
+  struct Release {  // the workspace goes back to the pool after this call's kernels
+    uint8_t* p;
+    hipStream_t s;
+    ~Release() { (void)scratch_free(p, s); }
+  } release{work, s};
   for (size_t g0 = 0; g0 < groups; g0 += per) {
     const size_t gn = std::min(per, groups - g0);
     a.g0 = g0;
@@ -278,7 +322,7 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
       a.desc = c->d_table;
     } else {
       ugo::kern::Prep pr{};
-      pr.desc = c->d_work;
+      pr.desc = work;
       pr.present = present;
       pr.M = c->d_M;
       pr.gf_exp = c->d_gf;
@@ -292,7 +336,7 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
       pr.dpad = c->dpad;
       pr.epad = c->epad;
       if (ugo::kern::launch_prepare(pr, static_cast<uint32_t>(gn), s) != hipSuccess) return UGO_FEC_ERR_HIP;
-      a.desc = c->d_work;
+      a.desc = work;
       a.g_desc0 = g0;
     }
     hipError_t e = fast ? ugo::kern::launch_apply(mode, ugo::kern::apply_dmax(c->d), a, s)
@@ -628,8 +672,17 @@ int ugo_fec_reconstruct_into(ugo_fec* c, const uint8_t* shards, const uint64_t* 
   int st = check_batch(c, shards, groups, S, L);
   if (st) return st;
   if (groups == 0) return UGO_FEC_OK;
-  // p output slots of S bytes per group: slots must not overlap each other or the next group's
-  if (!out || (c->p > 1 && out_row_stride < S) || (groups > 1 && out_group_stride < S)) return UGO_FEC_ERR_INVALID_ARG;
+  // p output slots of S bytes per group: no two slots may overlap (the smaller
+  // stride must clear S, the larger one a whole run of the smaller), and the
+  // output may not overlap the batch it reads (other lanes would read rows
+  // being overwritten)
+  if (!out || !layout_disjoint(S, out_row_stride, size_t(c->p), out_group_stride, groups)) return UGO_FEC_ERR_INVALID_ARG;
+  {
+    const size_t in_ext = extent(S, row_stride, size_t(c->n), group_stride, groups);
+    const size_t out_ext = extent(S, out_row_stride, size_t(c->p), out_group_stride, groups);
+    const uintptr_t i0 = reinterpret_cast<uintptr_t>(shards), o0 = reinterpret_cast<uintptr_t>(out);
+    if (o0 < i0 + in_ext && i0 < o0 + out_ext) return UGO_FEC_ERR_INVALID_ARG;
+  }
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
   if (!device_view(shards) || !device_view(present) || !device_view(status) || !device_view(out))
@@ -682,7 +735,8 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
   if (npk == 0) return UGO_FEC_OK;
-  if (!wire || !lens || !shards || !present || groups == 0 || c->n > 64) return UGO_FEC_ERR_INVALID_ARG;
+  if (!wire || !lens || !shards || !present || groups == 0 || c->n > 64 || npk >= 0xffffffffull)
+    return UGO_FEC_ERR_INVALID_ARG;
   if (slot_stride % 16 || slot_stride < 16 || reinterpret_cast<uintptr_t>(wire) % 16 ||
       reinterpret_cast<uintptr_t>(shards) % 16 || row_stride % 16 || group_stride % 16 ||
       (pad && reinterpret_cast<uintptr_t>(pad) % 16) || S > 0xffffffffu)
@@ -709,7 +763,18 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   a.gstride = group_stride;
   a.S = static_cast<uint32_t>(S);
   a.n = static_cast<uint32_t>(c->n);
-  return hip_status(ugo::kern::launch_rx_scatter(a, static_cast<hipStream_t>(stream)));
+  // first arrival wins (ugo/fec.go:123-129): claim words [groups][n], all 0xff
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t wbytes = groups * size_t(c->n) * sizeof(uint32_t);
+  void* win = nullptr;
+  int st = scratch_alloc(c, wbytes, s, &win);
+  if (st) return st;
+  a.win = static_cast<uint32_t*>(win);
+  if (hipMemsetAsync(win, 0xff, wbytes, s) != hipSuccess) st = UGO_FEC_ERR_HIP;
+  if (!st) st = hip_status(ugo::kern::launch_rx_claim(a, s));
+  if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
+  const int fr = scratch_free(win, s);
+  return st ? st : fr;
 }
 
 int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const uint16_t* lens, size_t groups,

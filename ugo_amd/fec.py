@@ -272,7 +272,11 @@ class Encoder:
         """RX group assembly (include/ugo_fec.h ugo_fec_rx_assemble): wire = uint8 CUDA
         tensor [npk, slot] of received packets, lens = int16/uint16 CUDA tensor [npk];
         pad = uint8 CUDA keystream (>= slot bytes) or None; present = int64 CUDA [G]
-        (zeroed by the caller); stats = int32 CUDA [4] or None."""
+        (zeroed by the caller); stats = int32 CUDA [5] (accepted, bad flag, out of
+        window, too short, duplicate) or None.  A repeated seqid keeps its first
+        copy in ring order (ugo/fec.go:123-129)."""
+        if stats is not None:
+            assert stats.numel() >= 5 and stats.element_size() == 4
         G, pitch, rs, gs = self._geom(shards, shard_major)
         npk, slot = wire.shape
         assert wire.is_contiguous() and lens.is_contiguous() and lens.element_size() == 2 and lens.numel() == npk
