@@ -1,5 +1,8 @@
 // reedsolomon.cpp -- see reedsolomon.hpp.  One group per call, staged through
 // a pinned buffer into the host-batch entry points of the C-ABI (groups = 1).
+// Rows are staged at a 16-byte pitch, so the vector kernels run whatever the
+// shard size (ugo's 1470-B calcECC window and 1476-B input shards are not
+// multiples of 16), and the pinned stage is used zero-copy by the engine.
 #include "reedsolomon.hpp"
 
 #include <cstring>
@@ -46,15 +49,18 @@ int Encoder::Encode(std::vector<Bytes>& shards) {
   return EncodeWindows(rows.data(), S);
 }
 
+static inline size_t pitch_of(size_t S) { return (S + 15) / 16 * 16; }
+
 int Encoder::EncodeWindows(uint8_t* const* rows, size_t S) {
   const int n = Shards();
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
-  uint8_t* buf = staging(size_t(n) * S);
+  const size_t pitch = pitch_of(S);
+  uint8_t* buf = staging(size_t(n) * pitch);
   if (!buf) return UGO_FEC_ERR_HIP;
-  for (int k = 0; k < d_; ++k) std::memcpy(buf + size_t(k) * S, rows[k], S);
-  const int st = ugo_fec_encode_host(ctx_, buf, 1, S, S);
+  for (int k = 0; k < d_; ++k) std::memcpy(buf + size_t(k) * pitch, rows[k], S);
+  const int st = ugo_fec_encode_host(ctx_, buf, 1, S, pitch);
   if (st) return st;
-  for (int k = d_; k < n; ++k) std::memcpy(rows[k], buf + size_t(k) * S, S);
+  for (int k = d_; k < n; ++k) std::memcpy(rows[k], buf + size_t(k) * pitch, S);
   return UGO_FEC_OK;
 }
 
@@ -67,20 +73,21 @@ int Encoder::reconstruct(std::vector<Bytes>& shards, unsigned flags) {
   size_t S = 0;
   int st = ugo_fec_check_shards(n, lens.data(), 1, &S);
   if (st) return st;
-  uint8_t* buf = staging(size_t(n) * S);
+  const size_t pitch = pitch_of(S);
+  uint8_t* buf = staging(size_t(n) * pitch);
   if (!buf) return UGO_FEC_ERR_HIP;
   uint64_t mask = 0;
   for (int r = 0; r < n; ++r)
     if (lens[r]) {
       mask |= 1ull << r;
-      std::memcpy(buf + size_t(r) * S, shards[r].data(), S);
+      std::memcpy(buf + size_t(r) * pitch, shards[r].data(), S);
     }
   int8_t status = 0;
-  st = ugo_fec_reconstruct_host(ctx_, buf, &mask, 1, S, S, flags, &status);
+  st = ugo_fec_reconstruct_host(ctx_, buf, &mask, 1, S, pitch, flags, &status);
   if (st) return st;
   const int limit = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? d_ : n;
   for (int r = 0; r < limit; ++r)
-    if (!lens[r]) shards[r].assign(buf + size_t(r) * S, buf + size_t(r + 1) * S);
+    if (!lens[r]) shards[r].assign(buf + size_t(r) * pitch, buf + size_t(r) * pitch + S);
   return UGO_FEC_OK;
 }
 

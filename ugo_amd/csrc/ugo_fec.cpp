@@ -29,6 +29,7 @@ namespace {
 
 constexpr int kStreams = 3;
 constexpr size_t kStageBytes = size_t(64) << 20;  // per host-path staging buffer
+constexpr size_t kZeroCopyEncodeBytes = size_t(4) << 20;  // pinned encode batches up to this run zero-copy
 constexpr uint32_t kMaxItems = 0x7fffffffu;
 
 inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -443,11 +444,11 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
   // device mapping, reading the d survivor rows of each group over PCIe and
   // writing the erased rows back in place -- d rows in per group instead of the
   // staged path's d + p (tools/zerocopy_probe.py: (10,3) 13.3 vs 23.8 ms,
-  // (32,8) 40.6 vs 62.6 ms).  Only the masks and statuses are staged.  The
+  // (32,8) 40.6 vs 62.6 ms).  Only the masks and statuses are staged.  A large
   // encode stays staged: its DMA copies beat zero-copy reads (16.2 vs 18.5 ms).
-  if (recon) {
+  uint8_t* mapped = nullptr;
+  {
     hipPointerAttribute_t at{};
-    uint8_t* mapped = nullptr;
     if (hipPointerGetAttributes(&at, shards) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer) {
       mapped = static_cast<uint8_t*>(at.devicePointer);
       if (at.hostPointer && at.hostPointer != at.devicePointer)
@@ -457,7 +458,17 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
     } else {
       (void)hipGetLastError();  // pageable: clear the sticky lookup error
     }
-    if (mapped) return host_reconstruct_mapped(c, mapped, present, groups, S, pitch, flags, status);
+  }
+  if (recon && mapped) return host_reconstruct_mapped(c, mapped, present, groups, S, pitch, flags, status);
+  // Encode of a small pinned batch (the per-group calls of the drop-in
+  // reedsolomon::Encoder, calcECC): zero-copy too -- one launch reading the data
+  // rows and writing the parity rows through the mapping, one synchronize --
+  // instead of the three-copy pipeline, whose DMA only wins on large batches.
+  if (!recon && mapped && groups * gbytes <= kZeroCopyEncodeBytes) {
+    hipStream_t s = c->streams[0];
+    st = encode_dev(c, mapped, groups, S, interleaved(c, pitch), s);
+    if (st) return st;
+    return hip_status(hipStreamSynchronize(s));
   }
   size_t chunk = 0;
   for (size_t g0 = 0; g0 < groups; g0 += per, ++chunk) {
