@@ -333,6 +333,19 @@ def cpu_baseline(args, d, p, S, n):
         c0 = [sample(1024, 1) for _ in range(threads)]
         v_all, n_all, t_all = leg(c0, 1, args.cpu_baseline_seconds)
         v_one, n_one, t_one = leg(c0[:1], 1, args.cpu_baseline_seconds)
+        # per call on 1 core (the drop-in per-group path's CPU figure):
+        # the C loop makes one Encode / Reconstruct per group, no ctypes in between
+        sh, masks = c0[0]
+        per = {"encode": [], "reconstruct_1loss": []}
+        for _ in range(20):
+            t0 = time.perf_counter()
+            rs_ref.c_encode(d, p, sh, threads=1)
+            t1 = time.perf_counter()
+            rs_ref.c_reconstruct(d, p, sh, masks, threads=1)
+            t2 = time.perf_counter()
+            per["encode"].append((t1 - t0) / sh.shape[0] * 1e6)
+            per["reconstruct_1loss"].append((t2 - t1) / sh.shape[0] * 1e6)
+        per_us = {k: round(sorted(v)[len(v) // 2], 3) for k, v in per.items()}
         c2 = [sample(4096, args.erasures) for _ in range(threads)]
         v_two, n_two, t_two = leg(c2, args.erasures, args.cpu_baseline_seconds / 2)
     finally:
@@ -346,7 +359,7 @@ def cpu_baseline(args, d, p, S, n):
                      f"[{simd}], a C restatement of the klauspost algorithm and its SIMD strategy (the Go "
                      f"reference cannot run: go toolchain {info['go_toolchain']})",
            "single_core": {"value": v_one, "unit": "GiB/s", "cores": 1, "passes": n_one,
-                           "seconds": round(t_one, 2)},
+                           "seconds": round(t_one, 2), "per_group_us": per_us},
            "two_erasure_4096": {"value": v_two, "unit": "GiB/s", "cores": threads, "passes": n_two,
                                 "seconds": round(t_two, 2),
                                 "sample": f"{threads} instances x 4096 groups, encode + {args.erasures}-erasure "

@@ -54,6 +54,25 @@ int ugo_fecconn_input(ugo_fecconn* f, const uint8_t* wire, size_t len, uint32_t*
 int ugo_fecconn_calc_ecc(ugo_fecconn* f, uint8_t* const* bufs, const size_t* lens, int n, int offset,
                          int maxlen);
 
+/* Batched recovery (a GPU extension; ugo has none).  With groups > 0, input
+ * does not Reconstruct each recoverable lossy group (ugo/fec.go:196-217) on
+ * its own: the group's shards[k][:maxlen] are copied into a pinned batch that
+ * is recovered in ONE launch when it holds `groups` groups (inside the
+ * ugo_fecconn_input call that completes it) or on ugo_fecconn_flush.  The
+ * recovered data shards then come back group by group in completion order,
+ * each group's in index order -- the concatenation of what per-call input
+ * returns, delayed.  The rx queue, buffer pool, dedupe, expiry and rxlimit
+ * trim are unchanged.  In this mode ugo_fecconn_input and ugo_fecconn_flush
+ * need out_cap >= groups * d * UGO_FEC_MAX_PACKET (checked before anything
+ * is consumed).  groups = 0 restores per-call recovery (the default).  Both
+ * calls first flush what is pending into out (same capacity rule, the old
+ * batch size's).  UGO_FEC_ERR_INVALID_ARG for groups < 0 or d+p > 64. */
+int ugo_fecconn_set_batch(ugo_fecconn* f, int groups, uint8_t* out, size_t out_cap, int* nrec,
+                          size_t* rec_len);
+int ugo_fecconn_flush(ugo_fecconn* f, uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len);
+/* Lossy groups staged and not yet recovered. */
+int ugo_fecconn_pending(const ugo_fecconn* f, size_t* groups);
+
 /* len(fec.rx): packets held in the ordered receive queue. */
 int ugo_fecconn_rx_len(const ugo_fecconn* f, size_t* len);
 

@@ -142,3 +142,68 @@ def test_paws_wrap_on_device_object(gpu):
     b = bytearray(16)
     f.markFEC(b)
     assert f.next == 0 and b[4:6] == b"\xf2\x00"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 4, 7])
+def test_batched_recovery_is_per_call_recovery_delayed(gpu, batch):
+    """set_batch(n): recoverable lossy groups are staged and recovered n per
+    launch.  Every step's (seqid, flag) and len(rx) equal the reference
+    restatement's; the recovered shards, concatenated over the run and the
+    final flush, equal the per-call sequence byte for byte, and what has come
+    back at any step is a prefix of it."""
+    rng = np.random.default_rng(20 + batch)
+    now = [2_000_000]
+    clock = lambda: now[0]  # noqa: E731
+    tx = fec_ref.FEC.new(RXLIMIT, D, P, clock)
+    pk, _ = _tx_stream(tx, 60, np.random.default_rng(batch), False)
+    wire = _channel(pk, rng, drop=0.15, dup=0.05, junk=0.02)
+    rx_b = fec.FecConn(RXLIMIT, D, P)
+    rx_b.set_clock(clock)
+    assert rx_b.set_batch(batch) is None
+    rx_o = fec_ref.FEC.new(RXLIMIT, D, P, clock)
+    got, want = [], []
+    for i, pkt in enumerate(wire):
+        now[0] += int(rng.integers(0, 40))
+        if i == len(wire) // 2:
+            now[0] += fec_ref.fecExpire + 1
+        sb, fb, rb = rx_b.input(pkt)
+        so, fo, ro = fec_ref.handle(rx_o, pkt)
+        assert (sb, fb) == (so, fo)
+        assert rx_b.rx_len() == len(rx_o.rx), f"step {i}: len(rx)"
+        assert rx_b.pending() < batch
+        got += [bytes(x) for x in rb or []]
+        want += [bytes(x) for x in ro or []]
+        assert got == want[:len(got)], f"step {i}: recovered shards out of order or different"
+    pending = rx_b.pending()
+    got += [bytes(x) for x in rx_b.flush() or []]
+    assert rx_b.pending() == 0
+    assert got == want and len(want) > 0
+    if batch > 1:
+        assert pending > 0 or len(want) % batch == 0
+
+
+@pytest.mark.gpu
+def test_set_batch_flushes_pending_and_rejects_bad_sizes(gpu):
+    rng = np.random.default_rng(31)
+    tx = fec_ref.FEC.new(RXLIMIT, D, P, clock=lambda: 0)
+    pk, _ = _tx_stream(tx, 6, np.random.default_rng(31), True)
+    rx_o = fec_ref.FEC.new(RXLIMIT, D, P, clock=lambda: 0)
+    rx_b = fec.FecConn(RXLIMIT, D, P)
+    rx_b.set_clock(lambda: 0)
+    rx_b.set_batch(64)
+    want = []
+    for g in range(6):  # drop data shard g % D of every group: 6 lossy groups
+        for k, pkt in enumerate(pk[g * N:(g + 1) * N]):
+            if k == g % D:
+                continue
+            _, _, rb = rx_b.input(pkt)
+            assert rb is None, "nothing comes back before the batch is full"
+            want += [bytes(x) for x in fec_ref.handle(rx_o, pkt)[2] or []]
+    assert rx_b.pending() == 6 and len(want) == 6
+    with pytest.raises(fec.FecError):
+        rx_b.set_batch(-1)
+    assert rx_b.pending() == 6, "a refused set_batch consumes nothing"
+    got = rx_b.set_batch(0)  # back to per call: the pending groups come back first
+    assert [bytes(x) for x in got] == want and rx_b.pending() == 0
+    del rng

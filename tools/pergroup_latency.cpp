@@ -1,0 +1,163 @@
+// pergroup_latency.cpp -- per-call cost of the drop-in per-group path (the
+// "unchanged signatures" route: ugo calls Encode once per group from calcECC,
+// ugo/fec.go:238, and Reconstruct once per lossy group from input, :202, via
+// Conn.handlePacket ugo/conn.go:392-400), measured through the C-ABI only
+// (include/ugo_fec.h, include/ugo_fec_conn.h), on the GPU box.
+//
+//   calc_ecc        ugo_fecconn_calc_ecc, 13 x 1476-B buffers, window [6, 1476)
+//   encode_host_g1  ugo_fec_encode_host, one pinned group (10+3) x 1470
+//   input_lossless  the 13 ugo_fecconn_input calls of a group with no loss
+//   input_lossy     the 12 ugo_fecconn_input calls of a group missing one data
+//                   shard (the 11th triggers Reconstruct on the GPU)
+//   input_batch_B   the same lossy stream with ugo_fecconn_set_batch(B):
+//                   one launch per B lossy groups, flush included
+//
+// Prints one JSON line per case: median / p10 / p90 microseconds per group
+// (per call for calc_ecc and encode_host_g1) over `reps` repetitions.
+// Build: make -C tools pergroup_latency (links ugo_amd/libugofec.so).
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../include/ugo_fec.h"
+#include "../include/ugo_fec_conn.h"
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+constexpr int D = 10, P = 3, N = 13, RXLIMIT = 128;
+constexpr size_t PKT = UGO_FEC_MAX_PACKET;
+
+double us_since(clk::time_point t0) {
+  return std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+}
+
+void report(const char* name, std::vector<double> v, const char* unit, double extra = -1.0) {
+  std::sort(v.begin(), v.end());
+  const auto q = [&](double f) { return v[std::min(v.size() - 1, static_cast<size_t>(f * v.size()))]; };
+  std::printf("{\"case\": \"%s\", \"median_us\": %.3f, \"p10_us\": %.3f, \"p90_us\": %.3f, \"unit\": \"%s\", \"reps\": %zu",
+              name, q(0.5), q(0.1), q(0.9), unit, v.size());
+  if (extra >= 0) std::printf(", \"groups_per_rep\": %.0f", extra);
+  std::printf("}\n");
+  std::fflush(stdout);
+}
+
+void check(int st, const char* what) {
+  if (st != UGO_FEC_OK) {
+    std::fprintf(stderr, "%s: %s\n", what, ugo_fec_strerror(st));
+    std::exit(1);
+  }
+}
+
+// Wire packets of `groups` groups starting at seqid base; shard `drop` of
+// every group is left out (drop < 0: none).
+std::vector<std::vector<uint8_t>> stream(uint32_t base, int groups, int drop, std::mt19937& rng) {
+  std::vector<std::vector<uint8_t>> out;
+  for (int g = 0; g < groups; ++g)
+    for (int k = 0; k < N; ++k) {
+      if (k == drop) continue;
+      std::vector<uint8_t> w(PKT);
+      const uint32_t seq = base + static_cast<uint32_t>(g * N + k);
+      std::memcpy(w.data(), &seq, 4);
+      const uint16_t flag = k < D ? UGO_FEC_TYPE_DATA : UGO_FEC_TYPE_FEC;
+      std::memcpy(w.data() + 4, &flag, 2);
+      for (size_t i = 6; i < PKT; ++i) w[i] = static_cast<uint8_t>(rng());
+      out.push_back(std::move(w));
+    }
+  return out;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? std::atoi(argv[1]) : 2000;
+  std::mt19937 rng(0x5EED);
+
+  // calcECC per call
+  {
+    ugo_fecconn* f = nullptr;
+    check(ugo_fecconn_new(RXLIMIT, D, P, 0, &f), "new");
+    std::vector<std::vector<uint8_t>> bufs(N, std::vector<uint8_t>(PKT));
+    for (auto& b : bufs)
+      for (auto& x : b) x = static_cast<uint8_t>(rng());
+    std::vector<uint8_t*> ptrs(N);
+    std::vector<size_t> lens(N, PKT);
+    for (int k = 0; k < N; ++k) ptrs[k] = bufs[k].data();
+    for (int i = 0; i < 200; ++i) check(ugo_fecconn_calc_ecc(f, ptrs.data(), lens.data(), N, 6, PKT), "calc_ecc");
+    std::vector<double> t;
+    for (int i = 0; i < reps; ++i) {
+      const auto t0 = clk::now();
+      check(ugo_fecconn_calc_ecc(f, ptrs.data(), lens.data(), N, 6, PKT), "calc_ecc");
+      t.push_back(us_since(t0));
+    }
+    report("calc_ecc", t, "us per call (one group)");
+    ugo_fecconn_free(f);
+  }
+
+  // Encoder.Encode at G = 1 on a pinned group
+  {
+    ugo_fec* ctx = nullptr;
+    check(ugo_fec_create(0, D, P, &ctx), "create");
+    void* p = nullptr;
+    const size_t S = PKT - 6, pitch = (S + 15) / 16 * 16;
+    check(ugo_fec_host_alloc(N * pitch, &p), "host_alloc");
+    auto* g = static_cast<uint8_t*>(p);
+    for (size_t i = 0; i < N * pitch; ++i) g[i] = static_cast<uint8_t>(rng());
+    for (int i = 0; i < 200; ++i) check(ugo_fec_encode_host(ctx, g, 1, S, pitch), "encode_host");
+    std::vector<double> t;
+    for (int i = 0; i < reps; ++i) {
+      const auto t0 = clk::now();
+      check(ugo_fec_encode_host(ctx, g, 1, S, pitch), "encode_host");
+      t.push_back(us_since(t0));
+    }
+    report("encode_host_g1", t, "us per call (one group)");
+    ugo_fec_host_free(p);
+    ugo_fec_destroy(ctx);
+  }
+
+  // input: lossless / lossy per call / lossy batched
+  std::vector<uint8_t> out(size_t(4096) * D * PKT);
+  auto run = [&](const char* name, int drop, int batch) {
+    const int gpr = std::max(64, batch);  // groups per repetition
+    const int nrep = std::max(10, reps / gpr);
+    ugo_fecconn* f = nullptr;
+    check(ugo_fecconn_new(RXLIMIT, D, P, 0, &f), "new");
+    int nrec = 0;
+    size_t rl = 0;
+    check(ugo_fecconn_set_batch(f, batch, out.data(), out.size(), &nrec, &rl), "set_batch");
+    uint32_t base = 0;
+    std::vector<double> t;
+    long recovered = 0;
+    for (int r = -3; r < nrep; ++r) {  // 3 untimed repetitions
+      const auto pk = stream(base, gpr, drop, rng);
+      base += static_cast<uint32_t>(gpr * N);
+      const auto t0 = clk::now();
+      for (const auto& w : pk) {
+        uint32_t seq;
+        uint16_t flag;
+        check(ugo_fecconn_input(f, w.data(), w.size(), &seq, &flag, out.data(), out.size(), &nrec, &rl), "input");
+        recovered += nrec;
+      }
+      check(ugo_fecconn_flush(f, out.data(), out.size(), &nrec, &rl), "flush");
+      recovered += nrec;
+      if (r >= 0) t.push_back(us_since(t0) / gpr);
+    }
+    const long want = drop >= 0 && drop < D ? static_cast<long>(nrep + 3) * gpr : 0;
+    if (recovered != want) {
+      std::fprintf(stderr, "%s: recovered %ld shards, expected %ld\n", name, recovered, want);
+      std::exit(1);
+    }
+    report(name, t, "us per group (all its input calls)", gpr);
+    ugo_fecconn_free(f);
+  };
+  run("input_lossless", -1, 0);
+  run("input_lossy", 3, 0);
+  run("input_batch_16", 3, 16);
+  run("input_batch_64", 3, 64);
+  run("input_batch_256", 3, 256);
+  return 0;
+}

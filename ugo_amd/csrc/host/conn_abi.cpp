@@ -10,6 +10,33 @@ struct ugo_fecconn {
   std::unique_ptr<ugo::FEC> fec;
 };
 
+namespace {
+
+// Recovered shards out at a UGO_FEC_MAX_PACKET stride; every shard of one
+// call has the same length (the pool's buffers are all maxPacketSize long).
+int emit(const std::vector<ugo::Bytes>& rec, uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len) {
+  if (rec.empty()) return UGO_FEC_OK;
+  const size_t L = rec[0].size();
+  if (!out || out_cap < rec.size() * ugo::maxPacketSize || L > ugo::maxPacketSize) return UGO_FEC_ERR_INVALID_ARG;
+  for (size_t i = 0; i < rec.size(); ++i) {
+    if (rec[i].size() != L) return UGO_FEC_ERR_INVALID_ARG;
+    std::memcpy(out + i * ugo::maxPacketSize, rec[i].data(), L);
+  }
+  if (nrec) *nrec = static_cast<int>(rec.size());
+  if (rec_len) *rec_len = L;
+  return UGO_FEC_OK;
+}
+
+// In batch mode one call can return a whole batch: the caller's buffer must
+// hold it before anything is consumed.
+bool batch_cap_ok(const ugo_fecconn* f, const uint8_t* out, size_t out_cap) {
+  const size_t cap = static_cast<size_t>(f->fec->batch());
+  if (cap == 0) return true;
+  return out && out_cap >= cap * static_cast<size_t>(f->fec->dataShards()) * ugo::maxPacketSize;
+}
+
+}  // namespace
+
 extern "C" {
 
 int ugo_fecconn_new(int rxlimit, int d, int p, int device, ugo_fecconn** out) {
@@ -72,6 +99,7 @@ int ugo_fecconn_input(ugo_fecconn* f, const uint8_t* wire, size_t len, uint32_t*
   if (!f || !wire || len < ugo::fecHeaderSize) return UGO_FEC_ERR_INVALID_ARG;
   if (nrec) *nrec = 0;
   if (rec_len) *rec_len = 0;
+  if (!batch_cap_ok(f, out, out_cap)) return UGO_FEC_ERR_INVALID_ARG;
   ugo::fecPacket pkt = f->fec->decode(wire, len);
   if (seqid) *seqid = pkt.seqid;
   if (flag) *flag = pkt.flag;
@@ -82,14 +110,35 @@ int ugo_fecconn_input(ugo_fecconn* f, const uint8_t* wire, size_t len, uint32_t*
     return UGO_FEC_OK;
   }
   std::vector<ugo::Bytes> rec = f->fec->input(pkt);
-  if (!rec.empty()) {
-    const size_t L = rec[0].size();
-    if (!out || out_cap < rec.size() * ugo::maxPacketSize || L > ugo::maxPacketSize) return UGO_FEC_ERR_INVALID_ARG;
-    for (size_t i = 0; i < rec.size(); ++i) std::memcpy(out + i * ugo::maxPacketSize, rec[i].data(), L);
-    if (nrec) *nrec = static_cast<int>(rec.size());
-    if (rec_len) *rec_len = L;
-  }
+  const int st = emit(rec, out, out_cap, nrec, rec_len);
+  if (st) return st;
   return f->fec->lastError() == UGO_FEC_ERR_HIP ? UGO_FEC_ERR_HIP : UGO_FEC_OK;
+}
+
+int ugo_fecconn_set_batch(ugo_fecconn* f, int groups, uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len) {
+  if (nrec) *nrec = 0;
+  if (rec_len) *rec_len = 0;
+  if (!f || groups < 0 || (groups > 0 && f->fec->dataShards() + f->fec->parityShards() > 64))
+    return UGO_FEC_ERR_INVALID_ARG;
+  if (!batch_cap_ok(f, out, out_cap)) return UGO_FEC_ERR_INVALID_ARG;
+  std::vector<ugo::Bytes> rec = f->fec->setBatch(groups);
+  return emit(rec, out, out_cap, nrec, rec_len);
+}
+
+int ugo_fecconn_flush(ugo_fecconn* f, uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len) {
+  if (nrec) *nrec = 0;
+  if (rec_len) *rec_len = 0;
+  if (!f || !batch_cap_ok(f, out, out_cap)) return UGO_FEC_ERR_INVALID_ARG;
+  std::vector<ugo::Bytes> rec = f->fec->flush();
+  const int st = emit(rec, out, out_cap, nrec, rec_len);
+  if (st) return st;
+  return f->fec->lastError() == UGO_FEC_ERR_HIP ? UGO_FEC_ERR_HIP : UGO_FEC_OK;
+}
+
+int ugo_fecconn_pending(const ugo_fecconn* f, size_t* groups) {
+  if (!f || !groups) return UGO_FEC_ERR_INVALID_ARG;
+  *groups = f->fec->pending();
+  return UGO_FEC_OK;
 }
 
 int ugo_fecconn_calc_ecc(ugo_fecconn* f, uint8_t* const* bufs, const size_t* lens, int n, int offset, int maxlen) {

@@ -123,13 +123,11 @@ std::vector<Bytes> FEC::input(fecPacket pkt) {  // :107-226
     int numshard = 0, numDataShard = 0, first = -1;
     size_t maxlen = 0;
     std::vector<Bytes*> shards(shardSize_, nullptr);
-    std::vector<bool> shardsflag(shardSize_, false);
     for (int i = searchBegin; i <= searchEnd; ++i) {  // :170-188
       const uint32_t seqid = rx_[i].seqid;
       if (seqid > shardEnd) break;
       if (seqid >= shardBegin) {
         shards[seqid % ss] = rx_[i].data;
-        shardsflag[seqid % ss] = true;
         numshard++;
         if (rx_[i].flag == typeData) numDataShard++;
         if (numshard == 1) first = i;
@@ -140,15 +138,7 @@ std::vector<Bytes> FEC::input(fecPacket pkt) {  // :107-226
       for (int i = first; i < first + numshard; ++i) poolPut(rx_[i].data);
       rx_.erase(rx_.begin() + first, rx_.begin() + first + numshard);
     } else if (numshard >= dataShards_) {  // recoverable :196-217
-      std::vector<Bytes> rs(shardSize_);
-      for (int k = 0; k < shardSize_; ++k)
-        if (shards[k]) rs[k].assign(shards[k]->begin(), shards[k]->begin() + maxlen);  // shards[k][:maxlen]
-      const int err = enc_->Reconstruct(rs);  // :202 -> GPU
-      lastError_ = err;
-      if (err == UGO_FEC_OK) {
-        for (int k = 0; k < dataShards_; ++k)
-          if (!shardsflag[k]) recovered.push_back(std::move(rs[k]));
-      }  // else: logged and swallowed upstream (:208-210)
+      recoverGroup(shards, maxlen, recovered);
       for (int i = first; i < first + numshard; ++i) poolPut(rx_[i].data);
       rx_.erase(rx_.begin() + first, rx_.begin() + first + numshard);
     }
@@ -158,6 +148,97 @@ std::vector<Bytes> FEC::input(fecPacket pkt) {  // :107-226
     rx_.erase(rx_.begin());
   }
   return recovered;
+}
+
+// The recoverable branch of input (ugo/fec.go:196-217).  Per call: reslice
+// to maxlen, Reconstruct (:202, on the GPU), append the erased data shards in
+// index order (:203-207).  Batched: the same bytes are staged and recovered
+// with the rest of the batch (flushInto), so the result is identical.
+void FEC::recoverGroup(const std::vector<Bytes*>& shards, size_t maxlen, std::vector<Bytes>& out) {
+  if (batchCap_ > 0) {
+    const size_t n = static_cast<size_t>(shardSize_);
+    const size_t pitch = (maxlen + 15) / 16 * 16;
+    if (!pendMask_.empty() && maxlen != batchS_) flushInto(out);  // one shard size per batch
+    const size_t need = static_cast<size_t>(batchCap_) * n * pitch;
+    if (need > batchBytes_) {  // pendMask_ is empty here
+      if (batchBuf_) ugo_fec_host_free(batchBuf_);
+      batchBuf_ = nullptr;
+      batchBytes_ = 0;
+      void* p = nullptr;
+      if (ugo_fec_host_alloc(need, &p) == UGO_FEC_OK) {
+        batchBuf_ = static_cast<uint8_t*>(p);
+        batchBytes_ = need;
+      }
+    }
+    if (batchBuf_) {
+      batchS_ = maxlen;
+      batchPitch_ = pitch;
+      uint8_t* grp = batchBuf_ + pendMask_.size() * n * pitch;
+      uint64_t mask = 0;
+      for (size_t k = 0; k < n; ++k)
+        if (shards[k]) {
+          std::memcpy(grp + k * pitch, shards[k]->data(), maxlen);  // shards[k][:maxlen]
+          mask |= 1ull << k;
+        }
+      pendMask_.push_back(mask);
+      if (pendMask_.size() == static_cast<size_t>(batchCap_)) flushInto(out);
+      return;
+    }
+    lastError_ = UGO_FEC_ERR_HIP;  // no pinned batch: recover this group per call
+  }
+  std::vector<Bytes> rs(shardSize_);
+  for (int k = 0; k < shardSize_; ++k)
+    if (shards[k]) rs[k].assign(shards[k]->begin(), shards[k]->begin() + maxlen);  // shards[k][:maxlen]
+  const int err = enc_->Reconstruct(rs);  // :202 -> GPU
+  lastError_ = err;
+  if (err == UGO_FEC_OK) {
+    for (int k = 0; k < dataShards_; ++k)
+      if (!shards[k]) out.push_back(std::move(rs[k]));
+  }  // else: logged and swallowed upstream (:208-210)
+}
+
+// One launch over the pending groups (data rows only: input returns data
+// shards, :203-207).  A group whose status is not OK yields nothing, as a
+// failing per-call Reconstruct does.
+void FEC::flushInto(std::vector<Bytes>& out) {
+  const size_t G = pendMask_.size();
+  if (G == 0) return;
+  const size_t n = static_cast<size_t>(shardSize_);
+  std::vector<int8_t> st(G, 0);
+  const int err = enc_->ReconstructBatch(batchBuf_, pendMask_.data(), G, batchS_, batchPitch_,
+                                         UGO_FEC_RECONSTRUCT_DATA_ONLY, st.data());
+  lastError_ = err;
+  if (err != UGO_FEC_ERR_HIP) {
+    for (size_t g = 0; g < G; ++g) {
+      if (st[g] != 0) continue;
+      const uint8_t* grp = batchBuf_ + g * n * batchPitch_;
+      for (int k = 0; k < dataShards_; ++k)
+        if (!((pendMask_[g] >> k) & 1ull)) out.emplace_back(grp + k * batchPitch_, grp + k * batchPitch_ + batchS_);
+    }
+  }
+  pendMask_.clear();
+}
+
+std::vector<Bytes> FEC::flush() {
+  std::vector<Bytes> out;
+  flushInto(out);
+  return out;
+}
+
+std::vector<Bytes> FEC::setBatch(int groups) {
+  std::vector<Bytes> out;
+  if (groups < 0 || (groups > 0 && shardSize_ > 64)) {
+    lastError_ = UGO_FEC_ERR_INVALID_ARG;
+    return out;
+  }
+  flushInto(out);
+  batchCap_ = groups;
+  lastError_ = UGO_FEC_OK;
+  return out;
+}
+
+FEC::~FEC() {
+  if (batchBuf_) ugo_fec_host_free(batchBuf_);
 }
 
 std::vector<Bytes*> FEC::calcECC(std::vector<Bytes>& data, int offset, int maxlen) {  // :228-243

@@ -51,6 +51,23 @@ class FEC {
   // on error (length mismatch, window outside a buffer, Encode error).
   std::vector<Bytes*> calcECC(std::vector<Bytes>& data, int offset, int maxlen);
 
+  // Batched recovery (a GPU extension; ugo has none).  With setBatch(n), n > 0,
+  // input() does not Reconstruct a recoverable lossy group itself
+  // (ugo/fec.go:196-217): it copies the group's shards[k][:maxlen] into a
+  // pinned group-major batch and recovers the whole batch in ONE launch when
+  // it holds n groups (inside the input() call that completes it) or on
+  // flush().  Recovered data shards come back group by group in completion
+  // order, each group's in index order: exactly the concatenation of what
+  // per-call input() returns, only later.  The rx queue, buffer pool, dedupe,
+  // expiry and rxlimit trim do not change.  setBatch(0) restores the
+  // reference's per-call behaviour.  Both return the shards of any groups
+  // still pending (they are flushed first).  d+p must be <= 64.
+  std::vector<Bytes> setBatch(int groups);
+  std::vector<Bytes> flush();
+  int batch() const { return batchCap_; }
+  size_t pending() const { return pendMask_.size(); }
+  ~FEC();
+
   // test / inspection hooks
   void setClock(std::function<uint32_t()> clock) { clock_ = std::move(clock); }
   size_t rxLen() const { return rx_.size(); }
@@ -68,6 +85,8 @@ class FEC {
   FEC() = default;
   Bytes* poolGet();
   void poolPut(Bytes* b);
+  void recoverGroup(const std::vector<Bytes*>& shards, size_t maxlen, std::vector<Bytes>& out);
+  void flushInto(std::vector<Bytes>& out);
 
   std::vector<fecPacket> rx_;  // ordered receive queue
   int rxlimit_ = 0;
@@ -82,6 +101,12 @@ class FEC {
   std::vector<Bytes*> poolFree_;
   std::function<uint32_t()> clock_;
   int lastError_ = 0;
+  // batched recovery: pinned [batchCap_][d+p][batchPitch_] and one presence
+  // mask per pending group
+  int batchCap_ = 0;
+  size_t batchS_ = 0, batchPitch_ = 0, batchBytes_ = 0;
+  uint8_t* batchBuf_ = nullptr;
+  std::vector<uint64_t> pendMask_;
 };
 
 }  // namespace ugo

@@ -91,6 +91,11 @@ int Encoder::reconstruct(std::vector<Bytes>& shards, unsigned flags) {
   return UGO_FEC_OK;
 }
 
+int Encoder::ReconstructBatch(uint8_t* batch, const uint64_t* present, size_t groups, size_t S, size_t pitch,
+                              unsigned flags, int8_t* status) {
+  return ugo_fec_reconstruct_host(ctx_, batch, present, groups, S, pitch, flags, status);
+}
+
 int Encoder::Reconstruct(std::vector<Bytes>& shards) { return reconstruct(shards, 0); }
 int Encoder::ReconstructData(std::vector<Bytes>& shards) {
   return reconstruct(shards, UGO_FEC_RECONSTRUCT_DATA_ONLY);

@@ -32,6 +32,11 @@ class Encoder {
   // Reconstruct: every empty shard is rebuilt (data and parity).
   int Reconstruct(std::vector<Bytes>& shards);
   int ReconstructData(std::vector<Bytes>& shards);
+  // Reconstruct every group of a pinned group-major batch [G][d+p][pitch]
+  // (ugo_fec_reconstruct_host): the batched form of G Reconstruct calls,
+  // one launch.  status (G entries, nullable) gets each group's status.
+  int ReconstructBatch(uint8_t* batch, const uint64_t* present, size_t groups, size_t shard_size,
+                       size_t pitch, unsigned flags, int8_t* status);
 
   int DataShards() const { return d_; }
   int ParityShards() const { return p_; }

@@ -463,6 +463,9 @@ def _bind_conn(lib):
                                       vp, sz, ctypes.POINTER(i), ctypes.POINTER(sz)]
     lib.ugo_fecconn_calc_ecc.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(sz), i, i, i]
     lib.ugo_fecconn_rx_len.argtypes = [vp, ctypes.POINTER(sz)]
+    lib.ugo_fecconn_set_batch.argtypes = [vp, i, vp, sz, ctypes.POINTER(i), ctypes.POINTER(sz)]
+    lib.ugo_fecconn_flush.argtypes = [vp, vp, sz, ctypes.POINTER(i), ctypes.POINTER(sz)]
+    lib.ugo_fecconn_pending.argtypes = [vp, ctypes.POINTER(sz)]
     lib._conn_bound = True
     return lib
 
@@ -514,6 +517,13 @@ class FecConn:
     def next(self, v: int):
         _raise(self._lib.ugo_fecconn_set_next(self._h, v))
 
+    def _recovered(self, nrec, rlen):
+        if not nrec.value:
+            return None
+        raw = bytes(self._out)
+        return [bytearray(raw[i * UGO_FEC_MAX_PACKET: i * UGO_FEC_MAX_PACKET + rlen.value])
+                for i in range(nrec.value)]
+
     def input(self, wire: bytes):
         """decode + input (ugo/conn.go:394-396): returns (seqid, flag, recovered list | None)."""
         seq, flag = ctypes.c_uint32(), ctypes.c_uint16()
@@ -522,12 +532,37 @@ class FecConn:
         _raise(self._lib.ugo_fecconn_input(self._h, ctypes.addressof(w), len(wire), ctypes.byref(seq),
                                            ctypes.byref(flag), ctypes.addressof(self._out), len(self._out),
                                            ctypes.byref(nrec), ctypes.byref(rlen)))
-        rec = None
-        if nrec.value:
-            raw = bytes(self._out)
-            rec = [bytearray(raw[i * UGO_FEC_MAX_PACKET: i * UGO_FEC_MAX_PACKET + rlen.value])
-                   for i in range(nrec.value)]
-        return seq.value, flag.value, rec
+        return seq.value, flag.value, self._recovered(nrec, rlen)
+
+    def set_batch(self, groups: int):
+        """Batched recovery (include/ugo_fec_conn.h): recoverable lossy groups are
+        recovered `groups` at a time in one launch; 0 = per call.  Returns the
+        recovered shards of groups that were pending (list | None)."""
+        nrec, rlen = ctypes.c_int(), ctypes.c_size_t()
+        need = max(groups, 1) * self.dataShards * UGO_FEC_MAX_PACKET
+        new_out = (ctypes.c_uint8 * max(need, len(self._out)))()
+        old_out, self._out = self._out, new_out
+        try:
+            _raise(self._lib.ugo_fecconn_set_batch(self._h, groups, ctypes.addressof(self._out), len(self._out),
+                                                   ctypes.byref(nrec), ctypes.byref(rlen)))
+        except Exception:
+            self._out = old_out
+            raise
+        rec = self._recovered(nrec, rlen)
+        self._out = (ctypes.c_uint8 * need)()
+        return rec
+
+    def flush(self):
+        """Recover every pending group now (list | None)."""
+        nrec, rlen = ctypes.c_int(), ctypes.c_size_t()
+        _raise(self._lib.ugo_fecconn_flush(self._h, ctypes.addressof(self._out), len(self._out),
+                                           ctypes.byref(nrec), ctypes.byref(rlen)))
+        return self._recovered(nrec, rlen)
+
+    def pending(self) -> int:
+        v = ctypes.c_size_t()
+        _raise(self._lib.ugo_fecconn_pending(self._h, ctypes.byref(v)))
+        return v.value
 
     def calcECC(self, data: List[bytearray], offset: int, maxlen: int):
         n = len(data)
