@@ -67,8 +67,8 @@ struct ugo_fec {
   uint8_t* d_stage[kStreams] = {};
   uint64_t* d_mask[kStreams] = {};
   int8_t* d_status[kStreams] = {};
-  uint64_t* d_zc_mask = nullptr;  // zero-copy host reconstruct: presence masks / status of the batch
-  int8_t* d_zc_status = nullptr;
+  uint64_t* d_zc_mask = nullptr;  // zero-copy host reconstruct: presence masks / status of the batch,
+  int8_t* d_zc_status = nullptr;   // pinned host memory the kernels read / write through its mapping
   size_t zc_groups = 0;
   size_t stage_groups = 0;  // groups per staging buffer
   size_t stage_pitch = 0;
@@ -160,8 +160,8 @@ void free_ctx(ugo_fec* c) {
   (void)hipFree(c->d_gf);
   (void)hipFree(c->d_encdesc);
   (void)hipFree(c->d_table);
-  (void)hipFree(c->d_zc_mask);
-  (void)hipFree(c->d_zc_status);
+  (void)hipHostFree(c->d_zc_mask);
+  (void)hipHostFree(c->d_zc_status);
   for (int i = 0; i < kStreams; ++i) {
     (void)hipFree(c->d_stage[i]);
     (void)hipFree(c->d_mask[i]);
@@ -399,31 +399,34 @@ int host_reconstruct_mapped(ugo_fec* c, uint8_t* mapped, const uint64_t* present
                             size_t pitch, unsigned flags, int8_t* status) {
   if (!c->streams[0] && hipStreamCreateWithFlags(&c->streams[0], hipStreamNonBlocking) != hipSuccess)
     return UGO_FEC_ERR_HIP;
+  // masks and statuses live in pinned memory too: no copy launches, so a small
+  // batch (the per-group calls, FEC::flush) costs one launch and one sync
   if (c->zc_groups < groups) {
-    (void)hipFree(c->d_zc_mask);
-    (void)hipFree(c->d_zc_status);
+    (void)hipHostFree(c->d_zc_mask);
+    (void)hipHostFree(c->d_zc_status);
     c->d_zc_mask = nullptr;
     c->d_zc_status = nullptr;
     c->zc_groups = 0;
-    if (hipMalloc(&c->d_zc_mask, groups * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
-    if (hipMalloc(&c->d_zc_status, groups) != hipSuccess) return UGO_FEC_ERR_HIP;
-    c->zc_groups = groups;
+    const size_t cap = std::max<size_t>(groups, 256);
+    if (hipHostMalloc(&c->d_zc_mask, cap * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (hipHostMalloc(&c->d_zc_status, cap) != hipSuccess) return UGO_FEC_ERR_HIP;
+    c->zc_groups = cap;
   }
+  uint64_t* dmask = c->d_zc_mask;
+  int8_t* dstatus = c->d_zc_status;
+  if (!device_view(dmask) || !device_view(dstatus)) return UGO_FEC_ERR_HIP;
   hipStream_t s = c->streams[0];
-  std::vector<int8_t> tmp_status;
-  if (!status) {
-    tmp_status.resize(groups);
-    status = tmp_status.data();
-  }
-  if (hipMemcpyAsync(c->d_zc_mask, present, groups * sizeof(uint64_t), hipMemcpyHostToDevice, s) != hipSuccess)
-    return UGO_FEC_ERR_HIP;
-  const int st = reconstruct_dev(c, mapped, c->d_zc_mask, groups, S, interleaved(c, pitch), flags, c->d_zc_status, s);
+  std::memcpy(c->d_zc_mask, present, groups * sizeof(uint64_t));
+  const int st = reconstruct_dev(c, mapped, dmask, groups, S, interleaved(c, pitch), flags, dstatus, s);
   if (st) return st;
-  if (hipMemcpyAsync(status, c->d_zc_status, groups, hipMemcpyDeviceToHost, s) != hipSuccess) return UGO_FEC_ERR_HIP;
   if (hipStreamSynchronize(s) != hipSuccess) return UGO_FEC_ERR_HIP;
-  for (size_t g = 0; g < groups; ++g)
-    if (status[g]) return status[g];
-  return UGO_FEC_OK;
+  int first = UGO_FEC_OK;
+  for (size_t g = 0; g < groups; ++g) {
+    const int8_t v = c->d_zc_status[g];
+    if (status) status[g] = v;
+    if (v && !first) first = v;
+  }
+  return first;
 }
 
 // Host path: chunks of stage_groups groups round-robin over kStreams streams:
