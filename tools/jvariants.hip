@@ -14,6 +14,150 @@
 using namespace ugo;
 using namespace ugo::kern;
 
+// ---------------------------------------------- k_apply_gq (A/B only)
+// Round-2 attempt at fusing k_prepare into the jumbo apply:
+// bit-exact, but 634.6 us against 569.3 us for k_prepare + k_apply_q
+// (jvar_r2h.jsonl).  Kept here, out of the product, as the record.
+constexpr uint32_t kMaxDescBytes = 1024;
+// Group-per-block reconstruct for d + p > 16 (MODE 2) with the descriptor
+// build fused in: block b owns group g0 + b.  The block stages M and the GF
+// tables in LDS, wave 0 builds the group's descriptor there (prep_wave), and
+// after one barrier the block streams the group's chunks exactly as
+// k_apply_q does -- every descriptor word read from LDS and made scalar by
+// readfirstlane, the coefficient tables read as scalar loads.  One launch
+// instead of k_prepare + k_apply_q, no workspace, and no wave ever spans two
+// groups (no per-lane table pick).  A block of W waves covers the group's C
+// chunks in P = ceil(C / 256) passes (W = ceil(C / 64P): 3 waves x 3 passes
+// for the 563 chunks of a 9000-B row, 97.7% of the lanes busy).  Survivor
+// rows are read with buffer loads: a wave-uniform resource per row (SALU
+// address arithmetic) and the lane's chunk offset.
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t* p) {  // LDS word -> SGPR (uniform address)
+  return __builtin_amdgcn_readfirstlane(*p);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint8_t* base, uint64_t off) {
+  const uint64_t a64 = reinterpret_cast<uint64_t>(base) + off;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a64));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a64 >> 32));
+  void* p = reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, 0, 0x7fffffff, 0x00020000);
+}
+
+template <int NT>
+__device__ __forceinline__ V4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, (NT & 1) ? 2 : 0));
+  return V4{{v.x, v.y, v.z, v.w}};
+}
+
+typedef const __attribute__((address_space(4))) uint32_t* ctab_t;
+
+// PREP (A/B only, tools/jvariants.hip): 1 = copy a descriptor k_prepare left
+// in pr.desc instead of building it (isolates the cost of the build).
+template <int EMAX, int NT, int RING = 4, int PREP = 0>
+__global__ __launch_bounds__(256) void k_apply_gq(Batch a, Prep pr) {
+  static_assert(RING == 4, "one coefficient word per input quad");
+  __shared__ PrepShared sh;
+  __shared__ PrepWave s;
+  __shared__ uint32_t sdesc[kMaxDescBytes / 4];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t g = a.g0 + blockIdx.x;
+  const uint32_t d = a.d;
+  if constexpr (PREP == 0) {
+    prep_stage(pr, sh, threadIdx.x, blockDim.x);
+    __syncthreads();
+    if (wave == 0) prep_wave(pr, g, reinterpret_cast<uint8_t*>(sdesc), sh, s, lane);
+  } else {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(pr.desc + (g - pr.g_desc0) * pr.desc_stride);
+    for (uint32_t i = threadIdx.x; i < pr.desc_stride / 4; i += blockDim.x) sdesc[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t hdr = lds_u32(&sdesc[0]);
+  const uint32_t st = (hdr >> 16) & 0xffu;
+  const uint32_t e = st ? 0u : (a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu));
+  const bool wst = a.status != nullptr && threadIdx.x == 0;
+  if (e == 0) {  // block-uniform
+    if (wst) a.status[g] = static_cast<int8_t>(st);
+    return;
+  }
+  // survivors: the first d present rows in index order (the rows prep_wave
+  // lists), popped from the mask with scalar bit scans
+  const uint64_t m64 = pr.present[g] & pr.nmask;
+  const uint32_t mlo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(m64));  // (int -> u32: no sign
+  const uint32_t mhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(m64 >> 32));  //  extension)
+  const uint64_t mask = static_cast<uint64_t>(mhi) << 32 | mlo;
+  const uint8_t* gbase = a.base + g * a.gstride;
+  // The tables are read through the constant address space: this kernel
+  // stores to LDS (the descriptor) and to global memory (status, outputs)
+  // before it reads them, which would make plain global reads per-lane vector
+  // loads; constant reads are scalar loads whatever was stored before (the
+  // tables are never written by any kernel).
+  const ctab_t ctab = (ctab_t)a.mult;
+  const uint32_t cbase = 4 + a.dpad + a.epad;  // byte offset of coefficient row 0 (multiple of 4)
+  const uint8_t* orow = reinterpret_cast<const uint8_t*>(sdesc) + 4 + a.dpad;
+  for (uint32_t c0 = 0; c0 < a.chunks; c0 += blockDim.x) {  // passes (block-uniform)
+    const uint32_t c = c0 + threadIdx.x;
+    const bool live = c < a.chunks;
+    const uint32_t voff = live ? c * 16u : 0u;  // idle lanes load chunk 0 and store nothing
+    uint64_t rem = mask;                         // present rows not yet loaded
+    auto load_next = [&](uint32_t k) -> V4 {
+      if (k >= d) return V4{{0u, 0u, 0u, 0u}};  // uniform: every lane takes the same rows
+      const uint32_t r = static_cast<uint32_t>(__builtin_ctzll(rem));
+      rem &= rem - 1;
+      return bload16<NT>(row_rsrc(gbase, static_cast<uint64_t>(r) * a.rstride), voff);
+    };
+    V4 ring[RING];
+#pragma unroll
+    for (int j = 0; j < RING; ++j) ring[j] = load_next(j);
+    V4 acc[EMAX];
+#pragma unroll
+    for (int i = 0; i < EMAX; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
+    for (uint32_t k0 = 0; k0 < d; k0 += RING) {
+#pragma unroll
+      for (int j = 0; j < RING; j += 2) {
+        const uint32_t k = k0 + j;
+        uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
+        p_sel(ring[j], s0, s1, s2);
+        p_sel(ring[j + 1], r0, r1, r2);
+        ring[j] = load_next(k + RING);
+        ring[j + 1] = load_next(k + RING + 1);
+#pragma unroll
+        for (int i = 0; i < EMAX; ++i) {
+          if (i >= static_cast<int>(e)) continue;
+          const uint32_t cw = lds_u32(&sdesc[(cbase + i * a.dpad + k0) >> 2]);  // inputs k0..k0+3
+          const ctab_t tA = ctab + 8u * ((cw >> (8 * j)) & 0xffu);
+          const ctab_t tB = ctab + 8u * ((cw >> (8 * (j + 1))) & 0xffu);
+          uint32_t t[5], u[5];
+#pragma unroll
+          for (int q = 0; q < 5; ++q) {
+            t[q] = tA[q];
+            u[q] = tB[q];
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            uint32_t y = xor3(acc[i].v[q], perm(t[1], t[0], s0[q]), perm(t[3], t[2], s1[q]));
+            y = xor3(y, perm(0u, t[4], s2[q]), perm(u[1], u[0], r0[q]));
+            acc[i].v[q] = xor3(y, perm(u[3], u[2], r1[q]), perm(0u, u[4], r2[q]));
+          }
+        }
+      }
+    }
+    if (live) {
+      uint8_t* gp = a.base + g * a.gstride + voff;
+      const uint32_t nb = a.S - voff;
+#pragma unroll
+      for (int i = 0; i < EMAX; ++i) {
+        if (i >= static_cast<int>(e)) continue;
+        const uint32_t r = (lds_u32(reinterpret_cast<const uint32_t*>(orow) + (i >> 2)) >> (8 * (i & 3))) & 0xffu;
+        store16<NT>(out_row(a, gp, g, voff, r, i), acc[i], nb);
+      }
+    }
+  }
+  if (wst) a.status[g] = 0;
+}
+
+
+
 int main(int argc, char** argv) {
   const int d = 32, p = 8, n = 40;
   const uint32_t S = 9000, pitch = 9008;
@@ -97,6 +241,18 @@ int main(int argc, char** argv) {
   add(k_apply_q<8, 2, 0, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt0");
   add(k_apply<32, 2, 3>, ar, dec_bytes, "dec masked-horner k_apply nt3 (before)");
   vars.push_back({"k_prepare (8192 groups)", 0.0, [=]() { launch_prepare(pr, G, 0); }, {}});
+  {  // fused descriptor build, one group per block (k_apply_gq, A/B only)
+    const uint32_t passes = (a.chunks + 255) / 256, bs = 64 * ((a.chunks + 64 * passes - 1) / (64 * passes));
+    Batch af = a;
+    af.present = masks;
+    vars.push_back({"dec fused k_apply_gq (production)", dec_bytes, [=]() {
+      hipLaunchKernelGGL((k_apply_gq<8, 3>), dim3(G), dim3(bs), 0, 0, af, pr); }, {}});
+    vars.push_back({"dec fused k_apply_gq, PROBE descriptor copied from k_prepare's workspace", dec_bytes, [=]() {
+      hipLaunchKernelGGL((k_apply_gq<8, 3, 4, 1>), dim3(G), dim3(bs), 0, 0, af, pr); }, {}});
+    vars.push_back({"dec k_prepare + k_apply_q (production before)", dec_bytes, [=]() {
+      launch_prepare(pr, G, 0);
+      hipLaunchKernelGGL((k_apply_q<8, 2, 3, 1, 4>), dim3(grid), dim3(256), 0, 0, ar); }, {}});
+  }
   // encode variants must agree: run const then perm encode over the same data
   auto same_rows = [&](const std::vector<uint8_t>& x, const std::vector<uint8_t>& y) {  // bytes [0, S) only
     for (uint64_t r = 0; r < uint64_t(n); ++r)

@@ -631,20 +631,54 @@ __device__ __forceinline__ uint8_t lmul(const uint8_t* lg, const uint8_t* ex, ui
 //   coef[pos(P_m)] = M[r][P_m] + sum_l M[r][E_l] Dinv[E_l][pos],  coef[pos(J_i)] = sum_l M[r][E_l] Binv[l][i]
 // The same linear map as the full Gauss-Jordan of klauspost's Reconstruct
 // (exact arithmetic), at e_d^3 + e_d^2 d instead of d^3 work.
-__global__ __launch_bounds__(64) void k_prepare(Prep a) {
-  __shared__ uint8_t ex[512];
-  __shared__ uint8_t lg[256];
-  __shared__ uint8_t Ba[32 * 64];  // [B | I], e_d <= min(d, p) <= 32 since d + p <= 64
-  __shared__ uint8_t DE[32 * 64];  // Dinv rows of the erased data rows, over survivor positions
-  __shared__ uint8_t fcol[32];
-  __shared__ uint8_t surv[64], outr[64], Pl[64], El[64], Jl[64];
-  const uint32_t lane = threadIdx.x;
-  const uint64_t g = a.g0 + blockIdx.x;
+//
+// prep_wave is the body: ONE wave builds group g's descriptor at `desc`
+// (global workspace for k_prepare, LDS for k_apply_gq) with its scratch in
+// `s`.  It synchronises only its own lanes (wsync: a wave's LDS operations
+// complete in order, so a code-motion barrier is enough), so one wave of a
+// larger block can run it while the others do something else.
+struct PrepShared {     // per block: staged once, read by every wave
+  uint8_t ex[512];
+  uint8_t lg[256];
+  uint8_t M[64 * 64];   // the (d+p) x d encoding matrix
+};
+struct PrepWave {       // per wave (per group being built)
+  uint8_t Ba[32 * 64];  // [B | I], e_d <= min(d, p) <= 32 since d + p <= 64
+  uint8_t DE[32 * 64];  // Dinv rows of the erased data rows, over survivor positions
+  uint8_t fcol[32];
+  uint8_t surv[64], outr[64], Pl[64], El[64], Jl[64];
+};
+
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Stage the GF tables and M into LDS with 16-B loads by threads [0, nthr):
+// every later read of the descriptor build is an LDS read (global reads
+// inside its dependent loops cost a full memory latency each under load).
+// The caller synchronises before prep_wave reads them.
+__device__ __forceinline__ void prep_stage(const Prep& a, PrepShared& s, uint32_t tid, uint32_t nthr) {
+  const uint32_t mb = a.n * a.d, m16 = mb / 16;
+  for (uint32_t i = tid; i < 32 + 16 + m16; i += nthr) {
+    const u32x4* src = i < 32 ? reinterpret_cast<const u32x4*>(a.gf_exp) + i
+                     : i < 48 ? reinterpret_cast<const u32x4*>(a.gf_log) + (i - 32)
+                              : reinterpret_cast<const u32x4*>(a.M) + (i - 48);
+    u32x4* dst = i < 32 ? reinterpret_cast<u32x4*>(s.ex) + i
+               : i < 48 ? reinterpret_cast<u32x4*>(s.lg) + (i - 32)
+                        : reinterpret_cast<u32x4*>(s.M) + (i - 48);
+    *dst = *src;
+  }
+  for (uint32_t i = m16 * 16 + tid; i < mb; i += nthr) s.M[i] = a.M[i];
+}
+
+template <typename DescPtr>
+__device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr desc, const PrepShared& sh, PrepWave& s,
+                                          uint32_t lane) {
   const uint32_t d = a.d, n = a.n;
-  for (uint32_t i = lane; i < 512; i += 64) ex[i] = a.gf_exp[i];
-  for (uint32_t i = lane; i < 256; i += 64) lg[i] = a.gf_log[i];
+  const uint8_t* M = sh.M;
   const uint64_t mask = a.present[g] & a.nmask;
-  uint8_t* desc = a.desc + (g - a.g_desc0) * a.desc_stride;
   const uint32_t np = __popcll(mask);
   if (np == n || np < d) {
     if (lane == 0) {
@@ -653,6 +687,8 @@ __global__ __launch_bounds__(64) void k_prepare(Prep a) {
     }
     return;
   }
+  const uint8_t* lg = sh.lg;
+  const uint8_t* ex = sh.ex;
   const uint64_t dmask = (d >= 64) ? ~0ull : ((1ull << d) - 1);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const uint32_t e = n - np;
@@ -661,26 +697,26 @@ __global__ __launch_bounds__(64) void k_prepare(Prep a) {
   if (lane < n) {
     const bool present = (mask >> lane) & 1ull;
     if (lane < d) {
-      if (present) Pl[__popcll(mask & dmask & below)] = static_cast<uint8_t>(lane);
-      else El[__popcll(~mask & dmask & below)] = static_cast<uint8_t>(lane);
+      if (present) s.Pl[__popcll(mask & dmask & below)] = static_cast<uint8_t>(lane);
+      else s.El[__popcll(~mask & dmask & below)] = static_cast<uint8_t>(lane);
     } else if (present) {
       const uint32_t rank = __popcll(mask & ~dmask & below);
-      if (rank < ed) Jl[rank] = static_cast<uint8_t>(lane);
+      if (rank < ed) s.Jl[rank] = static_cast<uint8_t>(lane);
     }
-    if (!present) outr[__popcll(~mask & a.nmask & below)] = static_cast<uint8_t>(lane);
+    if (!present) s.outr[__popcll(~mask & a.nmask & below)] = static_cast<uint8_t>(lane);
   }
-  __syncthreads();
-  if (lane < d) surv[lane] = lane < npd ? Pl[lane] : Jl[lane - npd];
+  wsync();
+  if (lane < d) s.surv[lane] = lane < npd ? s.Pl[lane] : s.Jl[lane - npd];
   // [B | I], B[i][l] = M[J_i][E_l]
   const uint32_t w = 2 * ed;
   for (uint32_t idx = lane; idx < ed * w; idx += 64) {
     const uint32_t i = idx / w, col = idx - i * w;
-    Ba[idx] = col < ed ? a.M[Jl[i] * d + El[col]] : static_cast<uint8_t>(col - ed == i ? 1 : 0);
+    s.Ba[idx] = col < ed ? M[s.Jl[i] * d + s.El[col]] : static_cast<uint8_t>(col - ed == i ? 1 : 0);
   }
-  __syncthreads();
+  wsync();
   for (uint32_t r = 0; r < ed; ++r) {
-    if (Ba[r * w + r] == 0) {  // uniform branch (every lane reads the same byte)
-      const bool cand = lane > r && lane < ed && Ba[lane * w + r] != 0;
+    if (s.Ba[r * w + r] == 0) {  // uniform branch (every lane reads the same byte)
+      const bool cand = lane > r && lane < ed && s.Ba[lane * w + r] != 0;
       const uint64_t bal = __ballot(cand);
       if (bal == 0) {  // singular: cannot happen for an MDS code
         if (lane == 0) *reinterpret_cast<uint32_t*>(desc) = 7u << 16;
@@ -688,56 +724,73 @@ __global__ __launch_bounds__(64) void k_prepare(Prep a) {
       }
       const uint32_t b = __ffsll(static_cast<long long>(bal)) - 1;
       for (uint32_t col = lane; col < w; col += 64) {
-        const uint8_t t = Ba[r * w + col];
-        Ba[r * w + col] = Ba[b * w + col];
-        Ba[b * w + col] = t;
+        const uint8_t t = s.Ba[r * w + col];
+        s.Ba[r * w + col] = s.Ba[b * w + col];
+        s.Ba[b * w + col] = t;
       }
-      __syncthreads();
+      wsync();
     }
-    const uint32_t s = ex[255 - lg[Ba[r * w + r]]];  // 1 / pivot
-    __syncthreads();
-    for (uint32_t col = lane; col < w; col += 64) Ba[r * w + col] = lmul(lg, ex, s, Ba[r * w + col]);
-    if (lane < ed) fcol[lane] = Ba[lane * w + r];
-    __syncthreads();
+    const uint32_t sc = ex[255 - lg[s.Ba[r * w + r]]];  // 1 / pivot
+    wsync();
+    for (uint32_t col = lane; col < w; col += 64) s.Ba[r * w + col] = lmul(lg, ex, sc, s.Ba[r * w + col]);
+    if (lane < ed) s.fcol[lane] = s.Ba[lane * w + r];
+    wsync();
     for (uint32_t idx = lane; idx < ed * w; idx += 64) {
       const uint32_t o = idx / w, col = idx - o * w;
-      if (o != r) Ba[idx] ^= lmul(lg, ex, fcol[o], Ba[r * w + col]);
+      if (o != r) s.Ba[idx] ^= lmul(lg, ex, s.fcol[o], s.Ba[r * w + col]);
     }
-    __syncthreads();
+    wsync();
   }
   // Dinv rows of the erased data rows (Binv = Ba[:, ed:])
   for (uint32_t idx = lane; idx < ed * d; idx += 64) {
     const uint32_t l = idx / d, pos = idx - l * d;
     uint8_t v;
     if (pos >= npd) {
-      v = Ba[l * w + ed + (pos - npd)];
+      v = s.Ba[l * w + ed + (pos - npd)];
     } else {
       v = 0;
-      for (uint32_t i = 0; i < ed; ++i) v ^= lmul(lg, ex, Ba[l * w + ed + i], a.M[Jl[i] * d + Pl[pos]]);
+      for (uint32_t i = 0; i < ed; ++i) v ^= lmul(lg, ex, s.Ba[l * w + ed + i], M[s.Jl[i] * d + s.Pl[pos]]);
     }
-    DE[l * 64 + pos] = v;
+    s.DE[l * 64 + pos] = v;
   }
-  __syncthreads();
+  wsync();
   // header + rows + coefficients
   const uint32_t dpad = a.dpad, epad = a.epad;
   if (lane == 0) *reinterpret_cast<uint32_t*>(desc) = (e & 0xffu) | (ed << 8);
-  for (uint32_t i = lane; i < dpad; i += 64) desc[4 + i] = i < d ? surv[i] : 0;
-  for (uint32_t i = lane; i < epad; i += 64) desc[4 + dpad + i] = i < e ? outr[i] : 0;
-  uint8_t* coef = desc + 4 + dpad + epad;
+  for (uint32_t i = lane; i < dpad; i += 64) desc[4 + i] = i < d ? s.surv[i] : 0;
+  for (uint32_t i = lane; i < epad; i += 64) desc[4 + dpad + i] = i < e ? s.outr[i] : 0;
+  DescPtr coef = desc + 4 + dpad + epad;
   for (uint32_t idx = lane; idx < e * dpad; idx += 64) {
     const uint32_t i = idx / dpad, pos = idx - i * dpad;
     uint8_t v = 0;
     if (pos < d) {
       if (i < ed) {
-        v = DE[i * 64 + pos];
+        v = s.DE[i * 64 + pos];
       } else {
-        const uint32_t r = outr[i];
-        if (pos < npd) v = a.M[r * d + Pl[pos]];
-        for (uint32_t l = 0; l < ed; ++l) v ^= lmul(lg, ex, a.M[r * d + El[l]], DE[l * 64 + pos]);
+        const uint32_t r = s.outr[i];
+        if (pos < npd) v = M[r * d + s.Pl[pos]];
+        for (uint32_t l = 0; l < ed; ++l) v ^= lmul(lg, ex, M[r * d + s.El[l]], s.DE[l * 64 + pos]);
       }
     }
     coef[idx] = v;
   }
+}
+
+// kPrepWaves groups per block, one per wave: the tables and M are staged
+// once per block, and 8192 jumbo groups fit the chip in about one round
+// (22 KiB of LDS per block).
+constexpr uint32_t kPrepWaves = 4;
+
+__global__ __launch_bounds__(64 * kPrepWaves) void k_prepare(Prep a, uint32_t groups) {
+  __shared__ PrepShared sh;
+  __shared__ PrepWave sw[kPrepWaves];
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  prep_stage(a, sh, threadIdx.x, 64 * kPrepWaves);
+  __syncthreads();
+  const uint32_t gl = blockIdx.x * kPrepWaves + w;
+  if (gl >= groups) return;
+  const uint64_t g = a.g0 + gl;
+  prep_wave(a, g, a.desc + (g - a.g_desc0) * a.desc_stride, sh, sw[w], lane);
 }
 
 // ------------------------------------------------------------- launchers
@@ -853,7 +906,7 @@ hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s) {
 }
 
 hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s) {
-  launch(kKPrepare, k_prepare, dim3(groups), dim3(64), 0, s, a);
+  launch(kKPrepare, k_prepare, dim3((groups + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0, s, a, groups);
   return hipGetLastError();
 }
 

@@ -58,5 +58,6 @@ hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s);
 hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s);
 
 
+
 }  // namespace kern
 }  // namespace ugo
