@@ -9,6 +9,11 @@
 #include <string>
 #include <vector>
 
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+using namespace ugo;
+using namespace ugo::kern;
+
 // (A/B only, round 2: 549.0 vs 544.7 us production, profiles/r2/jvariants_wave_aligned.jsonl;
 // VALU per wave down ~28% but 113 VGPRs -> 4 waves/SIMD, spills at 5.)
 // Wave-aligned form of k_apply_q for rows whose chunk count is just under a
@@ -93,10 +98,6 @@ __global__ __launch_bounds__(256) void k_apply_qa(Batch a) {
   if (wst) a.status[g] = 0;
 }
 
-#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
-
-using namespace ugo;
-using namespace ugo::kern;
 
 // ---------------------------------------------- k_apply_gq (A/B only)
 // Round-2 attempt at fusing k_prepare into the jumbo apply:
