@@ -185,9 +185,19 @@ def rx_case(G, loss, reps, encrypt=True):
     ta = e[0].elapsed_time(e[1]) / reps * 1e-3
     tr = e[1].elapsed_time(e[2]) / reps * 1e-3
     ti = ei[0].elapsed_time(ei[1]) / reps * 1e-3
+    # per-kernel durations of rx_assemble: optimistic placement, then the three
+    # dedupe kernels gated on the duplicate flag (empty launches without duplicates)
+    names = ("place", "claim_fill_gated", "claim_gated", "replace_gated")
+    enc.timing_begin(len(names) * reps)
+    for _ in range(reps):
+        present.zero_()
+        enc.rx_assemble(wire, lens, sh, present, shard_size=S, pad=pad if encrypt else None, stats=st)
+    recs, _ = enc.timing_end()
+    ms = recs["ms"].reshape(-1, len(names))
+    kern = {nm: round(float(np.median(ms[:, k])) * 1e3, 1) for k, nm in enumerate(names)}
     asm_bytes = npk * (1476 + S)  # packet read + slot write
     return [{"case": f"rx assemble (10+3) loss={loss} rc4={encrypt}", "groups": G, "packets": npk,
-             "us": ta * 1e6, "GBps": asm_bytes / ta / 1e9, "Mpkt_per_s": npk / ta / 1e6},
+             "us": ta * 1e6, "GBps": asm_bytes / ta / 1e9, "Mpkt_per_s": npk / ta / 1e6, "kernel_us": kern},
             {"case": f"rx reconstruct data-only after assemble", "groups": G, "us": tr * 1e6,
              "Mpkt_per_s_total": npk / (ta + tr) / 1e6},
             {"case": f"rx reconstruct_into data-only after assemble", "groups": G, "us": ti * 1e6,

@@ -103,7 +103,10 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(d_lens, lens.data(), npk * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_row, dst_row.data(), npk * 4, hipMemcpyHostToDevice));
   CK(hipMemset(d_stats, 0, 16));
-  RxArgs a{d_wire, d_lens, d_pad, d_sh, d_present, d_stats, npk, slot, 0, G, G * pitch, pitch, S, n};
+  RxArgs a{};
+  a.wire = d_wire; a.lens = d_lens; a.pad = d_pad; a.shards = d_sh; a.present = d_present; a.stats = d_stats;
+  a.npk = npk; a.slot = slot; a.first_group = 0; a.groups = G; a.rstride = G * pitch; a.gstride = pitch;
+  a.S = S; a.n = n;
   const uint32_t blocks = rx_blocks(a);
   const double bytes = double(npk) * (1476 + S);  // algorithmic: packet read + payload written
 

@@ -15,9 +15,15 @@
 //
 // Duplicates: input drops a packet whose seqid is already queued, so the
 // first arrival of a seqid is the one kept (ugo/fec.go:123-129).  A batch is
-// one window of arrivals in ring order: k_rx_claim takes, per (group, row),
-// the smallest packet index of an accepted packet (atomicMin), and the place
-// kernels write only that packet; later copies count as duplicates.
+// one window of arrivals in ring order, and the first copy in ring order must
+// win.  Duplicates are rare, so placement is optimistic: the place kernel
+// writes every accepted packet and learns from its presence atomicOr whether
+// the (group, row) was already taken; if any was, a flag is set and three
+// gated kernels -- which return at once when it is not -- fill the claim
+// words, take per (group, row) the smallest packet index (atomicMin,
+// k_rx_claim) and re-place exactly the winners over whatever the racing
+// copies left.  Without duplicates that costs three empty launches instead of
+// a claim pass over every header before placement.
 //
 // The packet sits at a 16-aligned slot, so its payload (offset 6) is
 // misaligned: each thread loads the two aligned chunks covering its 16 output
@@ -49,7 +55,39 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
 // next packet's header is fetched before the current payload is processed.
 // Measured alternatives: one wave per packet with two loads per chunk 1.4x
 // slower; one thread per chunk across packets 4.5x slower (5 loads per 16 B).
+// Presence bit, duplicate detection and stats of placed packets (lane 0 of
+// each half-wave): the optimistic pass counts a packet whose bit was already
+// set as a duplicate and raises a.dup; the re-place pass touches nothing.
+// The presence atomicOr returns the old mask, and waiting for it inside the
+// packet loop stalls the wave for a full memory round trip per packet (RX
+// 512 vs ~470 us), so a packet's result is settled one iteration later.
+struct RxAccount {
+  unsigned long long old = 0;
+  uint32_t why = 5, row = 0;
+  __device__ __forceinline__ void settle(const RxArgs& a, uint32_t* bstats) {
+    if (why >= 5) return;
+    uint32_t w = why;
+    if (w == 0 && a.dup && ((old >> row) & 1ull)) {
+      w = 4;
+      *a.dup = 1u;
+    }
+    atomicAdd(&bstats[w], 1u);
+    why = 5;
+  }
+  __device__ __forceinline__ void issue(const RxArgs& a, uint32_t* bstats, uint32_t w, uint64_t gs, uint32_t r) {
+    settle(a, bstats);
+    if (a.fixup || w >= 5) return;
+    why = w;
+    row = r;
+    old = 0;
+    if (w == 0) old = atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << r);
+  }
+};
+
+__device__ __forceinline__ bool rx_gated_off(const RxArgs& a) { return a.gate && *a.gate == 0u; }
+
 __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
+  if (rx_gated_off(a)) return;
   // stats: summed per block in LDS, one atomic per block per counter (a device
   // counter hit once per packet serialises at ~11 ns per atomic:
   // MI355X_MICROARCH.md "fanin")
@@ -60,6 +98,7 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
   const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
   const uint64_t nwaves = (gridDim.x * 256ull) >> 6;
   const uint32_t nq = (a.S + 15u) / 16u;  // output chunks per row
+  RxAccount acct;
   uint64_t i = 2 * wave + half;
   u32x4 hn = {0u, 0u, 0u, 0u};
   if (i < a.npk) hn = ld16(a.wire + i * a.slot);
@@ -130,11 +169,9 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
         }
       }
     }
-    if (hl == 0 && why < 5) {
-      if (ok) atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
-      atomicAdd(&bstats[why], 1u);
-    }
+    if (hl == 0) acct.issue(a, bstats, why, gs, row);
   }
+  if (hl == 0) acct.settle(a, bstats);
   if (a.stats) {
     __syncthreads();
     if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
@@ -155,6 +192,7 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 // NT: bit 0 nontemporal payload loads, bit 1 nontemporal stores.
 template <int NP, int MODE = 0, int NT = 0>
 __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
+  if (rx_gated_off(a)) return;
   __shared__ uint32_t bstats[5];
   if (threadIdx.x < 5) bstats[threadIdx.x] = 0;
   __syncthreads();
@@ -177,6 +215,7 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
       kby[q] = B.y;
     }
   }
+  RxAccount acct;
   uint64_t i = 2 * wave + half;
   u32x4 hn = zero;
   uint32_t ln = 0;
@@ -273,11 +312,14 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
         }
       }
     }
-    if (hl == 0 && why < 5) {
-      if (MODE == 0 && ok) atomicOr(reinterpret_cast<unsigned long long*>(&a.present[grp - a.first_group]), 1ull << row);
-      atomicAdd(&bstats[why], 1u);
+    if (hl == 0) {
+      if constexpr (MODE == 0)
+        acct.issue(a, bstats, why, grp - a.first_group, row);
+      else if (why < 5)
+        atomicAdd(&bstats[why], 1u);
     }
   }
+  if (hl == 0) acct.settle(a, bstats);
   if (a.stats) {
     __syncthreads();
     if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
@@ -288,6 +330,7 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
 // flag), classifies it exactly as the place kernels do, and takes the
 // smallest index per (group, row).  ~8 B read per 1.5-KB packet.
 __global__ __launch_bounds__(256) void k_rx_claim(RxArgs a) {
+  if (rx_gated_off(a)) return;
   const uint64_t nthreads = gridDim.x * 256ull;
   uint32_t k0 = 0u, k1 = 0u;
   if (a.pad) {
@@ -305,6 +348,19 @@ __global__ __launch_bounds__(256) void k_rx_claim(RxArgs a) {
     if (grp < a.first_group || grp >= a.first_group + a.groups) continue;
     atomicMin(&a.win[(grp - a.first_group) * a.n + seqid % a.n], static_cast<uint32_t>(i));
   }
+}
+
+__global__ __launch_bounds__(256) void k_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate) {
+  if (gate && *gate == 0u) return;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < words; i += gridDim.x * 256ull) win[i] = 0xffffffffu;
+}
+
+hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, hipStream_t s) {
+  uint64_t blocks = (words + 255) / 256;
+  if (blocks == 0) return hipSuccess;
+  if (blocks > 1024u) blocks = 1024u;
+  launch(kKRx, k_rx_fill, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, win, words, gate);
+  return hipGetLastError();
 }
 
 static inline uint32_t rx_blocks(const RxArgs& a) {

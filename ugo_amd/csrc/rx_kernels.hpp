@@ -15,6 +15,9 @@ struct RxArgs {
   uint64_t* present;       // per-group presence masks (device, OR-ed)
   uint32_t* stats;         // accepted, bad flag, out of window, too short, duplicate (device, nullable)
   uint32_t* win;           // [groups][n] first packet index per (group, row) (k_rx_claim), or null
+  uint32_t* dup;           // optimistic pass: set to 1 when a packet finds its presence bit set, or null
+  const uint32_t* gate;    // if non-null, the kernel does nothing unless *gate != 0
+  uint32_t fixup;          // re-place pass: claim winners only, no stats, presence already set
   uint64_t npk;
   uint64_t slot;
   uint64_t first_group;
@@ -26,8 +29,9 @@ struct RxArgs {
 };
 
 // Claims every (group, row) for its first packet in ring order (atomicMin of
-// the packet index into a.win, which the caller fills with 0xff bytes), then
+// the packet index into a.win, which launch_rx_fill sets to 0xffffffff), then
 // places the winners.  a.win == null places every accepted packet.
+hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, hipStream_t s);
 hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s);
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s);
 

@@ -777,17 +777,29 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   a.gstride = group_stride;
   a.S = static_cast<uint32_t>(S);
   a.n = static_cast<uint32_t>(c->n);
-  // first arrival wins (ugo/fec.go:123-129): claim words [groups][n], all 0xff
+  // First arrival in ring order wins (ugo/fec.go:123-129), optimistically
+  // (rx_kernels.hip): place everything, flag a (group, row) taken twice, and
+  // only then -- gated on the flag, on the device -- claim and re-place.
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  const size_t wbytes = groups * size_t(c->n) * sizeof(uint32_t);
-  void* win = nullptr;
-  int st = scratch_alloc(c, wbytes, s, &win);
+  const uint64_t words = groups * uint64_t(c->n);
+  void* scratch = nullptr;
+  int st = scratch_alloc(c, words * sizeof(uint32_t) + 16, s, &scratch);
   if (st) return st;
-  a.win = static_cast<uint32_t*>(win);
-  if (hipMemsetAsync(win, 0xff, wbytes, s) != hipSuccess) st = UGO_FEC_ERR_HIP;
-  if (!st) st = hip_status(ugo::kern::launch_rx_claim(a, s));
+  uint32_t* win = static_cast<uint32_t*>(scratch);
+  uint32_t* dup = win + words;
+  if (hipMemsetAsync(dup, 0, sizeof(uint32_t), s) != hipSuccess) st = UGO_FEC_ERR_HIP;
+  a.dup = dup;
   if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
-  const int fr = scratch_free(win, s);
+  if (!st) st = hip_status(ugo::kern::launch_rx_fill(win, words, dup, s));
+  ugo::kern::RxArgs f = a;  // the gated claim and re-place of the first copies
+  f.win = win;
+  f.gate = dup;
+  f.dup = nullptr;
+  f.stats = nullptr;
+  f.fixup = 1;
+  if (!st) st = hip_status(ugo::kern::launch_rx_claim(f, s));
+  if (!st) st = hip_status(ugo::kern::launch_rx_scatter(f, s));
+  const int fr = scratch_free(scratch, s);
   return st ? st : fr;
 }
 
