@@ -174,9 +174,12 @@ int ugo_fec_check_shards(int n, const size_t* lens, int nil_ok, size_t* shard_si
  *    by what it puts in a ring and by [first_group, first_group + groups):
  *    packets of groups outside that window are counted out-of-window and
  *    dropped, as a packet older than rxlimit arrivals or fecExpire is;
- *  - duplicates are only detected within one call: a seqid placed by an
- *    earlier call into the same batch is overwritten by a later call's copy
- *    (give each window its own batch, or one call per batch).
+ *  - duplicates are only resolved within one call: a seqid placed by an
+ *    earlier call into the same batch is overwritten by this call's first
+ *    copy, which stats then counts as a duplicate (give each window its own
+ *    batch, or one call per batch).
+ * Placement is optimistic: the extra claim and re-place passes run (inside
+ * the call, gated on the device) only when the window holds a duplicate.
  * The engine takes (groups*(d+p)*4) bytes of stream-ordered scratch per call.
  * npackets < 2^32 - 1. */
 int ugo_fec_rx_assemble(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, const uint16_t* lens,
