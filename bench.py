@@ -112,14 +112,25 @@ def launcher_cmd(argv, nproc: int, port: int, script: str = None):
             "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)] + list(argv)
 
 
+def result_json(line: str):
+    """The result object in one line of the ranks' shared stdout, or None.
+    Ranks write to one pipe, so another rank's output can share the line,
+    before or after the object: it is parsed from the first '{' it starts at."""
+    dec = json.JSONDecoder()
+    k = line.find("{")
+    while k >= 0:
+        try:
+            obj, end = dec.raw_decode(line, k)
+            if isinstance(obj, dict) and "metric" in obj:
+                return line[k:end]
+        except ValueError:
+            pass
+        k = line.find("{", k + 1)
+    return None
+
+
 def is_result_line(line: str) -> bool:
-    s = line.strip()
-    if not s.startswith("{"):
-        return False
-    try:
-        return "metric" in json.loads(s)
-    except ValueError:
-        return False
+    return result_json(line) is not None
 
 
 def launch(argv, nproc: int, script: str = None, timeout: float = None) -> int:
@@ -135,10 +146,14 @@ def launch(argv, nproc: int, script: str = None, timeout: float = None) -> int:
     n_lines = 0
     try:
         for line in proc.stdout:
-            if is_result_line(line) and n_lines == 0:
-                sys.stdout.write(line if line.endswith("\n") else line + "\n")
+            res = result_json(line)
+            if res is not None and n_lines == 0:
+                sys.stdout.write(res + "\n")
                 sys.stdout.flush()
                 n_lines += 1
+                rest = line.replace(res, "", 1)
+                if rest.strip():
+                    sys.stderr.write(rest if rest.endswith("\n") else rest + "\n")
             else:
                 sys.stderr.write(line)
         rc = proc.wait(timeout=timeout)

@@ -51,6 +51,9 @@ def test_result_line_filter():
     assert not bench.is_result_line('{"other": 1}')
     assert not bench.is_result_line("rank 1 noise on stdout")
     assert not bench.is_result_line("{not json")
+    # another rank's unterminated output sharing the pipe line
+    assert bench.result_json('rank 1 noise{x}{"metric": "x", "value": 1}\n') == '{"metric": "x", "value": 1}'
+    assert bench.result_json('{"metric": "x", "value": 1}rank 1 noise\n') == '{"metric": "x", "value": 1}'
 
 
 @pytest.mark.parametrize("total", [1000, 7])
