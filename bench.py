@@ -225,15 +225,20 @@ def all_ranks_ok(ok: bool, world: int) -> bool:
 
 def timed_region(step, steps: int, sync, world: int) -> float:
     """Exactly `steps` steps bracketed by barrier + device synchronize on both
-    sides; returns this rank's wall time (reduce_max gives the job's)."""
+    sides; returns this rank's wall time from the start barrier to its own
+    last step done (reduce_max gives the job's: the slowest rank's).  The
+    closing barrier is outside the clock: its latency (a gloo round over all
+    ranks) is not step time, and at --steps 20 (a ~7 ms region) it would be
+    a visible share of it."""
     barrier(world)
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     sync()
+    elapsed = time.perf_counter() - t0
     barrier(world)
-    return time.perf_counter() - t0
+    return elapsed
 
 
 def clock_warmup(step, sync, min_ms: float, chunk: int = 5, tol: float = 0.02, max_ms: float = None):
