@@ -323,6 +323,24 @@ int main(int argc, char** argv) {
   add(k_apply_q<8, 2, 1, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt1");
   add(k_apply_q<8, 2, 1, 1, 8>, ar, dec_bytes, "dec perm streaming ring8 nt1");
   add(k_apply_q<8, 2, 3, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt3 (production)");
+  {  // residency caps (round 2): dynamic LDS so that exactly `bpc` blocks fit a CU
+    auto cap = [](uint32_t bpc, uint32_t static_kib) { return 160u * 1024u / bpc - static_kib * 1024u - 1024u; };
+    for (uint32_t bpc : {4u, 3u, 2u}) {
+      const uint32_t x = cap(bpc, 0);
+      vars.push_back({"dec perm streaming (production), OCC " + std::to_string(bpc) + " blocks/CU", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_q<8, 2, 3, 1, 4>), dim3(grid), dim3(256), x, 0, ar); }, {}});
+    }
+    for (uint32_t bpc : {4u, 3u, 2u, 1u}) {
+      const uint32_t x = cap(bpc, 32);
+      vars.push_back({"enc const-network lds-dma 8 rows, nt stores, OCC " + std::to_string(bpc) + " blocks/CU", enc_bytes,
+                      [=]() { hipLaunchKernelGGL((k_encode_g<32, 8, 2, 8>), dim3(grid), dim3(256), x, 0, a); }, {}});
+    }
+    {
+      const uint32_t x = cap(1, 64);
+      vars.push_back({"enc const-network lds-dma 16 rows, nt stores, OCC 1 block/CU", enc_bytes,
+                      [=]() { hipLaunchKernelGGL((k_encode_g<32, 8, 2, 16>), dim3(grid), dim3(256), x, 0, a); }, {}});
+    }
+  }
   {  // wave-aligned groups: item = g * 576 + chunk
     Batch aa = ar;
     aa.items = G * ((a.chunks + 63) / 64 * 64);

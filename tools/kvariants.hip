@@ -548,6 +548,62 @@ int main(int argc, char** argv) {
       vars.push_back({"COLD dec MEMORY PATTERN ONLY lds-dma nt stores, OUT-OF-PLACE outputs", dec_bytes, [=]() {
         hipLaunchKernelGGL((k_pattern_rec<3, true, true>), dim3(grid), dim3(256), 0, 0, roto[(*cnt)++ & 3]); }, {}});
     }
+    {  // occupancy sweep (round 2): extra dynamic LDS per block caps the blocks per CU, so fewer
+       // requests are in flight -- does a lower load on the DRAM banks help the mixed stream pattern?
+      const uint32_t grid = (pl.items + 255) / 256;
+      std::vector<Batch> rotk(rot);
+      for (auto& b : rotk) {
+        uint8_t* ob;
+        CK(hipMalloc(&ob, 4 * G * pitch));
+        b.out = ob;
+        b.ogstride = pitch;
+        b.orstride = G * pitch;
+      }
+      for (uint32_t bpc : {5u, 4u, 3u, 2u}) {  // blocks per CU (k_encode_g: 32 KiB static LDS each)
+        const uint32_t extra = bpc == 5 ? 0u : (160u * 1024u / bpc - 32u * 1024u - 1024u);  // exactly bpc fit
+        vars.push_back({"COLD OCC enc production, " + std::to_string(bpc) + " blocks/CU", enc_bytes, [=]() {
+          hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8>), dim3(grid), dim3(256), extra, 0, rot[(*cnt)++ & 3]); }, {}});
+      }
+      auto occ_extra = [](uint32_t bpc, uint32_t static_kib) {  // dynamic LDS so that bpc blocks fit a CU
+        return 160u * 1024u / bpc - static_kib * 1024u - 1024u;  // exactly bpc blocks fit
+      };
+      vars.push_back({"COLD OCC2 enc lds-dma 10 rows (40 KiB: 4 blocks/CU natively)", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 10>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      for (uint32_t bpc : {6u, 5u, 4u}) {
+        const uint32_t extra = occ_extra(bpc, 24);
+        vars.push_back({"COLD OCC2 enc lds-dma 6 rows, " + std::to_string(bpc) + " blocks/CU", enc_bytes, [=]() {
+          hipLaunchKernelGGL((k_encode_g<10, 3, 2, 6>), dim3(grid), dim3(256), extra, 0, rot[(*cnt)++ & 3]); }, {}});
+      }
+      for (uint32_t bpc : {8u, 6u, 5u, 4u, 3u}) {  // all rows to registers (62 VGPRs: 8 waves/SIMD)
+        const uint32_t extra = bpc == 8 ? 0u : occ_extra(bpc, 0);
+        vars.push_back({"COLD OCC2 enc nt3 registers, " + std::to_string(bpc) + " blocks/CU", enc_bytes, [=]() {
+          hipLaunchKernelGGL((k_encode_c<10, 3, 3>), dim3(grid), dim3(256), extra, 0, rot[(*cnt)++ & 3]); }, {}});
+      }
+      // the bench step: encode then reconstruct_into of the same batch, old vs new encode occupancy
+      vars.push_back({"COLD OCC STEP enc 8-row stage (5 blocks/CU) + dec INTO", enc_bytes + dec_bytes, [=]() {
+        const int r = (*cnt)++ & 3;
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8>), dim3(grid), dim3(256), 0, 0, rot[r]);
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[r]); }, {}});
+      vars.push_back({"COLD OCC STEP enc 10-row stage (4 blocks/CU, production) + dec INTO", enc_bytes + dec_bytes, [=]() {
+        const int r = (*cnt)++ & 3;
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 10>), dim3(grid), dim3(256), 0, 0, rot[r]);
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[r]); }, {}});
+      vars.push_back({"COLD OCC enc 10-row stage (4 blocks/CU) alone", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 10>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD OCC enc 13-row stage (3 blocks/CU) alone", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD OCC STEP enc 13-row stage (3 blocks/CU) + dec INTO", enc_bytes + dec_bytes, [=]() {
+        const int r = (*cnt)++ & 3;
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[r]);
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[r]); }, {}});
+      vars.push_back({"COLD OCC enc 20-row stage (2 blocks/CU) alone", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 20>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      for (uint32_t bpc : {5u, 4u, 3u, 2u}) {  // k_apply_p into: VGPR-limited to 5 blocks/CU
+        const uint32_t extra = bpc == 5 ? 0u : (160u * 1024u / bpc - 1024u);  // exactly bpc fit
+        vars.push_back({"COLD OCC dec INTO production, " + std::to_string(bpc) + " blocks/CU", dec_bytes, [=]() {
+          hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), extra, 0, rotk[(*cnt)++ & 3]); }, {}});
+      }
+    }
     {  // canonical survivor slots (same kernels, descriptor table with slot r = row r)
       std::vector<Batch> rotc(rot);
       for (auto& b : rotc) b.desc = dtabc;

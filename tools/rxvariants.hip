@@ -147,6 +147,17 @@ int main(int argc, char** argv) {
     vs.push_back({"COLD k_rx_place<3> nt loads", [&] { k_rx_place<3, 0, 1><<<blocks, 256>>>(nx()); }, {}});
     vs.push_back({"COLD k_rx_place<3> nt stores", [&] { k_rx_place<3, 0, 2><<<blocks, 256>>>(nx()); }, {}});
     vs.push_back({"COLD k_rx_place<3> nt loads + stores", [&] { k_rx_place<3, 0, 3><<<blocks, 256>>>(nx()); }, {}});
+    // occupancy (round 2): grid size (blocks per CU of the grid-stride loop) and LDS-capped residency
+    for (uint32_t bpc : {8u, 6u, 4u, 3u}) {
+      const uint32_t gb = 256u * bpc;
+      vs.push_back({"COLD OCC k_rx_place<3> nt3, grid " + std::to_string(bpc) + " blocks/CU",
+                    [&, gb] { k_rx_place<3, 0, 3><<<gb, 256>>>(nx()); }, {}});
+    }
+    for (uint32_t bpc : {6u, 4u}) {
+      const uint32_t extra = 160u * 1024u / bpc + 512u;
+      vs.push_back({"COLD OCC k_rx_place<3> nt3, grid 8/CU, LDS-capped at " + std::to_string(bpc) + " blocks/CU",
+                    [&, extra] { k_rx_place<3, 0, 3><<<2048, 256, extra>>>(nx()); }, {}});
+    }
     vs.push_back({"COLD PATTERN: linear copy of the same bytes", [&] {
       const int r = cnt++ % 3;
       k_copy_linear<<<4096, 256>>>(reinterpret_cast<const u32x4*>(rot[r].wire), reinterpret_cast<u32x4*>(lin[r]), npk * 1480 / 16); }, {}});

@@ -102,6 +102,23 @@ int main(int argc, char** argv) {
     addc(k_tx_c<10, 3, 3, false>, "COLD tx nt3 (nt loads + stores)");
     addc(k_tx_pattern<0>, "COLD TX MEMORY PATTERN ONLY (nt loads, plain stores)");
     addc(k_tx_pattern<2>, "COLD TX MEMORY PATTERN ONLY (nt loads + stores)");
+    // occupancy sweep (round 2): dynamic LDS caps the blocks per CU
+    for (uint32_t bpc : {4u, 3u, 2u}) {
+      const uint32_t extra = 160u * 1024u / bpc + 512u;
+      vars.push_back({"COLD OCC tx production (scalar lens, nt3), " + std::to_string(bpc) + " blocks/CU",
+                      [=, &rot, &cnt]() {
+                        hipLaunchKernelGGL((k_tx_c<10, 3, 3, true>), dim3(grid), dim3(256), extra, 0, rot[cnt++ % 3]);
+                      }, {}});
+    }
+    vars.push_back({"COLD OCC tx production (scalar lens, nt3), natural occupancy", [=, &rot, &cnt]() {
+      hipLaunchKernelGGL((k_tx_c<10, 3, 3, true>), dim3(grid), dim3(256), 0, 0, rot[cnt++ % 3]); }, {}});
+    for (uint32_t bpc : {4u, 3u, 2u}) {
+      const uint32_t extra = 160u * 1024u / bpc + 512u;
+      vars.push_back({"COLD OCC TX MEMORY PATTERN ONLY (nt3), " + std::to_string(bpc) + " blocks/CU",
+                      [=, &rot, &cnt]() {
+                        hipLaunchKernelGGL((k_tx_pattern<2>), dim3(grid), dim3(256), extra, 0, rot[cnt++ % 3]);
+                      }, {}});
+    }
   }
   // correctness: every variant writes the same wire bytes
   std::vector<uint8_t> ref(G * n * slot), got(G * n * slot);

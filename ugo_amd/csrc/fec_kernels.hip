@@ -102,11 +102,18 @@ __global__ __launch_bounds__(256) void k_encode_c(Batch a) {
 }
 
 // k_encode_c with the first GR row loads staged through LDS by LDS-DMA (nt)
-// and the rest loaded to registers (nt): each wave owns GR x 1 KiB of LDS
-// (GR = 10: 40 KiB per block, 4 blocks per CU).
-template <int D, int P, int NTS = 0, int GR = D, int BS = 256>
+// and the rest loaded to registers (nt): each wave owns GR x 1 KiB of LDS.
+// LR >= GR sizes the stage, and with it the blocks per CU: the (10,3) encode
+// stages 8 rows in a 13-row stage (52 KiB per block), which caps it at 3
+// blocks = 3 waves per SIMD.  Fewer requests in flight run the 10-read +
+// 3-write stream mix faster on a cold batch: 188.6 us at 3 blocks/CU against
+// 194.9 at 4, 194.7 at 5 (the 8-row stage's natural occupancy) and 193.1 at
+// 2; in the bench's encode + reconstruct step 366.0 against 372.0 us
+// (profiles/r2/kvar_cold_occupancy_exact.jsonl).
+template <int D, int P, int NTS = 0, int GR = D, int BS = 256, int LR = GR>
 __global__ __launch_bounds__(BS) void k_encode_g(Batch a) {
-  __shared__ u32x4 stage[BS / 64][GR][64];
+  static_assert(LR >= GR, "the stage holds at least the staged rows");
+  __shared__ u32x4 stage[BS / 64][LR][64];
   const uint32_t item = blockIdx.x * BS + threadIdx.x;
   if (item >= a.items) return;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -813,6 +820,7 @@ static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
 // because the Infinity Cache then absorbs the rewritten parity lines.
 constexpr int kEncNT = 3;    // nontemporal loads and stores
 constexpr int kEncLdsRows = 8;  // (10,3): rows 0-7 by LDS-DMA nt, 8-9 to registers
+constexpr int kEncStageRows = 13;  // (10,3): 52-KiB stage, 3 blocks per CU (see k_encode_g)
 constexpr int kEncJumboNT = 3;  // (32,8): NT loads and stores (578 vs 615 us, tools/jvariants.hip)
 constexpr int kEncJumboLdsRows = 16;  // (32,8): rows 0-15 by LDS-DMA nt (557 vs 571 us)
 constexpr int kApplyNT = 3;  // nontemporal loads and stores
@@ -835,7 +843,7 @@ bool has_const_encode(int d, int p) { return (d == 10 && p == 3) || (d == 32 && 
 hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   const dim3 grid(blocks_for(a.items, 256)), block(256);
   if (d == 10 && p == 3)
-    launch(kKEncode, k_encode_g<10, 3, kEncNT & 2, kEncLdsRows>, grid, block, 0, s, a);
+    launch(kKEncode, k_encode_g<10, 3, kEncNT & 2, kEncLdsRows, 256, kEncStageRows>, grid, block, 0, s, a);
   else if (d == 32 && p == 8)
     launch(kKEncode, k_encode_g<32, 8, kEncJumboNT & 2, kEncJumboLdsRows>, grid, block, 0, s, a);
   else
