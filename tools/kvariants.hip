@@ -598,6 +598,18 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[r]); }, {}});
       vars.push_back({"COLD OCC enc 20-row stage (2 blocks/CU) alone", enc_bytes, [=]() {
         hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 20>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      for (uint32_t bpc : {4u, 3u}) {  // survivors by LDS-DMA (10 rows: 40 KiB, 4 blocks/CU natively)
+        const uint32_t extra = bpc == 4 ? 0u : (160u * 1024u / bpc - 40u * 1024u - 1024u);
+        vars.push_back({"COLD OCC dec INTO lds-dma 10, " + std::to_string(bpc) + " blocks/CU", dec_bytes, [=]() {
+          hipLaunchKernelGGL((k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 10>), dim3(grid), dim3(256), extra, 0,
+                             rotk[(*cnt)++ & 3]); }, {}});
+      }
+      for (uint32_t bpc : {5u, 4u, 3u}) {  // survivors 0-7 by LDS-DMA (32 KiB)
+        const uint32_t extra = bpc == 5 ? 0u : (160u * 1024u / bpc - 32u * 1024u - 1024u);
+        vars.push_back({"COLD OCC dec INTO lds-dma 8, " + std::to_string(bpc) + " blocks/CU", dec_bytes, [=]() {
+          hipLaunchKernelGGL((k_apply_p<10, 1, 3, 1, 1, 4, true, 0, 8>), dim3(grid), dim3(256), extra, 0,
+                             rotk[(*cnt)++ & 3]); }, {}});
+      }
       for (uint32_t bpc : {5u, 4u, 3u, 2u}) {  // k_apply_p into: VGPR-limited to 5 blocks/CU
         const uint32_t extra = bpc == 5 ? 0u : (160u * 1024u / bpc - 1024u);  // exactly bpc fit
         vars.push_back({"COLD OCC dec INTO production, " + std::to_string(bpc) + " blocks/CU", dec_bytes, [=]() {
