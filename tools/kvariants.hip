@@ -596,6 +596,27 @@ int main(int argc, char** argv) {
         const int r = (*cnt)++ & 3;
         hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[r]);
         hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[r]); }, {}});
+      vars.push_back({"COLD OCC3 enc 13-row stage, 10 rows by LDS-DMA", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 10, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD OCC3 enc 13-row stage, 6 rows by LDS-DMA", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 6, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD OCC3 enc 13-row stage, 4 rows by LDS-DMA", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 4, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"COLD OCC3 enc 13-row stage, 8 rows, plain stores", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 0, 8, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      for (uint32_t bpc : {4u, 3u}) {
+        const uint32_t x = 160u * 1024u / bpc - 1024u;
+        vars.push_back({"COLD OCC3 enc nt3 registers, exactly " + std::to_string(bpc) + " blocks/CU", enc_bytes, [=]() {
+          hipLaunchKernelGGL((k_encode_c<10, 3, 3>), dim3(grid), dim3(256), x, 0, rot[(*cnt)++ & 3]); }, {}});
+      }
+      {
+        const uint32_t g512 = (pl.items + 511) / 512;
+        vars.push_back({"COLD OCC3 enc block 512, 8 rows, 13-row stage (1 block = 8 waves/CU... 104 KiB)", enc_bytes, [=]() {
+          hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 512, 13>), dim3(g512), dim3(512), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+        const uint32_t g128 = (pl.items + 127) / 128;
+        vars.push_back({"COLD OCC3 enc block 128, 8 rows, 13-row stage (26 KiB: 6 blocks = 12 waves/CU)", enc_bytes, [=]() {
+          hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 128, 13>), dim3(g128), dim3(128), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      }
       vars.push_back({"COLD OCC enc 20-row stage (2 blocks/CU) alone", enc_bytes, [=]() {
         hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 20>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
       for (uint32_t bpc : {4u, 3u}) {  // survivors by LDS-DMA (10 rows: 40 KiB, 4 blocks/CU natively)
