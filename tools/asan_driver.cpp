@@ -1,0 +1,245 @@
+// asan_driver.cpp -- the C-ABI's host code under AddressSanitizer + UBSan
+// ("ASan/UBSan on the C++ host path").  Built by
+// tools/asan_build.sh together with every library source, host code
+// instrumented, device code not (-Xarch_host -fsanitize=...), and run on the
+// GPU box.  It drives every entry point family through its host logic --
+// argument checks, staging, pinned zero-copy paths, the C++ FEC object in
+// per-call and batched modes, RX/TX assembly -- and checks its own results
+// by round trips (encode -> erase -> reconstruct == original; TX -> RX ==
+// the sent payloads), so any memory error, UB or wrong byte stops it.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../include/ugo_fec.h"
+#include "../include/ugo_fec_conn.h"
+
+namespace {
+
+int failures = 0;
+#define EXPECT(c)                                                              \
+  do {                                                                         \
+    if (!(c)) {                                                                \
+      std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c);        \
+      ++failures;                                                              \
+    }                                                                          \
+  } while (0)
+
+std::mt19937_64 rng(0x5EED);
+uint8_t rb() { return static_cast<uint8_t>(rng()); }
+
+void check_shards_cases() {
+  size_t S = 0;
+  const size_t a[3] = {10, 10, 10}, b[3] = {10, 0, 10}, c[3] = {0, 0, 0}, e[3] = {10, 9, 10};
+  EXPECT(ugo_fec_check_shards(3, a, 0, &S) == UGO_FEC_OK && S == 10);
+  EXPECT(ugo_fec_check_shards(3, b, 1, &S) == UGO_FEC_OK && S == 10);
+  EXPECT(ugo_fec_check_shards(3, b, 0, &S) == UGO_FEC_ERR_SHARD_SIZE);
+  EXPECT(ugo_fec_check_shards(3, c, 1, &S) == UGO_FEC_ERR_SHARD_NO_DATA);
+  EXPECT(ugo_fec_check_shards(3, e, 1, &S) == UGO_FEC_ERR_SHARD_SIZE);
+}
+
+void null_args() {
+  ugo_fec* ctx = nullptr;
+  EXPECT(ugo_fec_create(0, 10, 3, nullptr) != UGO_FEC_OK);
+  EXPECT(ugo_fec_create(0, 0, 3, &ctx) != UGO_FEC_OK && ctx == nullptr);
+  EXPECT(ugo_fec_create(0, 200, 100, &ctx) != UGO_FEC_OK);
+  EXPECT(ugo_fec_encode_host(nullptr, nullptr, 1, 10, 16) == UGO_FEC_ERR_INVALID_ARG);
+  EXPECT(ugo_fec_reconstruct_host(nullptr, nullptr, nullptr, 1, 10, 16, 0, nullptr) == UGO_FEC_ERR_INVALID_ARG);
+  ugo_fecconn* f = nullptr;
+  EXPECT(ugo_fecconn_new(12, 10, 3, 0, &f) == UGO_FEC_ERR_INV_SHARD_NUM && f == nullptr);
+  EXPECT(ugo_fecconn_input(nullptr, nullptr, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr) != UGO_FEC_OK);
+  EXPECT(ugo_fec_strerror(UGO_FEC_ERR_SHARD_SIZE) != nullptr);
+}
+
+// encode -> erase up to p rows -> reconstruct == original, host buffers
+void host_round_trip(int d, int p, size_t S, size_t G, bool pinned) {
+  const int n = d + p;
+  const size_t pitch = (S + 15) / 16 * 16 + (pinned ? 0 : 16);
+  ugo_fec* ctx = nullptr;
+  EXPECT(ugo_fec_create(0, d, p, &ctx) == UGO_FEC_OK);
+  if (!ctx) return;
+  const size_t bytes = G * n * pitch;
+  uint8_t* buf = nullptr;
+  std::vector<uint8_t> pageable;
+  if (pinned) {
+    void* v = nullptr;
+    EXPECT(ugo_fec_host_alloc(bytes, &v) == UGO_FEC_OK);
+    buf = static_cast<uint8_t*>(v);
+  } else {
+    pageable.resize(bytes);
+    buf = pageable.data();
+  }
+  for (size_t i = 0; i < bytes; ++i) buf[i] = rb();
+  EXPECT(ugo_fec_encode_host(ctx, buf, G, S, pitch) == UGO_FEC_OK);
+  std::vector<uint8_t> ref(buf, buf + bytes);
+  std::vector<uint64_t> mask(G);
+  std::vector<int8_t> st(G, -1);
+  for (size_t g = 0; g < G; ++g) {
+    uint64_t m = (n >= 64 ? ~0ull : ((1ull << n) - 1));
+    const int e = static_cast<int>(rng() % (p + 1));
+    for (int k = 0; k < e; ++k) m &= ~(1ull << (rng() % n));
+    mask[g] = m;
+    for (int r = 0; r < n; ++r)
+      if (!((m >> r) & 1)) std::memset(buf + (g * n + r) * pitch, 0xA5, S);
+  }
+  EXPECT(ugo_fec_reconstruct_host(ctx, buf, mask.data(), G, S, pitch, 0, st.data()) == UGO_FEC_OK);
+  for (size_t g = 0; g < G; ++g) EXPECT(st[g] == 0);
+  bool same = true;
+  for (size_t g = 0; g < G && same; ++g)
+    for (int r = 0; r < n && same; ++r)
+      same = std::memcmp(buf + (g * n + r) * pitch, ref.data() + (g * n + r) * pitch, S) == 0;
+  EXPECT(same);
+  if (pinned) ugo_fec_host_free(buf);
+  ugo_fec_destroy(ctx);
+}
+
+// the FEC object: TX by markData / calcECC / markFEC over reused buffers, RX
+// over a lossy, duplicating channel per call and batched -- same recovered
+// sequence, and every lost full-length payload comes back
+void fec_object(int batch) {
+  const int d = 10, p = 3, n = 13;
+  const size_t L = UGO_FEC_MAX_PACKET;
+  ugo_fecconn *tx = nullptr, *rx1 = nullptr, *rx2 = nullptr;
+  EXPECT(ugo_fecconn_new(128, d, p, 0, &tx) == UGO_FEC_OK);
+  EXPECT(ugo_fecconn_new(128, d, p, 0, &rx1) == UGO_FEC_OK);
+  EXPECT(ugo_fecconn_new(128, d, p, 0, &rx2) == UGO_FEC_OK);
+  if (!tx || !rx1 || !rx2) return;
+  std::vector<uint8_t> out1(size_t(batch + 1) * d * L), out2(size_t(batch + 1) * d * L);
+  int nrec = 0;
+  size_t rl = 0;
+  EXPECT(ugo_fecconn_set_batch(rx2, batch, out2.data(), out2.size(), &nrec, &rl) == UGO_FEC_OK);
+  std::vector<std::vector<uint8_t>> grp(n, std::vector<uint8_t>(L));
+  std::vector<std::vector<uint8_t>> wire, sent;
+  for (int g = 0; g < 40; ++g) {
+    for (int k = 0; k < d; ++k) {
+      for (auto& x : grp[k]) x = rb();
+      EXPECT(ugo_fecconn_mark_data(tx, grp[k].data()) == UGO_FEC_OK);
+      sent.push_back(grp[k]);
+    }
+    std::vector<uint8_t*> ptrs(n);
+    std::vector<size_t> lens(n, L);
+    for (int k = 0; k < n; ++k) ptrs[k] = grp[k].data();
+    EXPECT(ugo_fecconn_calc_ecc(tx, ptrs.data(), lens.data(), n, 6, static_cast<int>(L)) == UGO_FEC_OK);
+    for (int k = d; k < n; ++k) EXPECT(ugo_fecconn_mark_fec(tx, grp[k].data()) == UGO_FEC_OK);
+    for (int k = 0; k < n; ++k) {
+      if (rng() % 100 < 12) continue;  // lost
+      wire.push_back(grp[k]);
+      if (rng() % 100 < 5) wire.push_back(grp[k]);  // duplicated
+    }
+  }
+  std::vector<std::vector<uint8_t>> rec1, rec2;
+  for (const auto& w : wire) {
+    uint32_t seq;
+    uint16_t flag;
+    EXPECT(ugo_fecconn_input(rx1, w.data(), w.size(), &seq, &flag, out1.data(), out1.size(), &nrec, &rl) ==
+           UGO_FEC_OK);
+    for (int i = 0; i < nrec; ++i) rec1.emplace_back(out1.data() + i * L, out1.data() + i * L + rl);
+    EXPECT(ugo_fecconn_input(rx2, w.data(), w.size(), &seq, &flag, out2.data(), out2.size(), &nrec, &rl) ==
+           UGO_FEC_OK);
+    for (int i = 0; i < nrec; ++i) rec2.emplace_back(out2.data() + i * L, out2.data() + i * L + rl);
+  }
+  EXPECT(ugo_fecconn_flush(rx2, out2.data(), out2.size(), &nrec, &rl) == UGO_FEC_OK);
+  for (int i = 0; i < nrec; ++i) rec2.emplace_back(out2.data() + i * L, out2.data() + i * L + rl);
+  size_t a = 0, b = 0;
+  EXPECT(ugo_fecconn_rx_len(rx1, &a) == UGO_FEC_OK && ugo_fecconn_rx_len(rx2, &b) == UGO_FEC_OK && a == b);
+  EXPECT(rec1 == rec2);
+  EXPECT(!rec1.empty());
+  for (const auto& r : rec1) {  // a recovered shard is a sent payload (packet bytes [6, L))
+    bool found = false;
+    for (const auto& s : sent)
+      if (std::memcmp(s.data() + 6, r.data(), L - 6) == 0) {
+        found = true;
+        break;
+      }
+    EXPECT(found);
+  }
+  ugo_fecconn_free(tx);
+  ugo_fecconn_free(rx1);
+  ugo_fecconn_free(rx2);
+}
+
+// TX assembly -> RX assembly -> data-only reconstruct into: the data packets'
+// payloads come back, pinned buffers used zero-copy
+void tx_rx_batch() {
+  const int d = 10, p = 3, n = 13;
+  const size_t G = 64, max_len = 1476, slot = 1488, S = max_len - 6, pitch = 1472;
+  ugo_fec* ctx = nullptr;
+  EXPECT(ugo_fec_create(0, d, p, &ctx) == UGO_FEC_OK);
+  if (!ctx) return;
+  auto pin = [](size_t bytes) {
+    void* v = nullptr;
+    EXPECT(ugo_fec_host_alloc(bytes, &v) == UGO_FEC_OK);
+    return static_cast<uint8_t*>(v);
+  };
+  uint8_t* pkts = pin(G * d * slot);
+  uint8_t* wire = pin(G * n * slot);
+  auto* lens = reinterpret_cast<uint16_t*>(pin(G * d * 2));
+  auto* wlens = reinterpret_cast<uint16_t*>(pin(G * n * 2));
+  auto* status = reinterpret_cast<int8_t*>(pin(G));
+  uint8_t* pad = pin(slot);
+  EXPECT(ugo_fec_rc4_keystream(reinterpret_cast<const uint8_t*>("1234567890123456"), 16, pad, slot) == UGO_FEC_OK);
+  for (size_t i = 0; i < G * d * slot; ++i) pkts[i] = rb();
+  for (size_t i = 0; i < G * d; ++i) lens[i] = static_cast<uint16_t>(max_len);
+  EXPECT(ugo_fec_tx_assemble(ctx, pkts, slot, lens, G, 0, pad, max_len, wire, slot, wlens, status, nullptr) ==
+         UGO_FEC_OK);
+  EXPECT(hipDeviceSynchronize() == hipSuccess);
+  for (size_t g = 0; g < G; ++g) EXPECT(status[g] == 0);
+  // drop one data packet per group from the ring
+  std::vector<size_t> keep;
+  for (size_t g = 0; g < G; ++g)
+    for (int r = 0; r < n; ++r)
+      if (r != static_cast<int>(g % d)) keep.push_back(g * n + r);
+  uint8_t* ring = pin(keep.size() * slot);
+  auto* rlens = reinterpret_cast<uint16_t*>(pin(keep.size() * 2));
+  for (size_t i = 0; i < keep.size(); ++i) {
+    std::memcpy(ring + i * slot, wire + keep[i] * slot, slot);
+    rlens[i] = wlens[keep[i]];
+  }
+  uint8_t* shards = pin(n * G * pitch);
+  auto* present = reinterpret_cast<uint64_t*>(pin(G * 8));
+  auto* stats = reinterpret_cast<uint32_t*>(pin(5 * 4));
+  std::memset(present, 0, G * 8);
+  std::memset(stats, 0, 20);
+  EXPECT(ugo_fec_rx_assemble(ctx, ring, slot, rlens, keep.size(), pad, 0, G, shards, S, G * pitch, pitch, present,
+                             stats, nullptr) == UGO_FEC_OK);
+  EXPECT(hipDeviceSynchronize() == hipSuccess);
+  EXPECT(stats[0] == keep.size());
+  uint8_t* out = pin(p * G * pitch);
+  EXPECT(ugo_fec_reconstruct_into(ctx, shards, present, G, S, G * pitch, pitch, out, G * pitch, pitch,
+                                  UGO_FEC_RECONSTRUCT_DATA_ONLY, status, nullptr) == UGO_FEC_OK);
+  EXPECT(hipDeviceSynchronize() == hipSuccess);
+  bool same = true;
+  for (size_t g = 0; g < G && same; ++g) {
+    const size_t k = g % d;  // the lost data packet: output 0 of its group
+    same = std::memcmp(out + g * pitch, pkts + (g * d + k) * slot + 6, S) == 0;
+  }
+  EXPECT(same);
+  for (uint8_t* q : {pkts, wire, reinterpret_cast<uint8_t*>(lens), reinterpret_cast<uint8_t*>(wlens),
+                     reinterpret_cast<uint8_t*>(status), pad, ring, reinterpret_cast<uint8_t*>(rlens), shards,
+                     reinterpret_cast<uint8_t*>(present), reinterpret_cast<uint8_t*>(stats), out})
+    ugo_fec_host_free(q);
+  ugo_fec_destroy(ctx);
+}
+
+}  // namespace
+
+int main() {
+  check_shards_cases();
+  null_args();
+  for (bool pinned : {true, false}) {
+    host_round_trip(10, 3, 1350, 300, pinned);
+    host_round_trip(10, 3, 1470, 1, pinned);
+    host_round_trip(4, 2, 77, 7, pinned);
+    host_round_trip(32, 8, 9000, 12, pinned);
+    host_round_trip(20, 9, 1100, 33, pinned);
+  }
+  fec_object(1);
+  fec_object(16);
+  tx_rx_batch();
+  std::printf("{\"asan_driver\": \"%s\", \"failures\": %d}\n", failures ? "FAIL" : "ok", failures);
+  return failures ? 1 : 0;
+}
