@@ -617,6 +617,11 @@ int main(int argc, char** argv) {
         vars.push_back({"COLD OCC3 enc block 128, 8 rows, 13-row stage (26 KiB: 6 blocks = 12 waves/CU)", enc_bytes, [=]() {
           hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 128, 13>), dim3(g128), dim3(128), 0, 0, rot[(*cnt)++ & 3]); }, {}});
       }
+      for (uint32_t bpc : {5u, 4u, 3u}) {  // the compute-free encode pattern (8 LDS-DMA rows: 32 KiB)
+        const uint32_t x = bpc == 5 ? 0u : (160u * 1024u / bpc - 32u * 1024u - 1024u);
+        vars.push_back({"COLD OCC PATTERN enc (no GF), exactly " + std::to_string(bpc) + " blocks/CU", enc_bytes, [=]() {
+          hipLaunchKernelGGL((k_pattern_enc<8, 2>), dim3(grid), dim3(256), x, 0, rot[(*cnt)++ & 3]); }, {}});
+      }
       vars.push_back({"COLD OCC enc 20-row stage (2 blocks/CU) alone", enc_bytes, [=]() {
         hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 20>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
       for (uint32_t bpc : {4u, 3u}) {  // survivors by LDS-DMA (10 rows: 40 KiB, 4 blocks/CU natively)
