@@ -622,6 +622,17 @@ int main(int argc, char** argv) {
         vars.push_back({"COLD OCC PATTERN enc (no GF), exactly " + std::to_string(bpc) + " blocks/CU", enc_bytes, [=]() {
           hipLaunchKernelGGL((k_pattern_enc<8, 2>), dim3(grid), dim3(256), x, 0, rot[(*cnt)++ & 3]); }, {}});
       }
+      {  // 2 KiB per wave per row (2 chunks per lane): fewer distinct DRAM pages in flight per byte
+        const uint32_t g2 = (pl.items + 511) / 512;
+        for (uint32_t bpc : {4u, 3u, 2u}) {
+          const uint32_t x = 160u * 1024u / bpc - 1024u;
+          vars.push_back({"COLD OCC4 enc 2 chunks/lane nt3, exactly " + std::to_string(bpc) + " blocks/CU", enc_bytes,
+                          [=]() { hipLaunchKernelGGL((k_encode_cpt<2, 3>), dim3(g2), dim3(256), x, 0, rot[(*cnt)++ & 3]); },
+                          {}});
+        }
+        vars.push_back({"COLD OCC4 enc 2 chunks/lane nt3, natural", enc_bytes,
+                        [=]() { hipLaunchKernelGGL((k_encode_cpt<2, 3>), dim3(g2), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      }
       vars.push_back({"COLD OCC enc 20-row stage (2 blocks/CU) alone", enc_bytes, [=]() {
         hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 20>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
       for (uint32_t bpc : {4u, 3u}) {  // survivors by LDS-DMA (10 rows: 40 KiB, 4 blocks/CU natively)
