@@ -74,6 +74,8 @@ def parse(argv=None):
                          "k mod B). With B >= 2 every step meets a cold batch, as a fresh batch of packets is: "
                          "none of its lines are in the 256-MB Infinity Cache. B = 1 re-runs one batch, and the "
                          "cache then absorbs part of the rewritten parity (DESIGN.md §4)")
+    ap.add_argument("--row-pad", type=int, default=0,
+                    help="planar layout: bytes added between consecutive row streams (row stride G*pitch + this)")
     ap.add_argument("--layout", choices=["planar", "interleaved"], default="planar",
                     help="planar = shard-major [d+p][G][pitch] batch; interleaved = [G][d+p][pitch]")
     ap.add_argument("--decode", choices=["inplace", "into"], default="into",
@@ -430,7 +432,15 @@ def run_rank(args):
     planar = args.layout == "planar"
     shape = (n, G, pitch) if planar else (G, n, pitch)
     nb = max(1, args.batches)
-    batches = [torch.randint(0, 256, shape, dtype=torch.uint8, device=dev, generator=gen) for _ in range(nb)]
+    def new_batch():
+        if not planar or args.row_pad == 0:
+            return torch.randint(0, 256, shape, dtype=torch.uint8, device=dev, generator=gen)
+        # planar rows args.row_pad bytes further apart than G*pitch: a strided view
+        rs = G * pitch + args.row_pad
+        flat = torch.randint(0, 256, (n * rs,), dtype=torch.uint8, device=dev, generator=gen)
+        return flat.as_strided((n, G, pitch), (rs, pitch, 1))
+
+    batches = [new_batch() for _ in range(nb)]
     shards = batches[0]
     masks, erased = make_masks(G, n, e, args.seed + 1000 + rank, dev)
     into = args.decode == "into"
@@ -560,6 +570,7 @@ def run_rank(args):
                                    + workload, "groups_per_gpu": G, "total_groups": total_groups,
                        "data_shards": d, "parity_shards": p, "shard_size": S, "pitch": pitch, "erasures": e,
                        "layout": "shard-major [d+p][G][pitch]" if planar else "group-major [G][d+p][pitch]",
+                       "row_stride": (G * pitch + args.row_pad) if planar else pitch,
                        "batches_per_gpu": nb, "decode": args.decode,
                        "parallelism": f"dp{world} (independent packet groups, no collective)"},
             "clock_warmup_ms": round(cw_ms, 1), "clock_warmup_steps": cw_steps, "clock_settled": cw_settled,

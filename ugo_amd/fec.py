@@ -209,15 +209,17 @@ class Encoder:
 
     # -------------------------------------------------- device-resident batch
     def _geom(self, shards, shard_major: bool):
-        """(groups, pitch, row_stride, group_stride) of a contiguous uint8 tensor:
-        group-major [G, d+p, pitch] or shard-major [d+p, G, pitch] (planar)."""
-        assert shards.is_contiguous() and shards.dim() == 3 and shards.element_size() == 1
+        """(groups, pitch, row_stride, group_stride) of a uint8 tensor whose
+        last dimension is contiguous: group-major [G, d+p, pitch] or
+        shard-major [d+p, G, pitch] (planar); the row and group strides are the
+        tensor's own (a padded row stride is a strided view)."""
+        assert shards.dim() == 3 and shards.element_size() == 1 and shards.stride(2) == 1
         if shard_major:
             n, G, pitch = shards.shape
-            rs, gs = G * pitch, pitch
+            rs, gs = shards.stride(0), shards.stride(1)
         else:
             G, n, pitch = shards.shape
-            rs, gs = pitch, n * pitch
+            gs, rs = shards.stride(0), shards.stride(1)
         assert n == self.Shards, f"expected {self.Shards} rows per group, got {n}"
         return G, pitch, rs, gs
 
