@@ -243,6 +243,21 @@ __global__ __launch_bounds__(256) void k_apply_gq(Batch a, Prep pr) {
 
 
 
+// Floor of k_prepare (A/B only): the same grid, staging and mask read, and a
+// header store per group, no descriptor build.
+__global__ __launch_bounds__(64 * kPrepWaves) void k_prep_floor(Prep a, uint32_t groups) {
+  __shared__ PrepShared sh;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  prep_stage(a, sh, threadIdx.x, 64 * kPrepWaves);
+  __syncthreads();
+  const uint32_t gl = blockIdx.x * kPrepWaves + w;
+  if (gl >= groups) return;
+  const uint64_t g = a.g0 + gl;
+  const uint64_t mask = a.present[g] & a.nmask;
+  if (lane == 0)
+    *reinterpret_cast<uint32_t*>(a.desc + (g - a.g_desc0) * a.desc_stride) = __popcll(mask) | sh.M[lane] << 24;
+}
+
 int main(int argc, char** argv) {
   const int d = 32, p = 8, n = 40;
   const uint32_t S = 9000, pitch = 9008;
@@ -304,6 +319,7 @@ int main(int argc, char** argv) {
   Prep pr{};
   pr.desc = d_work; pr.present = masks; pr.M = d_M; pr.gf_exp = d_gf; pr.gf_log = d_gf + 512; pr.g0 = 0;
   pr.g_desc0 = 0; pr.nmask = a.nmask; pr.desc_stride = stride; pr.d = d; pr.n = n; pr.dpad = dpad; pr.epad = epad;
+  CK(hipMemset(d_work, 0xEE, G * stride));
   CK(launch_prepare(pr, G, 0));
   CK(hipDeviceSynchronize());
   const double enc_bytes = double(G) * n * S, dec_bytes = dec_rows * S;
@@ -350,7 +366,14 @@ int main(int argc, char** argv) {
   }
   add(k_apply_q<8, 2, 0, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt0");
   add(k_apply<32, 2, 3>, ar, dec_bytes, "dec masked-horner k_apply nt3 (before)");
+  // (round 2: the log-domain build, 21.0 us, against the table-product build with
+  // serial loops, 23.8 us, byte-identical descriptors: profiles/r2/jvariants_prepare_v2.jsonl)
   vars.push_back({"k_prepare (8192 groups)", 0.0, [=]() { launch_prepare(pr, G, 0); }, {}});
+  Prep pf = pr;  // own workspace: the timed decode variants read d_work
+  CK(hipMalloc(&pf.desc, G * stride + 64));
+  vars.push_back({"k_prepare FLOOR (staging + mask read + header store, no build)", 0.0, [=]() {
+    hipLaunchKernelGGL(k_prep_floor, dim3((G + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0, 0, pf,
+                       static_cast<uint32_t>(G)); }, {}});
   {  // fused descriptor build, one group per block (k_apply_gq, A/B only)
     const uint32_t passes = (a.chunks + 255) / 256, bs = 64 * ((a.chunks + 64 * passes - 1) / (64 * passes));
     Batch af = a;

@@ -623,11 +623,6 @@ __global__ __launch_bounds__(256) void k_apply_bytes(Batch a) {
 // over GF(2^8) in LDS, then coefficient rows: Dinv[r] for an erased data row r,
 // M[r] * Dinv for an erased parity row r.  d + p <= 64, so d <= 63 rows fit
 // the wave's lanes one row per lane.
-__device__ __forceinline__ uint8_t lmul(const uint8_t* lg, const uint8_t* ex, uint32_t a,
-                                        uint32_t b) {
-  return (a && b) ? ex[lg[a] + lg[b]] : 0;
-}
-
 // One wave per group.  The survivors are the first d present rows: the
 // present data rows P (identity rows of M) then the first e_d present parity
 // rows J, where e_d = number of erased data rows E.  So the d x d inverse
@@ -652,9 +647,17 @@ struct PrepShared {     // per block: staged once, read by every wave
 struct PrepWave {       // per wave (per group being built)
   uint8_t Ba[32 * 64];  // [B | I], e_d <= min(d, p) <= 32 since d + p <= 64
   uint8_t DE[32 * 64];  // Dinv rows of the erased data rows, over survivor positions
-  uint8_t fcol[32];
+  uint8_t fcol[32];     // log of column r of the pivot step (255 = zero)
+  uint8_t lrow[64];     // log of pivot row r scaled by 1/pivot
   uint8_t surv[64], outr[64], Pl[64], El[64], Jl[64];
 };
+
+// Branch-free product: the lookups always run (lg[0] is a valid byte), the
+// select zeroes them, so a lane never diverges around an LDS read.
+__device__ __forceinline__ uint32_t lmul(const uint8_t* lg, const uint8_t* ex, uint32_t a, uint32_t b) {
+  const uint32_t t = ex[lg[a] + lg[b]];
+  return (a && b) ? t : 0u;
+}
 
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -721,32 +724,52 @@ __device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr des
     s.Ba[idx] = col < ed ? M[s.Jl[i] * d + s.El[col]] : static_cast<uint8_t>(col - ed == i ? 1 : 0);
   }
   wsync();
-  for (uint32_t r = 0; r < ed; ++r) {
-    if (s.Ba[r * w + r] == 0) {  // uniform branch (every lane reads the same byte)
-      const bool cand = lane > r && lane < ed && s.Ba[lane * w + r] != 0;
-      const uint64_t bal = __ballot(cand);
-      if (bal == 0) {  // singular: cannot happen for an MDS code
-        if (lane == 0) *reinterpret_cast<uint32_t*>(desc) = 7u << 16;
-        return;
+  {
+    // Log-domain pivot step, 4 dependent LDS round trips: (pivot, row r,
+    // column r) -> their logs -> [store, sync] -> (row log, column log, entry)
+    // -> exp.  Row r is scaled by 1/pivot inside the logs, so every entry of
+    // the step is one product.  Pivots of an MDS code's B are never zero
+    // (every leading block is a square submatrix of the parity rows); the
+    // swap stays for safety.
+    for (uint32_t r = 0; r < ed; ++r) {
+      uint32_t piv = s.Ba[r * w + r];
+      uint32_t x = lane < w ? s.Ba[r * w + lane] : 0u;
+      uint32_t y = lane < ed ? s.Ba[lane * w + r] : 0u;
+      if (piv == 0) {  // uniform
+        const bool cand = lane > r && lane < ed && y != 0;
+        const uint64_t bal = __ballot(cand);
+        if (bal == 0) {
+          if (lane == 0) *reinterpret_cast<uint32_t*>(desc) = 7u << 16;
+          return;
+        }
+        const uint32_t b = __ffsll(static_cast<long long>(bal)) - 1;
+        if (lane < w) {
+          const uint8_t t = s.Ba[b * w + lane];
+          s.Ba[b * w + lane] = static_cast<uint8_t>(x);
+          s.Ba[r * w + lane] = t;
+        }
+        wsync();
+        piv = s.Ba[r * w + r];
+        x = lane < w ? s.Ba[r * w + lane] : 0u;
+        y = lane < ed ? s.Ba[lane * w + r] : 0u;
       }
-      const uint32_t b = __ffsll(static_cast<long long>(bal)) - 1;
-      for (uint32_t col = lane; col < w; col += 64) {
-        const uint8_t t = s.Ba[r * w + col];
-        s.Ba[r * w + col] = s.Ba[b * w + col];
-        s.Ba[b * w + col] = t;
+      const uint32_t pinv = 255u - sh.lg[piv];
+      const uint32_t lx = lg[x], ly = lg[y];
+      uint32_t t = lx + pinv;
+      t = t >= 255u ? t - 255u : t;
+      if (lane < w) s.lrow[lane] = static_cast<uint8_t>(x ? t : 255u);
+      if (lane < ed) s.fcol[lane] = static_cast<uint8_t>(y ? ly : 255u);
+      wsync();
+#pragma unroll 2
+      for (uint32_t idx = lane; idx < ed * w; idx += 64) {
+        const uint32_t o = idx / w, col = idx - o * w;
+        const uint32_t lr = s.lrow[col], lc = s.fcol[o], cur = s.Ba[idx];
+        const uint32_t pr = ex[lr + (o == r ? 0u : lc)];
+        const uint32_t pz = (lr == 255u || lc == 255u) ? 0u : pr;
+        s.Ba[idx] = static_cast<uint8_t>(o == r ? (lr == 255u ? 0u : pr) : cur ^ pz);
       }
       wsync();
     }
-    const uint32_t sc = ex[255 - lg[s.Ba[r * w + r]]];  // 1 / pivot
-    wsync();
-    for (uint32_t col = lane; col < w; col += 64) s.Ba[r * w + col] = lmul(lg, ex, sc, s.Ba[r * w + col]);
-    if (lane < ed) s.fcol[lane] = s.Ba[lane * w + r];
-    wsync();
-    for (uint32_t idx = lane; idx < ed * w; idx += 64) {
-      const uint32_t o = idx / w, col = idx - o * w;
-      if (o != r) s.Ba[idx] ^= lmul(lg, ex, s.fcol[o], s.Ba[r * w + col]);
-    }
-    wsync();
   }
   // Dinv rows of the erased data rows (Binv = Ba[:, ed:])
   for (uint32_t idx = lane; idx < ed * d; idx += 64) {
@@ -756,7 +779,11 @@ __device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr des
       v = s.Ba[l * w + ed + (pos - npd)];
     } else {
       v = 0;
-      for (uint32_t i = 0; i < ed; ++i) v ^= lmul(lg, ex, s.Ba[l * w + ed + i], M[s.Jl[i] * d + s.Pl[pos]]);
+      const uint32_t pc = s.Pl[pos];
+      uint32_t acc = 0;
+#pragma unroll 4
+      for (uint32_t i = 0; i < ed; ++i) acc ^= lmul(lg, ex, s.Ba[l * w + ed + i], M[s.Jl[i] * d + pc]);
+      v = static_cast<uint8_t>(acc);
     }
     s.DE[l * 64 + pos] = v;
   }
@@ -776,7 +803,10 @@ __device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr des
       } else {
         const uint32_t r = s.outr[i];
         if (pos < npd) v = M[r * d + s.Pl[pos]];
-        for (uint32_t l = 0; l < ed; ++l) v ^= lmul(lg, ex, M[r * d + s.El[l]], s.DE[l * 64 + pos]);
+        uint32_t acc = v;
+#pragma unroll 4
+        for (uint32_t l = 0; l < ed; ++l) acc ^= lmul(lg, ex, M[r * d + s.El[l]], s.DE[l * 64 + pos]);
+        v = static_cast<uint8_t>(acc);
       }
     }
     coef[idx] = v;
