@@ -151,7 +151,8 @@ def test_reconstruct_inconsistent_inputs(gpu, table_max, monkeypatch):
                                          (20, 4, 200, 208), (32, 8, 9000, 9008), (3, 1, 50, 50),
                                          (40, 6, 70, 80), (1, 1, 7, 16), (7, 0, 32, 32),
                                          (5, 3, 1500, 1504), (8, 4, 4096, 4096), (16, 4, 1030, 1040),
-                                         (56, 8, 256, 256)])  # d+p = 64: the widest presence mask
+                                         (56, 8, 256, 256),  # d+p = 64: the widest presence mask
+                                         (24, 8, 2040, 2048)])  # 128 chunks: k_apply_qa, no idle lane
 def test_generic_geometries(gpu, d, p, S, pitch):
     n = d + p
     G = 300
@@ -446,7 +447,11 @@ def test_more_than_64_shards_encode_only(gpu):
 @pytest.mark.parametrize("d,p,S,pitch,opitch,shard_major,table_max",
                          [(10, 3, 1350, 1360, 1360, True, "16"),    # headline kernel (k_apply_p)
                           (10, 3, 1350, 1360, 1360, False, "0"),    # k_prepare + per-group descriptors
-                          (32, 8, 9000, 9008, 9008, True, "16"),    # jumbo streaming kernel (k_apply_q)
+                          (32, 8, 9000, 9008, 9008, True, "16"),    # jumbo: wave-aligned groups (k_apply_qa)
+                          (32, 8, 1000, 1008, 1024, False, "16"),   # 63 chunks: k_apply_qa, 1 idle lane per group
+                          (10, 6, 1008, 1008, 1008, True, "16"),    # MODE 1 table, p > 4: k_apply_qa
+                          (20, 4, 2000, 2000, 2016, False, "16"),   # MODE 2, e <= 4: k_apply_qa<4>
+                          (16, 4, 1030, 1040, 1040, True, "16"),    # 65 chunks: streaming k_apply_q
                           (10, 3, 1350, 1353, 1355, False, "16"),   # unaligned: byte kernel
                           (6, 2, 77, 80, 96, True, "16"),           # rows < 64 chunks: k_apply
                           (12, 4, 1030, 1040, 1040, False, "16"),   # p = 4

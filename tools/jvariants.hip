@@ -14,90 +14,7 @@
 using namespace ugo;
 using namespace ugo::kern;
 
-// (A/B only, round 2: 549.0 vs 544.7 us production, profiles/r2/jvariants_wave_aligned.jsonl;
-// VALU per wave down ~28% but 113 VGPRs -> 4 waves/SIMD, spills at 5.)
-// Wave-aligned form of k_apply_q for rows whose chunk count is just under a
-// multiple of 64 ((32,8) x 9000: 563 of 576 lanes busy): every group starts at
-// a wave boundary (item = group * cpad + chunk, cpad = chunks rounded up to
-// 64), so a wave never spans two groups.  Its descriptor is wave-uniform, the
-// table words stay SGPRs and each v_perm reads its low word from the constant
-// bus: 4 VGPR copies per product pair instead of the 10 of k_apply_q, whose
-// merged uniform / two-group paths make every table word a VGPR (DESIGN.md
-// §3.4).  Lanes past the row's end load chunk 0 and store nothing.
-template <int EMAX, int MODE, int NT, int RING = 4>
-__global__ __launch_bounds__(256) void k_apply_qa(Batch a) {
-  static_assert(RING % 2 == 0, "inputs are consumed in pairs");
-  const uint32_t cpad = (a.chunks + 63u) & ~63u;
-  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
-  if (wfirst >= a.items) return;  // a.items = groups * cpad here
-  const uint32_t gl = wfirst / cpad;  // wave-uniform
-  const uint64_t g = a.g0 + gl;
-  const uint8_t* dA = desc_for<MODE>(a, g);
-  const uint32_t hA = ld32(dA);
-  const uint32_t st = (hA >> 16) & 0xffu;
-  const uint32_t e = st ? 0u : (a.data_only ? ((hA >> 8) & 0xffu) : (hA & 0xffu));
-  const uint32_t c = blockIdx.x * 256u + threadIdx.x - gl * cpad;
-  const bool live = c < a.chunks;
-  const bool wst = MODE != 0 && a.status != nullptr && c == 0;
-  if (e == 0) {  // wave-uniform
-    if (wst) a.status[g] = static_cast<int8_t>(st);
-    return;
-  }
-  const uint32_t coff = live ? c * 16u : 0u;
-  uint8_t* gp = a.base + g * a.gstride + coff;
-  auto load_in = [&](uint32_t k) -> V4 {
-    if (k >= a.d) return V4{{0u, 0u, 0u, 0u}};
-    const uint32_t r = (ld32(dA + 4 + (k & ~3u)) >> (8 * (k & 3u))) & 0xffu;
-    return load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
-  };
-  V4 acc[EMAX];
-#pragma unroll
-  for (int i = 0; i < EMAX; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
-  V4 ring[RING];
-#pragma unroll
-  for (int j = 0; j < RING; ++j) ring[j] = load_in(j);
-  const uint32_t cbase = 4 + a.dpad + a.epad;
-  for (uint32_t k0 = 0; k0 < a.d; k0 += RING) {
-#pragma unroll
-    for (int j = 0; j < RING; j += 2) {
-      const uint32_t k = k0 + j;
-      uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
-      p_sel(ring[j], s0, s1, s2);
-      p_sel(ring[j + 1], r0, r1, r2);
-      ring[j] = load_in(k + RING);
-      ring[j + 1] = load_in(k + RING + 1);
-#pragma unroll
-      for (int i = 0; i < EMAX; ++i) {
-        if (i >= static_cast<int>(e)) continue;
-        const uint32_t off = cbase + i * a.dpad + (k & ~3u);  // coefficient word of inputs k, k+1
-        uint32_t t[5], u[5];
-        p_tables<0>(t, a, dA, dA, off, j & 3, 0u);
-        p_tables<0>(u, a, dA, dA, off, (j & 3) + 1, 0u);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint32_t y = xor3(acc[i].v[q], perm(t[1], t[0], s0[q]), perm(t[3], t[2], s1[q]));
-          y = xor3(y, perm(0u, t[4], s2[q]), perm(u[1], u[0], r0[q]));
-          acc[i].v[q] = xor3(y, perm(u[3], u[2], r1[q]), perm(0u, u[4], r2[q]));
-        }
-      }
-    }
-  }
-  if (live) {
-    const uint32_t nb = a.S - coff;
-    constexpr int NO = (EMAX + 3) / 4;
-    uint32_t orw[NO];
-#pragma unroll
-    for (int w = 0; w < NO; ++w) orw[w] = ld32(dA + 4 + a.dpad + 4 * w);
-#pragma unroll
-    for (int i = 0; i < EMAX; ++i) {
-      if (i >= static_cast<int>(e)) continue;
-      const uint32_t r = (orw[i >> 2] >> (8 * (i & 3))) & 0xffu;
-      store16<NT>(out_row(a, gp, g, coff, r, i), acc[i], nb);
-    }
-  }
-  if (wst) a.status[g] = 0;
-}
-
+// k_apply_qa (wave-aligned groups) is production since round 2 (fec_kernels.hip).
 
 // ---------------------------------------------- k_apply_gq (A/B only)
 // Round-2 attempt at fusing k_prepare into the jumbo apply:
@@ -339,6 +256,7 @@ int main(int argc, char** argv) {
   add(k_apply_q<8, 2, 1, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt1");
   add(k_apply_q<8, 2, 1, 1, 8>, ar, dec_bytes, "dec perm streaming ring8 nt1");
   add(k_apply_q<8, 2, 3, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt3 (production)");
+  add(k_apply_q<8, 2, 3, 1, 2>, ar, dec_bytes, "dec perm streaming ring2 nt3");
   {  // residency caps (round 2): dynamic LDS so that exactly `bpc` blocks fit a CU
     auto cap = [](uint32_t bpc, uint32_t static_kib) { return 160u * 1024u / bpc - static_kib * 1024u - 1024u; };
     for (uint32_t bpc : {4u, 3u, 2u}) {
@@ -362,13 +280,26 @@ int main(int argc, char** argv) {
     aa.items = G * ((a.chunks + 63) / 64 * 64);
     const uint32_t ga = (aa.items + 255) / 256;
     vars.push_back({"dec perm streaming ring4 nt3, WAVE-ALIGNED groups (k_apply_qa)", dec_bytes, [=]() {
-      hipLaunchKernelGGL((k_apply_qa<8, 2, 3>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+      hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 4>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+    vars.push_back({"dec k_apply_qa ring4 waves_per_eu 5", dec_bytes, [=]() {
+      hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 4, 5>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+    vars.push_back({"dec k_apply_qa ring2 (production since round 2)", dec_bytes, [=]() {
+      hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+    vars.push_back({"dec k_apply_qa ring2 waves_per_eu 5", dec_bytes, [=]() {
+      hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2, 5>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+    vars.push_back({"dec k_apply_qa ring2 waves_per_eu 6", dec_bytes, [=]() {
+      hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2, 6>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+    vars.push_back({"dec k_apply_qa ring2 waves_per_eu 7", dec_bytes, [=]() {
+      hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2, 7>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   }
   add(k_apply_q<8, 2, 0, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt0");
   add(k_apply<32, 2, 3>, ar, dec_bytes, "dec masked-horner k_apply nt3 (before)");
   // (round 2: the log-domain build, 21.0 us, against the table-product build with
   // serial loops, 23.8 us, byte-identical descriptors: profiles/r2/jvariants_prepare_v2.jsonl)
-  vars.push_back({"k_prepare (8192 groups)", 0.0, [=]() { launch_prepare(pr, G, 0); }, {}});
+  vars.push_back({"k_prepare (8192 groups, production: small tier)", 0.0, [=]() { launch_prepare(pr, G, 0); }, {}});
+  vars.push_back({"k_prepare generic tier (EDM 32, 22.9 KiB LDS) on the jumbo code", 0.0, [=]() {
+    hipLaunchKernelGGL((k_prepare<32, 64 * 64>), dim3((G + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0, 0,
+                       pr, static_cast<uint32_t>(G)); }, {}});
   Prep pf = pr;  // own workspace: the timed decode variants read d_work
   CK(hipMalloc(&pf.desc, G * stride + 64));
   vars.push_back({"k_prepare FLOOR (staging + mask read + header store, no build)", 0.0, [=]() {
@@ -382,9 +313,17 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((k_apply_gq<8, 3>), dim3(G), dim3(bs), 0, 0, af, pr); }, {}});
     vars.push_back({"dec fused k_apply_gq, PROBE descriptor copied from k_prepare's workspace", dec_bytes, [=]() {
       hipLaunchKernelGGL((k_apply_gq<8, 3, 4, 1>), dim3(G), dim3(bs), 0, 0, af, pr); }, {}});
-    vars.push_back({"dec k_prepare + k_apply_q (production before)", dec_bytes, [=]() {
+    vars.push_back({"dec k_prepare + k_apply_q (round-2 production before k_apply_qa)", dec_bytes, [=]() {
       launch_prepare(pr, G, 0);
       hipLaunchKernelGGL((k_apply_q<8, 2, 3, 1, 4>), dim3(grid), dim3(256), 0, 0, ar); }, {}});
+    {
+      Batch aa = ar;
+      aa.items = G * ((a.chunks + 63) / 64 * 64);
+      const uint32_t ga = (aa.items + 255) / 256;
+      vars.push_back({"dec k_prepare + k_apply_qa ring2 (production)", dec_bytes, [=]() {
+        launch_prepare(pr, G, 0);
+        hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+    }
   }
   // encode variants must agree: run const then perm encode over the same data
   auto same_rows = [&](const std::vector<uint8_t>& x, const std::vector<uint8_t>& y) {  // bytes [0, S) only

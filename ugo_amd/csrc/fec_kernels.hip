@@ -541,13 +541,15 @@ __global__ __launch_bounds__(256) void k_apply_q(Batch a) {
       for (int i = 0; i < EMAX; ++i) {
         if (i >= static_cast<int>(emax)) continue;
         const uint32_t off = cbase + i * a.dpad + (k & ~3u);  // coefficient word of inputs k, k+1
+        // byte of input k in that word (compile-time when the ring is a multiple of 4)
+        const int kb = RING % 4 == 0 ? (j & 3) : static_cast<int>(k & 3u);
         uint32_t t[5], u[5];
         if (dS) {
-          p_tables<0>(t, a, dS, dS, off, j & 3, 0u);
-          p_tables<0>(u, a, dS, dS, off, (j & 3) + 1, 0u);
+          p_tables<0>(t, a, dS, dS, off, kb, 0u);
+          p_tables<0>(u, a, dS, dS, off, kb + 1, 0u);
         } else {
-          p_tables<TSEL>(t, a, dA, dB, off, j & 3, mB);
-          p_tables<TSEL>(u, a, dA, dB, off, (j & 3) + 1, mB);
+          p_tables<TSEL>(t, a, dA, dB, off, kb, mB);
+          p_tables<TSEL>(u, a, dA, dB, off, kb + 1, mB);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -570,6 +572,92 @@ __global__ __launch_bounds__(256) void k_apply_q(Batch a) {
     if (i >= static_cast<int>(e)) continue;
     const uint32_t r = (orw[i >> 2] >> (8 * (i & 3))) & 0xffu;
     store16<NT>(out_row(a, gp, g, c * 16u, r, i), acc[i], nb);
+  }
+  if (wst) a.status[g] = 0;
+}
+
+// Wave-aligned form of k_apply_q, for rows whose chunk count is just under a
+// multiple of 64 ((32,8) x 9000: 563 of 576 lanes busy): every group starts
+// at a wave boundary (item = group * cpad + chunk, cpad = chunks rounded up to
+// 64; the launcher sets items = groups * cpad), so a wave never spans two
+// groups.  Its descriptor is wave-uniform, the table words stay SGPRs and each
+// v_perm reads its low word from the constant bus: 4 VGPR copies per product
+// pair instead of the 10 of k_apply_q, whose merged uniform / two-group paths
+// make every table word a VGPR.  A 2-deep input ring keeps it at 79 VGPRs (6
+// waves/SIMD; the 4-deep ring takes 113 and 4 waves): 533.5 against 550.4 us
+// for the jumbo reconstruct (profiles/r2/jvariants_qa_ring2.jsonl).  Lanes
+// past the row's end load chunk 0 and store nothing.
+template <int EMAX, int MODE, int NT, int RING = 2, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_qa(Batch a) {
+  static_assert(RING % 2 == 0, "inputs are consumed in pairs");
+  const uint32_t cpad = (a.chunks + 63u) & ~63u;
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  if (wfirst >= a.items) return;  // a.items = groups * cpad here
+  const uint32_t gl = wfirst / cpad;  // wave-uniform
+  const uint64_t g = a.g0 + gl;
+  const uint8_t* dA = desc_for<MODE>(a, g);
+  const uint32_t hA = ld32(dA);
+  const uint32_t st = (hA >> 16) & 0xffu;
+  const uint32_t e = st ? 0u : (a.data_only ? ((hA >> 8) & 0xffu) : (hA & 0xffu));
+  const uint32_t c = blockIdx.x * 256u + threadIdx.x - gl * cpad;
+  const bool live = c < a.chunks;
+  const bool wst = MODE != 0 && a.status != nullptr && c == 0;
+  if (e == 0) {  // wave-uniform
+    if (wst) a.status[g] = static_cast<int8_t>(st);
+    return;
+  }
+  const uint32_t coff = live ? c * 16u : 0u;
+  uint8_t* gp = a.base + g * a.gstride + coff;
+  auto load_in = [&](uint32_t k) -> V4 {
+    if (k >= a.d) return V4{{0u, 0u, 0u, 0u}};
+    const uint32_t r = (ld32(dA + 4 + (k & ~3u)) >> (8 * (k & 3u))) & 0xffu;
+    return load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
+  };
+  V4 acc[EMAX];
+#pragma unroll
+  for (int i = 0; i < EMAX; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
+  V4 ring[RING];
+#pragma unroll
+  for (int j = 0; j < RING; ++j) ring[j] = load_in(j);
+  const uint32_t cbase = 4 + a.dpad + a.epad;
+  for (uint32_t k0 = 0; k0 < a.d; k0 += RING) {
+#pragma unroll
+    for (int j = 0; j < RING; j += 2) {
+      const uint32_t k = k0 + j;
+      uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
+      p_sel(ring[j], s0, s1, s2);
+      p_sel(ring[j + 1], r0, r1, r2);
+      ring[j] = load_in(k + RING);
+      ring[j + 1] = load_in(k + RING + 1);
+#pragma unroll
+      for (int i = 0; i < EMAX; ++i) {
+        if (i >= static_cast<int>(e)) continue;
+        const uint32_t off = cbase + i * a.dpad + (k & ~3u);  // coefficient word of inputs k, k+1
+        const int kb = RING % 4 == 0 ? (j & 3) : static_cast<int>(k & 3u);
+        uint32_t t[5], u[5];
+        p_tables<0>(t, a, dA, dA, off, kb, 0u);
+        p_tables<0>(u, a, dA, dA, off, kb + 1, 0u);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t y = xor3(acc[i].v[q], perm(t[1], t[0], s0[q]), perm(t[3], t[2], s1[q]));
+          y = xor3(y, perm(0u, t[4], s2[q]), perm(u[1], u[0], r0[q]));
+          acc[i].v[q] = xor3(y, perm(u[3], u[2], r1[q]), perm(0u, u[4], r2[q]));
+        }
+      }
+    }
+  }
+  if (live) {
+    const uint32_t nb = a.S - coff;
+    constexpr int NO = (EMAX + 3) / 4;
+    uint32_t orw[NO];
+#pragma unroll
+    for (int w = 0; w < NO; ++w) orw[w] = ld32(dA + 4 + a.dpad + 4 * w);
+#pragma unroll
+    for (int i = 0; i < EMAX; ++i) {
+      if (i >= static_cast<int>(e)) continue;
+      const uint32_t r = (orw[i >> 2] >> (8 * (i & 3))) & 0xffu;
+      store16<NT>(out_row(a, gp, g, coff, r, i), acc[i], nb);
+    }
   }
   if (wst) a.status[g] = 0;
 }
@@ -639,18 +727,27 @@ __global__ __launch_bounds__(256) void k_apply_bytes(Batch a) {
 // `s`.  It synchronises only its own lanes (wsync: a wave's LDS operations
 // complete in order, so a code-motion barrier is enough), so one wave of a
 // larger block can run it while the others do something else.
-struct PrepShared {     // per block: staged once, read by every wave
+template <int NMD>
+struct PrepSharedT {    // per block: staged once, read by every wave
   uint8_t ex[512];
   uint8_t lg[256];
-  uint8_t M[64 * 64];   // the (d+p) x d encoding matrix
+  uint8_t M[NMD];       // the (d+p) x d encoding matrix, NMD >= (d+p) d
 };
-struct PrepWave {       // per wave (per group being built)
-  uint8_t Ba[32 * 64];  // [B | I], e_d <= min(d, p) <= 32 since d + p <= 64
-  uint8_t DE[32 * 64];  // Dinv rows of the erased data rows, over survivor positions
+template <int EDM>
+struct PrepWaveT {      // per wave (per group being built), EDM >= e_d
+  uint8_t Ba[EDM * 2 * EDM];  // [B | I]
+  uint8_t DE[EDM * 64];       // Dinv rows of the erased data rows, over survivor positions
   uint8_t fcol[32];     // log of column r of the pivot step (255 = zero)
   uint8_t lrow[64];     // log of pivot row r scaled by 1/pivot
   uint8_t surv[64], outr[64], Pl[64], El[64], Jl[64];
 };
+// Any code (e_d <= min(d, p) <= 32 since d + p <= 64), and the small tier
+// k_prepare launches for codes with min(d, p) <= 8 and (d+p) d <= 2048 (the
+// (32,8) jumbo): 7 KiB of LDS per block instead of 22.9, so LDS no longer
+// caps the blocks per CU.
+using PrepShared = PrepSharedT<64 * 64>;
+using PrepWave = PrepWaveT<32>;
+constexpr int kPrepSmallEdm = 8, kPrepSmallNmd = 2048, kPrepSmallWpe = 1;
 
 // Branch-free product: the lookups always run (lg[0] is a valid byte), the
 // select zeroes them, so a lane never diverges around an LDS read.
@@ -658,6 +755,14 @@ __device__ __forceinline__ uint32_t lmul(const uint8_t* lg, const uint8_t* ex, u
   const uint32_t t = ex[lg[a] + lg[b]];
   return (a && b) ? t : 0u;
 }
+
+// floor(x / w) for x < 2^11 and 1 <= w <= 64 as a multiply by rw =
+// ceil(2^20 / w): the reciprocal's error, below x / 2^20 < 1/64, cannot carry
+// a quotient past the next integer (the fraction of x / w is at most 1 - 1/w).
+// The descriptor build's index splits would otherwise be ~20-instruction
+// integer divisions, a third of its VALU work.
+__device__ __forceinline__ uint32_t rcp_small(uint32_t w) { return ((1u << 20) + w - 1) / w; }
+__device__ __forceinline__ uint32_t div_small(uint32_t x, uint32_t rw) { return (x * rw) >> 20; }
 
 __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -669,7 +774,8 @@ __device__ __forceinline__ void wsync() {
 // every later read of the descriptor build is an LDS read (global reads
 // inside its dependent loops cost a full memory latency each under load).
 // The caller synchronises before prep_wave reads them.
-__device__ __forceinline__ void prep_stage(const Prep& a, PrepShared& s, uint32_t tid, uint32_t nthr) {
+template <typename PS>
+__device__ __forceinline__ void prep_stage(const Prep& a, PS& s, uint32_t tid, uint32_t nthr) {
   const uint32_t mb = a.n * a.d, m16 = mb / 16;
   for (uint32_t i = tid; i < 32 + 16 + m16; i += nthr) {
     const u32x4* src = i < 32 ? reinterpret_cast<const u32x4*>(a.gf_exp) + i
@@ -683,8 +789,8 @@ __device__ __forceinline__ void prep_stage(const Prep& a, PrepShared& s, uint32_
   for (uint32_t i = m16 * 16 + tid; i < mb; i += nthr) s.M[i] = a.M[i];
 }
 
-template <typename DescPtr>
-__device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr desc, const PrepShared& sh, PrepWave& s,
+template <typename DescPtr, typename PS, typename PW>
+__device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr desc, const PS& sh, PW& s,
                                           uint32_t lane) {
   const uint32_t d = a.d, n = a.n;
   const uint8_t* M = sh.M;
@@ -719,8 +825,9 @@ __device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr des
   if (lane < d) s.surv[lane] = lane < npd ? s.Pl[lane] : s.Jl[lane - npd];
   // [B | I], B[i][l] = M[J_i][E_l]
   const uint32_t w = 2 * ed;
+  const uint32_t rw = rcp_small(w ? w : 1u), rd = rcp_small(d), rdp = rcp_small(a.dpad);  // wave-uniform
   for (uint32_t idx = lane; idx < ed * w; idx += 64) {
-    const uint32_t i = idx / w, col = idx - i * w;
+    const uint32_t i = div_small(idx, rw), col = idx - i * w;
     s.Ba[idx] = col < ed ? M[s.Jl[i] * d + s.El[col]] : static_cast<uint8_t>(col - ed == i ? 1 : 0);
   }
   wsync();
@@ -762,7 +869,7 @@ __device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr des
       wsync();
 #pragma unroll 2
       for (uint32_t idx = lane; idx < ed * w; idx += 64) {
-        const uint32_t o = idx / w, col = idx - o * w;
+        const uint32_t o = div_small(idx, rw), col = idx - o * w;
         const uint32_t lr = s.lrow[col], lc = s.fcol[o], cur = s.Ba[idx];
         const uint32_t pr = ex[lr + (o == r ? 0u : lc)];
         const uint32_t pz = (lr == 255u || lc == 255u) ? 0u : pr;
@@ -773,7 +880,7 @@ __device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr des
   }
   // Dinv rows of the erased data rows (Binv = Ba[:, ed:])
   for (uint32_t idx = lane; idx < ed * d; idx += 64) {
-    const uint32_t l = idx / d, pos = idx - l * d;
+    const uint32_t l = div_small(idx, rd), pos = idx - l * d;
     uint8_t v;
     if (pos >= npd) {
       v = s.Ba[l * w + ed + (pos - npd)];
@@ -795,7 +902,7 @@ __device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr des
   for (uint32_t i = lane; i < epad; i += 64) desc[4 + dpad + i] = i < e ? s.outr[i] : 0;
   DescPtr coef = desc + 4 + dpad + epad;
   for (uint32_t idx = lane; idx < e * dpad; idx += 64) {
-    const uint32_t i = idx / dpad, pos = idx - i * dpad;
+    const uint32_t i = div_small(idx, rdp), pos = idx - i * dpad;
     uint8_t v = 0;
     if (pos < d) {
       if (i < ed) {
@@ -818,9 +925,11 @@ __device__ __forceinline__ void prep_wave(const Prep& a, uint64_t g, DescPtr des
 // (22 KiB of LDS per block).
 constexpr uint32_t kPrepWaves = 4;
 
-__global__ __launch_bounds__(64 * kPrepWaves) void k_prepare(Prep a, uint32_t groups) {
-  __shared__ PrepShared sh;
-  __shared__ PrepWave sw[kPrepWaves];
+template <int EDM, int NMD, int WPE = 1>
+__global__ __launch_bounds__(64 * kPrepWaves) __attribute__((amdgpu_waves_per_eu(WPE))) void k_prepare(Prep a,
+                                                                                                       uint32_t groups) {
+  __shared__ PrepSharedT<NMD> sh;
+  __shared__ PrepWaveT<EDM> sw[kPrepWaves];
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
   prep_stage(a, sh, threadIdx.x, 64 * kPrepWaves);
   __syncthreads();
@@ -893,6 +1002,17 @@ static void launch_apply_dm(const Batch& a, hipStream_t s) {
     }
   }
   if (a.chunks >= 64 && a.epad <= 8) {  // wide codes: streaming inputs
+    const uint32_t cpad = (a.chunks + 63u) & ~63u;
+    if (MODE != 0 && (cpad - a.chunks) * 16u <= cpad) {  // groups wave-aligned at <= 1/16 idle lanes
+      Batch b = a;
+      b.items = (a.items / a.chunks) * cpad;
+      const dim3 ga(blocks_for(b.items, 256));
+      if (a.epad == 4)
+        launch(kKReconstruct, k_apply_qa<4, MODE, kApplyQNT>, ga, block, 0, s, b);
+      else
+        launch(kKReconstruct, k_apply_qa<8, MODE, kApplyQNT>, ga, block, 0, s, b);
+      return;
+    }
     if (a.epad == 4)
       launch(kKReconstruct, k_apply_q<4, MODE, kApplyQNT, 1>, grid, block, 0, s, a);
     else
@@ -944,7 +1064,11 @@ hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s) {
 }
 
 hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s) {
-  launch(kKPrepare, k_prepare, dim3((groups + kPrepWaves - 1) / kPrepWaves), dim3(64 * kPrepWaves), 0, s, a, groups);
+  const dim3 grid((groups + kPrepWaves - 1) / kPrepWaves), block(64 * kPrepWaves);
+  if (std::min(a.d, a.n - a.d) <= static_cast<uint32_t>(kPrepSmallEdm) && a.n * a.d <= static_cast<uint32_t>(kPrepSmallNmd))
+    launch(kKPrepare, k_prepare<kPrepSmallEdm, kPrepSmallNmd, kPrepSmallWpe>, grid, block, 0, s, a, groups);
+  else
+    launch(kKPrepare, k_prepare<32, 64 * 64>, grid, block, 0, s, a, groups);
   return hipGetLastError();
 }
 
