@@ -28,7 +28,8 @@
 //    headline and the (32,8) jumbo geometry (k_encode_g in production).
 //  * k_apply_p<DMAX,MODE>: runtime coefficients through split v_perm_b32
 //    tables (the headline reconstruct), k_apply_q its streaming form for wide
-//    codes.
+//    codes, k_apply_qa the wave-aligned streaming form (the jumbo reconstruct:
+//    rows just under a multiple of 64 chunks, one group per wave).
 //  * k_apply<DMAX,MODE>: coefficients come from a *descriptor* (input rows,
 //    output rows, e x d coefficient matrix).  MODE 0: one descriptor for all
 //    groups (generic encode); MODE 1: descriptor table indexed by the group's
