@@ -248,11 +248,13 @@ int main(int argc, char** argv) {
   };
   add(k_encode_c<32, 8, 1>, a, enc_bytes, "enc const-network nt1");
   add(k_encode_c<32, 8, 3>, a, enc_bytes, "enc const-network nt3");
-  add(k_encode_g<32, 8, 2, 8>, a, enc_bytes, "enc const-network lds-dma 8 rows, nt stores");
-  add(k_encode_g<32, 8, 2, 16>, a, enc_bytes, "enc const-network lds-dma 16 rows, nt stores (production)");
+  add(k_encode_g<32, 8, 2, 8>, a, enc_bytes, "enc const-network lds-dma 8 rows, nt stores (production since round 2)");
+  add(k_encode_g<32, 8, 2, 16>, a, enc_bytes, "enc const-network lds-dma 16 rows, nt stores (round-1 production)");
   add(k_encode_g<32, 8, 0, 8>, a, enc_bytes, "enc const-network lds-dma 8 rows");
   add(k_apply_q<8, 0, 1, 1, 4>, ae, enc_bytes, "enc perm-tables streaming ring4 nt1");
   add(k_apply_q<8, 0, 1, 1, 8>, ae, enc_bytes, "enc perm-tables streaming ring8 nt1");
+  add(k_apply_q<8, 0, 3, 1, 4>, ae, enc_bytes, "enc perm-tables streaming ring4 nt3 (generic-code encode, production)");
+  add(k_apply_q<8, 0, 3, 1, 2>, ae, enc_bytes, "enc perm-tables streaming ring2 nt3");
   add(k_apply_q<8, 2, 1, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt1");
   add(k_apply_q<8, 2, 1, 1, 8>, ar, dec_bytes, "dec perm streaming ring8 nt1");
   add(k_apply_q<8, 2, 3, 1, 4>, ar, dec_bytes, "dec perm streaming ring4 nt3 (production)");

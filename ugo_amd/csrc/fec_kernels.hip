@@ -511,7 +511,9 @@ __global__ __launch_bounds__(256) void k_apply_q(Batch a) {
   }
   uint32_t mB;
   asm("v_mov_b32 %0, %1" : "=v"(mB) : "v"(inB ? ~0u : 0u));
-  const uint8_t* dS = dA == dB ? dA : nullptr;  // wave-uniform descriptor
+  // wave-uniform descriptor (always, in MODE 0: one descriptor for the batch,
+  // so the two-group table pick is compiled out and the table words stay SGPRs)
+  const uint8_t* dS = (MODE == 0 || dA == dB) ? dA : nullptr;
   uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
   const uint32_t nb = a.S - c * 16u;
   auto row_of = [&](uint32_t k) -> uint32_t {
@@ -545,7 +547,7 @@ __global__ __launch_bounds__(256) void k_apply_q(Batch a) {
         // byte of input k in that word (compile-time when the ring is a multiple of 4)
         const int kb = RING % 4 == 0 ? (j & 3) : static_cast<int>(k & 3u);
         uint32_t t[5], u[5];
-        if (dS) {
+        if (MODE == 0 || dS) {
           p_tables<0>(t, a, dS, dS, off, kb, 0u);
           p_tables<0>(u, a, dS, dS, off, kb + 1, 0u);
         } else {
@@ -962,7 +964,10 @@ constexpr int kEncNT = 3;    // nontemporal loads and stores
 constexpr int kEncLdsRows = 8;  // (10,3): rows 0-7 by LDS-DMA nt, 8-9 to registers
 constexpr int kEncStageRows = 13;  // (10,3): 52-KiB stage, 3 blocks per CU (see k_encode_g)
 constexpr int kEncJumboNT = 3;  // (32,8): NT loads and stores (578 vs 615 us, tools/jvariants.hip)
-constexpr int kEncJumboLdsRows = 16;  // (32,8): rows 0-15 by LDS-DMA nt (557 vs 571 us)
+// (32,8): rows 0-7 by LDS-DMA nt.  The round-1 pick of 16 rows (557 vs 571
+// us) lost to 8 rows in 9 of 12 interleaved round-2 runs (medians 565 vs 584 us)
+// (profiles/r2/jvariants_lds_rows_r2.txt)
+constexpr int kEncJumboLdsRows = 8;
 constexpr int kApplyNT = 3;  // nontemporal loads and stores
 constexpr int kApplyPNT = 3; // k_apply_p: nontemporal loads and stores (cold: 201.0 vs 228.4 us)
 constexpr int kApplyQNT = 3; // k_apply_q (jumbo): NT loads and stores (548 vs 572 us)
