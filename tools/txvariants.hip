@@ -102,7 +102,10 @@ int main(int argc, char** argv) {
     addc(k_tx_c<10, 3, 3, false>, "COLD tx nt3 (nt loads + stores)");
     addc(k_tx_pattern<0>, "COLD TX MEMORY PATTERN ONLY (nt loads, plain stores)");
     addc(k_tx_pattern<2>, "COLD TX MEMORY PATTERN ONLY (nt loads + stores)");
-    // occupancy sweep (round 2): dynamic LDS caps the blocks per CU
+    // occupancy sweep (round 2): dynamic LDS caps the blocks per CU.  (Also
+    // round 2, since removed: packets 0-7 or 0-9 by LDS-DMA at exactly 2 or 3
+    // blocks/CU lose to production, 454.5 / 457.2 vs 447.5 us at 2 blocks,
+    // profiles/r2/txvariants_ldsdma_exact_caps.jsonl.)
     for (uint32_t bpc : {4u, 3u, 2u}) {
       const uint32_t extra = 160u * 1024u / bpc + 512u;
       vars.push_back({"COLD OCC tx production (scalar lens, nt3), " + std::to_string(bpc) + " blocks/CU",
