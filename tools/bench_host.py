@@ -204,23 +204,23 @@ def rx_case(G, loss, reps, encrypt=True):
              "Mpkt_per_s_total": npk / (ta + ti) / 1e6}]
 
 
-def tx_case(G, reps, encrypt=True, full=True):
-    """TX path device-resident (ugo_fec_tx_assemble): G groups of 10 outgoing
-    data packets (16-B slots of 1488 B) -> headers + parity over [6, maxsize) +
-    RC4 pad XOR -> 13 wire packets per group.  Bytes = packet bytes read +
-    wire bytes written."""
-    d, p, n, slot = 10, 3, 13, 1488
+def tx_case(G, reps, encrypt=True, full=True, d=10, p=3, max_len=1476):
+    """TX path device-resident (ugo_fec_tx_assemble): G groups of d outgoing
+    data packets (16-B slots) -> headers + parity over [6, maxsize) + RC4 pad
+    XOR -> d+p wire packets per group.  Bytes = packet bytes read + wire bytes
+    written."""
+    n, slot = d + p, (max_len + 15) // 16 * 16
     enc = fec.New(d, p)
     gen = torch.Generator(device="cuda").manual_seed(5)
     pk = torch.randint(0, 256, (G * d, slot), dtype=torch.uint8, device="cuda", generator=gen)
     if full:
-        lens = torch.full((G * d,), 1476, dtype=torch.int16, device="cuda")
+        lens = torch.full((G * d,), max_len, dtype=torch.int16, device="cuda")
     else:
-        lens = torch.randint(6, 1477, (G * d,), dtype=torch.int16, device="cuda", generator=gen)
+        lens = torch.randint(6, max_len + 1, (G * d,), dtype=torch.int16, device="cuda", generator=gen)
     wire = torch.empty((G * n, slot), dtype=torch.uint8, device="cuda")
     wl = torch.empty(G * n, dtype=torch.int16, device="cuda")
     pad = torch.frombuffer(bytearray(fec.rc4_keystream(b"1234567890123456", slot)), dtype=torch.uint8).cuda()
-    run = lambda: enc.tx_assemble(pk, lens, wire, wl, pad=pad if encrypt else None)  # noqa: E731
+    run = lambda: enc.tx_assemble(pk, lens, wire, wl, pad=pad if encrypt else None, max_len=max_len)  # noqa: E731
     warm(run)
     s = torch.cuda.current_stream()
     e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -232,7 +232,7 @@ def tx_case(G, reps, encrypt=True, full=True):
     t = e[0].elapsed_time(e[1]) / reps * 1e-3
     L = lens.to(torch.int64).view(G, d)
     moved = int(2 * L.sum().item() + p * L.max(dim=1).values.sum().item())
-    return [{"case": f"tx assemble (10+3) full={full} rc4={encrypt}", "groups": G, "packets_out": G * n,
+    return [{"case": f"tx assemble ({d}+{p})x{max_len} full={full} rc4={encrypt}", "groups": G, "packets_out": G * n,
              "us": t * 1e6, "GBps": moved / t / 1e9, "Mpkt_per_s": G * n / t / 1e6}]
 
 
@@ -305,6 +305,10 @@ def main():
     ap.add_argument("--only", default="")
     args = ap.parse_args()
     res = []
+    if args.only == "txjumbo":
+        for r in tx_case(8192, args.reps, d=32, p=8, max_len=9006):
+            print(json.dumps(r), flush=True)
+        return
     if args.only == "jumbo":
         for r in device_case(32, 8, 9000, 8192, 8, args.reps):
             print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
