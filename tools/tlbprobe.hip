@@ -71,7 +71,8 @@ __global__ __launch_bounds__(256) void k_r10w3(uint8_t* __restrict__ a, uint64_t
   __builtin_nontemporal_store(y2, reinterpret_cast<u32x4*>(a + 12 * rstride + c * 16));
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool only_slices = argc > 1;
   const uint64_t GB = 1ull << 30;
   const uint64_t maxb = 160 * GB;
   uint8_t* buf;
@@ -84,6 +85,7 @@ int main() {
   CK(hipEventCreate(&e1));
   const char* names[4] = {"linear read", "10 streams, 1/10 apart", "linear nt write", "10 read + 3 write streams, 1/13 apart"};
   for (uint64_t gb : {1ull, 4ull, 16ull, 64ull, 128ull}) {
+    if (only_slices) break;
     for (int form = 0; form < 4; ++form) {
       const uint64_t bytes = gb * GB;
       const uint64_t n16 = bytes / 16;
@@ -125,6 +127,7 @@ int main() {
   // encode's streams over two alternating batches (cold, like bench.py), G
   // from the bench's 65,536 groups to BASELINE configs[3]'s 4M on one GPU.
   for (uint64_t G : {65536ull, 262144ull, 1048576ull, 2097152ull, 4194304ull}) {
+    if (only_slices && G != 4194304ull) continue;
     const uint64_t rstride = G * 1360, chunks = rstride / 16, batch = 13 * rstride;
     if (2 * batch > maxb) break;
     int flip = 0;
@@ -149,6 +152,37 @@ int main() {
            "\"TBps\":%.3f}\n", (unsigned long long)G, batch / 1e9, ms * 1e3 / reps,
            double(rstride) * 13 / (ms * 1e-3 / reps) / 1e12);
     fflush(stdout);
+  }
+  // The 4M-group geometry processed in slices of consecutive groups (one launch
+  // per slice, each covering 1/k of every row): does a slice behave like the
+  // smaller batch or like the 4M one?
+  {
+    const uint64_t G = 4194304ull, rstride = G * 1360, batch = 13 * rstride;
+    for (uint64_t slices : {1ull, 4ull, 16ull}) {
+      const uint64_t sc = rstride / 16 / slices;  // chunks per slice (per row)
+      int flip = 0;
+      auto go = [&]() {
+        uint8_t* b = buf + (flip++ & 1) * batch;
+        for (uint64_t s2 = 0; s2 < slices; ++s2)
+          hipLaunchKernelGGL(k_r10w3, dim3((sc + 255) / 256), dim3(256), 0, 0, b + s2 * sc * 16, sc, rstride);
+      };
+      auto t0 = std::chrono::steady_clock::now();
+      while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < 0.2) {
+        go();
+        CK(hipDeviceSynchronize());
+      }
+      const int reps = 6;
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r) go();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      CK(hipGetLastError());
+      printf("{\"form\":\"encode streams, 4M-group geometry in slices\",\"slices\":%llu,\"us\":%.1f,\"TBps\":%.3f}\n",
+             (unsigned long long)slices, ms * 1e3 / reps, double(rstride) * 13 / (ms * 1e-3 / reps) / 1e12);
+      fflush(stdout);
+    }
   }
   return 0;
 }
