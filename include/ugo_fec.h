@@ -19,8 +19,12 @@
  *   Any other layout is accepted and runs a slower byte-granular kernel.
  *
  * Erasures: present[g] bit r == 1  <=>  len(shards[r]) != 0 in Go terms.
- *   Batch presence masks are 64-bit, so the batch entry points need d+p <= 64
- *   (upstream allows 256; ugo uses (10,3)).
+ *   One uint64 per group for d+p <= 64.  Wider codes (up to upstream's 256
+ *   shards) take W = ceil((d+p)/64) words per group, present[g*W + r/64] bit
+ *   r%64 for shard r; their decode descriptors are built on the host per
+ *   erasure pattern (cached), so a device-resident mask batch is first copied
+ *   to the host (that call synchronises its stream).  RX assembly stays at
+ *   d+p <= 64 (ugo uses (10,3)).
  *
  * Threading: a context is single-owner (like ugo's FEC, used only from the
  * Conn.run goroutine, ugo/conn.go:106-127).  Distinct contexts -- e.g. one per
@@ -41,7 +45,9 @@ extern "C" {
 
 /* 2: ugo_fec_rx_assemble keeps the first copy of a repeated seqid and its
  *    stats grew a fifth counter (duplicates). */
-#define UGO_FEC_ABI_VERSION 2
+/* 3: reconstruct entry points accept d+p > 64 with ceil((d+p)/64) presence
+ *    words per group (one word, as before, for d+p <= 64). */
+#define UGO_FEC_ABI_VERSION 3
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
  * that ugo/fec.go logs and swallows (ugo/fec.go:60-63, 208-210, 239-241). */
@@ -52,7 +58,7 @@ typedef enum ugo_fec_status {
   UGO_FEC_ERR_TOO_FEW_SHARDS = 3, /* reedsolomon.ErrTooFewShards                     */
   UGO_FEC_ERR_SHARD_NO_DATA = 4,  /* reedsolomon.ErrShardNoData                      */
   UGO_FEC_ERR_SHARD_SIZE = 5,     /* reedsolomon.ErrShardSize                        */
-  UGO_FEC_ERR_INVALID_ARG = 6,    /* NULL pointer, pitch < shard_size, d+p > 64 ... */
+  UGO_FEC_ERR_INVALID_ARG = 6,    /* NULL pointer, pitch < shard_size, RX with d+p > 64 ... */
   UGO_FEC_ERR_SINGULAR = 7,       /* errSingular (cannot occur for this MDS code)    */
   UGO_FEC_ERR_HIP = 8,            /* HIP runtime failure (alloc, copy, launch)       */
   UGO_FEC_ERR_NO_DEVICE = 9       /* no usable gfx950 device / bad device ordinal    */
@@ -93,7 +99,7 @@ int ugo_fec_encode_strided(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t 
                            size_t row_stride, size_t group_stride, void* stream);
 
 /* Encoder.Reconstruct(shards) (ugo/fec.go:202) for every group.  `present`
- * (device, u64 per group) marks the non-empty shards.  Survivors are the first
+ * (device, one u64 per group; W words for d+p > 64) marks the non-empty shards.  Survivors are the first
  * d present rows in index order (upstream rule), every erased row is written.
  * Groups with fewer than d present shards are left untouched and get
  * status UGO_FEC_ERR_TOO_FEW_SHARDS; all others UGO_FEC_OK.  `status`

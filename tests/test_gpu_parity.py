@@ -427,21 +427,84 @@ def test_empty_batches_are_noops(gpu):
     torch.cuda.synchronize()
 
 
-def test_more_than_64_shards_encode_only(gpu):
-    """Upstream allows 256 shards; presence masks are 64-bit, so a batch
-    reconstruct with d+p > 64 is refused (documented in include/ugo_fec.h)
-    while encode works."""
-    d, p, S, G = 100, 20, 64, 8
+def _wide_masks(G, n, p, rng):
+    """[G][W] presence words (W = ceil(n/64)) with 0..p+1 erasures per group
+    (p+1: a too-few-shards group), plus the per-group erased-row sets."""
+    W = (n + 63) // 64
+    words = np.zeros((G, W), np.uint64)
+    erased = []
+    for g in range(G):
+        e = int(rng.integers(0, p + 2)) if g else p  # group 0: as many erasures as recoverable
+        er = set(int(r) for r in rng.choice(n, size=min(e, n), replace=False))
+        erased.append(er)
+        for r in range(n):
+            if r not in er:
+                words[g, r >> 6] |= np.uint64(1 << (r & 63))
+    return words, erased
+
+
+@pytest.mark.parametrize("d,p,S,G", [(70, 10, 40, 6),    # d > 32: byte kernel, descriptors built on the host
+                                     (30, 40, 48, 5),    # d <= 32, p > 8: k_apply
+                                     (8, 248, 16, 3)])   # 256 shards, upstream's maximum
+def test_more_than_64_shards(gpu, d, p, S, G):
+    """Upstream allows 256 shards: encode, batch reconstruct (in place and into
+    separate outputs, W = ceil((d+p)/64) presence words per group) and the
+    per-group Reconstruct against the independent Python restatement
+    (oracle/rs_ref.py reconstruct_group: first d present rows, two-stage)."""
     n = d + p
-    host = _rand(G, n, S, 7).numpy()
+    host = _rand(G, n, S, 7 + n).numpy()
     want = host.copy()
     rs_ref.c_encode(d, p, want, S=S)
     enc = fec.New(d, p)
+    assert enc.mask_words == (n + 63) // 64
     t = _dev(host)
     enc.encode_batch(t, shard_size=S)
     assert np.array_equal(t.cpu().numpy(), want)
-    with pytest.raises(fec.ErrInvalidArg):
-        enc.reconstruct_batch(t, torch.full((G,), -1, dtype=torch.int64, device="cuda"), shard_size=S)
+    M = rs_ref.build_matrix(d, p)
+    words, erased = _wide_masks(G, n, p, np.random.default_rng(n))
+    exp, exp_st = [], []
+    for g in range(G):
+        rows = [None if r in erased[g] else bytearray(want[g, r].tobytes()) for r in range(n)]
+        err = rs_ref.reconstruct_group(M, d, p, rows)
+        exp_st.append(0 if err is None else fec.ErrTooFewShards.code)
+        exp.append(rows)
+    inp = want.copy()
+    for g in range(G):
+        for r in erased[g]:
+            inp[g, r] = 0
+    dm = torch.as_tensor(words.view(np.int64)).cuda()
+    # in place
+    t = _dev(inp)
+    st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    enc.reconstruct_batch(t, dm, shard_size=S, status=st)
+    got, got_st = t.cpu().numpy(), st.cpu().numpy()
+    assert list(got_st) == exp_st
+    for g in range(G):
+        for r in range(n):
+            if exp_st[g] == 0:
+                assert got[g, r].tobytes() == bytes(exp[g][r]), (g, r)
+            else:
+                assert np.array_equal(got[g, r], inp[g, r]), (g, r)  # too few shards: untouched
+    # into separate outputs (slot i = i-th erased row)
+    out = torch.full((G, p, S), 0xA5, dtype=torch.uint8, device="cuda")
+    enc.reconstruct_into(_dev(inp), dm, out, shard_size=S, out_shard_major=False)
+    o = out.cpu().numpy()
+    for g in range(G):
+        if exp_st[g] == 0:
+            for i, r in enumerate(sorted(erased[g])):
+                assert o[g, i].tobytes() == bytes(exp[g][r]), (g, i)
+    # host batch (pinned zero-copy path) and the Go-shaped per-group call
+    hb = fec.host_alloc(G * n * S).reshape(G, n, S)
+    hb[:] = inp
+    hst = np.full(G, -1, np.int8)
+    enc.reconstruct_host(hb, words, S, status=hst)
+    assert list(hst) == exp_st
+    assert np.array_equal(hb, got)
+    fec.host_free(hb)
+    g = 0
+    shards = [None if r in erased[g] else bytearray(want[g, r].tobytes()) for r in range(n)]
+    enc.Reconstruct(shards)
+    assert [bytes(x) for x in shards] == [bytes(x) for x in exp[g]]
 
 
 @pytest.mark.parametrize("d,p,S,pitch,opitch,shard_major,table_max",

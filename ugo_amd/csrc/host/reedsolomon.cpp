@@ -67,7 +67,6 @@ int Encoder::EncodeWindows(uint8_t* const* rows, size_t S) {
 int Encoder::reconstruct(std::vector<Bytes>& shards, unsigned flags) {
   const int n = Shards();
   if (static_cast<int>(shards.size()) != n) return UGO_FEC_ERR_TOO_FEW_SHARDS;
-  if (n > 64) return UGO_FEC_ERR_INVALID_ARG;
   std::vector<size_t> lens(n);
   for (int i = 0; i < n; ++i) lens[i] = shards[i].size();
   size_t S = 0;
@@ -76,14 +75,14 @@ int Encoder::reconstruct(std::vector<Bytes>& shards, unsigned flags) {
   const size_t pitch = pitch_of(S);
   uint8_t* buf = staging(size_t(n) * pitch);
   if (!buf) return UGO_FEC_ERR_HIP;
-  uint64_t mask = 0;
+  uint64_t mask[4] = {0, 0, 0, 0};  // ceil(n / 64) words, n <= 256
   for (int r = 0; r < n; ++r)
     if (lens[r]) {
-      mask |= 1ull << r;
+      mask[r >> 6] |= 1ull << (r & 63);
       std::memcpy(buf + size_t(r) * pitch, shards[r].data(), S);
     }
   int8_t status = 0;
-  st = ugo_fec_reconstruct_host(ctx_, buf, &mask, 1, S, pitch, flags, &status);
+  st = ugo_fec_reconstruct_host(ctx_, buf, mask, 1, S, pitch, flags, &status);
   if (st) return st;
   const int limit = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? d_ : n;
   for (int r = 0; r < limit; ++r)

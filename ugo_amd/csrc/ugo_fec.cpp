@@ -15,6 +15,8 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "fec_kernels.hpp"
@@ -70,6 +72,9 @@ struct ugo_fec {
   uint64_t* d_zc_mask = nullptr;  // zero-copy host reconstruct: presence masks / status of the batch,
   int8_t* d_zc_status = nullptr;   // pinned host memory the kernels read / write through its mapping
   size_t zc_groups = 0;
+  // d+p > 64: decode descriptors built on the host, one per erasure pattern
+  // (klauspost caches its inversions per pattern the same way)
+  std::unordered_map<std::string, std::vector<uint8_t>> wide_cache;
   size_t stage_groups = 0;  // groups per staging buffer
   size_t stage_pitch = 0;
   // launch timing (ugo_fec_timing_begin/end)
@@ -103,11 +108,16 @@ void timer_release(ugo_fec* c) {
 // Survivors = first d present rows in index order (klauspost Reconstruct),
 // outputs = erased data rows then erased parity rows, coefficients
 // Dinv[r] (data row r) or M[r] * Dinv (parity row r).
-int build_desc(const ugo_fec* c, uint64_t mask, uint8_t* out) {
+// Presence words per group: one for d+p <= 64, ceil((d+p)/64) above (bit r of
+// the pattern = bit r % 64 of word r / 64).
+size_t mask_words(const ugo_fec* c) { return (size_t(c->n) + 63) / 64; }
+
+int build_desc_bits(const ugo_fec* c, const uint64_t* w, uint8_t* out) {
   const int d = c->d, n = c->n;
+  auto present = [w](int r) { return (w[r >> 6] >> (r & 63)) & 1; };
   std::memset(out, 0, c->desc_stride);
   int np = 0;
-  for (int r = 0; r < n; ++r) np += (mask >> r) & 1;
+  for (int r = 0; r < n; ++r) np += present(r);
   if (np == n) return UGO_FEC_OK;  // e = 0: nothing to rebuild
   if (np < d) {
     out[2] = UGO_FEC_ERR_TOO_FEW_SHARDS;
@@ -116,7 +126,7 @@ int build_desc(const ugo_fec* c, uint64_t mask, uint8_t* out) {
   std::vector<uint8_t> sub(size_t(d) * d), inv(size_t(d) * d), work(size_t(2) * d * d);
   std::vector<int> surv, outr;
   for (int r = 0; r < n; ++r) {
-    if ((mask >> r) & 1) {
+    if (present(r)) {
       if (int(surv.size()) < d) surv.push_back(r);
     } else {
       outr.push_back(r);
@@ -149,6 +159,8 @@ int build_desc(const ugo_fec* c, uint64_t mask, uint8_t* out) {
   }
   return UGO_FEC_OK;
 }
+
+int build_desc(const ugo_fec* c, uint64_t mask, uint8_t* out) { return build_desc_bits(c, &mask, out); }
 
 int hip_status(hipError_t e) { return e == hipSuccess ? UGO_FEC_OK : UGO_FEC_ERR_HIP; }
 
@@ -285,14 +297,84 @@ int scratch_alloc(ugo_fec* c, size_t bytes, hipStream_t s, void** out) {
 
 int scratch_free(void* ptr, hipStream_t s) { return ptr ? hip_status(hipFreeAsync(ptr, s)) : UGO_FEC_OK; }
 
+bool fast_out(const OutBatch& O) {
+  return !O.base || (reinterpret_cast<uintptr_t>(O.base) % 16 == 0 && O.L.rstride % 16 == 0 && O.L.gstride % 16 == 0);
+}
+
+constexpr size_t kWideCacheMax = 4096;  // patterns kept per context (d+p > 64)
+
+// d+p > 64 (wider than one presence word): the decode descriptors are built on
+// the host per erasure pattern (cached) and uploaded; the apply kernels run as
+// for k_prepare's descriptors (MODE 2).  The masks are read on the host: from
+// host_present when the caller has them there, else copied from the device
+// (a synchronising copy -- wide codes are not ugo's geometry).
+int reconstruct_wide(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
+                     const Layout& L, unsigned flags, int8_t* status, hipStream_t s, const OutBatch& O,
+                     const uint64_t* host_present) {
+  const size_t W = mask_words(c);
+  std::vector<uint64_t> hm;
+  if (!host_present) {
+    hm.resize(groups * W);
+    if (hipMemcpyAsync(hm.data(), present, hm.size() * sizeof(uint64_t), hipMemcpyDefault, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
+    host_present = hm.data();
+  }
+  const bool fast = fast_layout(c, shards, L) && fast_out(O);
+  ugo::kern::Batch a = base_batch(c, shards, S, L);
+  a.out = O.base;
+  a.ogstride = O.L.gstride;
+  a.orstride = O.L.rstride;
+  a.status = status;
+  a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
+  a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
+  const size_t per = std::min<size_t>(std::max<size_t>(1, kMaxItems / a.chunks), 65536);
+  const size_t stride = c->desc_stride;
+  std::vector<uint8_t> hd(std::min(per, groups) * stride);
+  uint8_t* work = nullptr;
+  int st = scratch_alloc(c, hd.size() + 64, s, reinterpret_cast<void**>(&work));
+  if (st) return st;
+  struct Release {
+    uint8_t* p;
+    hipStream_t s;
+    ~Release() { (void)scratch_free(p, s); }
+  } release{work, s};
+  for (size_t g0 = 0; g0 < groups; g0 += per) {
+    const size_t gn = std::min(per, groups - g0);
+    for (size_t g = 0; g < gn; ++g) {
+      const uint64_t* w = host_present + (g0 + g) * W;
+      std::string key(reinterpret_cast<const char*>(w), W * sizeof(uint64_t));
+      auto it = c->wide_cache.find(key);
+      if (it == c->wide_cache.end()) {
+        std::vector<uint8_t> dsc(stride);
+        (void)build_desc_bits(c, w, dsc.data());  // a failure is the group's status byte
+        if (c->wide_cache.size() >= kWideCacheMax) c->wide_cache.clear();
+        it = c->wide_cache.emplace(std::move(key), std::move(dsc)).first;
+      }
+      std::memcpy(&hd[g * stride], it->second.data(), stride);
+    }
+    // hd is refilled for the next slice: the copy must have read it first
+    if (hipMemcpyAsync(work, hd.data(), gn * stride, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
+    a.g0 = g0;
+    a.items = static_cast<uint32_t>(gn * a.chunks);
+    a.desc = work;
+    a.g_desc0 = g0;
+    const hipError_t e = fast ? ugo::kern::launch_apply(2, ugo::kern::apply_dmax(c->d), a, s)
+                              : ugo::kern::launch_apply_bytes(2, a, s);
+    if (e != hipSuccess) return UGO_FEC_ERR_HIP;
+  }
+  return UGO_FEC_OK;
+}
+
 int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
-                    const Layout& L, unsigned flags, int8_t* status, hipStream_t s, const OutBatch& O = {}) {
+                    const Layout& L, unsigned flags, int8_t* status, hipStream_t s, const OutBatch& O = {},
+                    const uint64_t* host_present = nullptr) {
   if (groups == 0) return UGO_FEC_OK;
   if (!present) return UGO_FEC_ERR_INVALID_ARG;
-  if (c->n > 64) return UGO_FEC_ERR_INVALID_ARG;  // 64-bit presence masks
-  const bool fast = fast_layout(c, shards, L) &&
-                    (!O.base || (reinterpret_cast<uintptr_t>(O.base) % 16 == 0 && O.L.rstride % 16 == 0 &&
-                                 O.L.gstride % 16 == 0));
+  if (c->n > 64) return reconstruct_wide(c, shards, present, groups, S, L, flags, status, s, O, host_present);
+  const bool fast = fast_layout(c, shards, L) && fast_out(O);
   const int mode = c->d_table ? 1 : 2;
   ugo::kern::Batch a = base_batch(c, shards, S, L);
   a.out = O.base;
@@ -364,7 +446,7 @@ int ensure_stage(ugo_fec* c, size_t pitch) {
     if (!c->streams[i] && hipStreamCreateWithFlags(&c->streams[i], hipStreamNonBlocking) != hipSuccess)
       return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_stage[i], want * gbytes + 16) != hipSuccess) return UGO_FEC_ERR_HIP;
-    if (hipMalloc(&c->d_mask[i], want * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (hipMalloc(&c->d_mask[i], want * mask_words(c) * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_status[i], want) != hipSuccess) return UGO_FEC_ERR_HIP;
   }
   c->stage_groups = want;
@@ -401,6 +483,7 @@ int host_reconstruct_mapped(ugo_fec* c, uint8_t* mapped, const uint64_t* present
     return UGO_FEC_ERR_HIP;
   // masks and statuses live in pinned memory too: no copy launches, so a small
   // batch (the per-group calls, FEC::flush) costs one launch and one sync
+  const size_t W = mask_words(c);
   if (c->zc_groups < groups) {
     (void)hipHostFree(c->d_zc_mask);
     (void)hipHostFree(c->d_zc_status);
@@ -408,7 +491,7 @@ int host_reconstruct_mapped(ugo_fec* c, uint8_t* mapped, const uint64_t* present
     c->d_zc_status = nullptr;
     c->zc_groups = 0;
     const size_t cap = std::max<size_t>(groups, 256);
-    if (hipHostMalloc(&c->d_zc_mask, cap * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (hipHostMalloc(&c->d_zc_mask, cap * W * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipHostMalloc(&c->d_zc_status, cap) != hipSuccess) return UGO_FEC_ERR_HIP;
     c->zc_groups = cap;
   }
@@ -416,8 +499,8 @@ int host_reconstruct_mapped(ugo_fec* c, uint8_t* mapped, const uint64_t* present
   int8_t* dstatus = c->d_zc_status;
   if (!device_view(dmask) || !device_view(dstatus)) return UGO_FEC_ERR_HIP;
   hipStream_t s = c->streams[0];
-  std::memcpy(c->d_zc_mask, present, groups * sizeof(uint64_t));
-  const int st = reconstruct_dev(c, mapped, dmask, groups, S, interleaved(c, pitch), flags, dstatus, s);
+  std::memcpy(c->d_zc_mask, present, groups * W * sizeof(uint64_t));
+  const int st = reconstruct_dev(c, mapped, dmask, groups, S, interleaved(c, pitch), flags, dstatus, s, {}, present);
   if (st) return st;
   if (hipStreamSynchronize(s) != hipSuccess) return UGO_FEC_ERR_HIP;
   int first = UGO_FEC_OK;
@@ -498,11 +581,13 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
       e = hipMemcpy3DAsync(&cp, s);
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
     } else {
+      const size_t W = mask_words(c);
       e = hipMemcpyAsync(dev, host, gn * gbytes, hipMemcpyHostToDevice, s);
       if (e == hipSuccess)
-        e = hipMemcpyAsync(c->d_mask[si], present + g0, gn * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+        e = hipMemcpyAsync(c->d_mask[si], present + g0 * W, gn * W * sizeof(uint64_t), hipMemcpyHostToDevice, s);
       if (e != hipSuccess) return UGO_FEC_ERR_HIP;
-      st = reconstruct_dev(c, dev, c->d_mask[si], gn, S, interleaved(c, pitch), flags, c->d_status[si], s);
+      st = reconstruct_dev(c, dev, c->d_mask[si], gn, S, interleaved(c, pitch), flags, c->d_status[si], s, {},
+                           present + g0 * W);
       if (st) return st;
       // all rows back: present rows and padding come back byte-identical (they
       // were copied in above and the kernels write only erased rows' [0, S))
@@ -735,7 +820,6 @@ int ugo_fec_reconstruct_host(ugo_fec* c, uint8_t* shards, const uint64_t* presen
   int st = check_batch(c, shards, groups, S, interleaved(c, pitch));
   if (st || groups == 0) return st;
   if (!present) return UGO_FEC_ERR_INVALID_ARG;
-  if (c->n > 64) return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
   TimerScope ts(c);

@@ -189,6 +189,7 @@ class Encoder:
         self.DataShards = data_shards
         self.ParityShards = parity_shards
         self.Shards = data_shards + parity_shards
+        self.mask_words = (self.Shards + 63) // 64  # presence words per group (include/ugo_fec.h)
         self.device = device
 
     def close(self):
@@ -234,9 +235,10 @@ class Encoder:
     def reconstruct_batch(self, shards, present, shard_size: Optional[int] = None, data_only=False,
                           status=None, stream=None, shard_major: bool = False):
         """present: int64/uint64 CUDA tensor [G] of presence bitmasks (bit r = shard r
-        non-empty); status: optional int8 CUDA tensor [G]."""
+        non-empty), [G][W] words for d+p > 64 (W = mask_words); status: optional int8
+        CUDA tensor [G]."""
         G, pitch, rs, gs = self._geom(shards, shard_major)
-        assert present.is_contiguous() and present.numel() == G and present.element_size() == 8
+        assert present.is_contiguous() and present.numel() == G * self.mask_words and present.element_size() == 8
         S = pitch if shard_size is None else shard_size
         st = None if status is None else status.data_ptr()
         _raise(load_library().ugo_fec_reconstruct_strided(self._h, shards.data_ptr(), present.data_ptr(), G, S, rs,
@@ -250,7 +252,7 @@ class Encoder:
         i-th erased row, ascending) goes to `out`, a contiguous uint8 CUDA tensor
         [p][G][opitch] (out_shard_major) or [G][p][opitch]."""
         G, pitch, rs, gs = self._geom(shards, shard_major)
-        assert present.is_contiguous() and present.numel() == G and present.element_size() == 8
+        assert present.is_contiguous() and present.numel() == G * self.mask_words and present.element_size() == 8
         assert out.is_contiguous() and out.element_size() == 1 and out.dim() == 3
         p = self.ParityShards
         if out_shard_major:
@@ -368,6 +370,7 @@ class Encoder:
         G, n, pitch = shards.shape
         assert n == self.Shards
         present = np.ascontiguousarray(present, dtype=np.uint64)
+        assert present.size == G * self.mask_words
         S = pitch if shard_size is None else shard_size
         st = None if status is None else status.ctypes.data
         if status is not None:
@@ -396,14 +399,14 @@ class Encoder:
             raise ErrTooFewShards(strerror(ErrTooFewShards.code))
         lens = [0 if s is None else len(s) for s in shards]
         S = check_shards(lens, nil_ok=True)
-        mask = 0
+        mask = np.zeros(self.mask_words, np.uint64)
         buf = np.zeros((1, self.Shards, S), np.uint8)
         for r, s in enumerate(shards):
             if lens[r]:
-                mask |= 1 << r
+                mask[r >> 6] |= np.uint64(1 << (r & 63))
                 buf[0, r] = np.frombuffer(bytes(s), np.uint8)
         status = np.zeros(1, np.int8)
-        rc = self.reconstruct_host(buf, np.array([mask], np.uint64), S, data_only, status)
+        rc = self.reconstruct_host(buf, mask, S, data_only, status)
         _raise(rc)
         limit = self.DataShards if data_only else self.Shards
         for r in range(limit):
