@@ -152,7 +152,9 @@ def test_reconstruct_inconsistent_inputs(gpu, table_max, monkeypatch):
                                          (40, 6, 70, 80), (1, 1, 7, 16), (7, 0, 32, 32),
                                          (5, 3, 1500, 1504), (8, 4, 4096, 4096), (16, 4, 1030, 1040),
                                          (56, 8, 256, 256),  # d+p = 64: the widest presence mask
-                                         (24, 8, 2040, 2048)])  # 128 chunks: k_apply_qa, no idle lane
+                                         (24, 8, 2040, 2048),  # 128 chunks: k_apply_qa, no idle lane
+                                         (40, 8, 2000, 2000),  # d > 32 on the streaming kernels (qa)
+                                         (50, 4, 1500, 1504)])  # d > 32, 94 chunks: k_apply_q
 def test_generic_geometries(gpu, d, p, S, pitch):
     n = d + p
     G = 300
@@ -444,6 +446,7 @@ def _wide_masks(G, n, p, rng):
 
 
 @pytest.mark.parametrize("d,p,S,G", [(70, 10, 40, 6),    # d > 32: byte kernel, descriptors built on the host
+                                     (60, 8, 1104, 4),   # d > 32, 69 chunks: streaming k_apply_q
                                      (30, 40, 48, 5),    # d <= 32, p > 8: k_apply
                                      (8, 248, 16, 3)])   # 256 shards, upstream's maximum
 def test_more_than_64_shards(gpu, d, p, S, G):

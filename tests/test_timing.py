@@ -52,3 +52,19 @@ def test_timing_covers_jumbo_prepare_and_apply(gpu):
     enc.reconstruct_batch(sh, masks, S, shard_major=True)
     recs, untimed = enc.timing_end()
     assert list(recs["kernel"]) == [1, 3, 2] and untimed == 0
+
+
+@pytest.mark.gpu
+def test_wide_data_codes_run_the_vector_kernels(gpu):
+    """d > 32 with at most 8 parity rows and rows of >= 64 chunks: encode and
+    reconstruct run the streaming vector kernels (ids 1 and 2, after k_prepare),
+    not the byte kernel (id 4)."""
+    d, p, n, S, G = 40, 8, 48, 2000, 64
+    enc = fec.New(d, p)
+    sh = torch.randint(0, 256, (G, n, S), dtype=torch.uint8, device=gpu)
+    masks = torch.full((G,), (1 << n) - 1 - 0b1011, dtype=torch.int64, device=gpu)
+    enc.timing_begin(8)
+    enc.encode_batch(sh, S)
+    enc.reconstruct_batch(sh, masks, S)
+    recs, untimed = enc.timing_end()
+    assert list(recs["kernel"]) == [1, 3, 2] and untimed == 0

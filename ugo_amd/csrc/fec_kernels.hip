@@ -996,6 +996,35 @@ hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Streaming kernels for wide codes (chunks >= 64, e <= 8 outputs): registers
+// do not grow with d, so any d (up to 255) runs here.  False if not eligible.
+// MODE 0 applies the encode descriptor: timed as an encode
+template <int MODE>
+constexpr KernelId apply_kid() { return MODE == 0 ? kKEncode : kKReconstruct; }
+
+template <int MODE>
+static bool launch_apply_stream(const Batch& a, hipStream_t s) {
+  if (a.chunks < 64 || a.epad > 8) return false;
+  const dim3 block(256);
+  const uint32_t cpad = (a.chunks + 63u) & ~63u;
+  if (MODE != 0 && (cpad - a.chunks) * 16u <= cpad) {  // groups wave-aligned at <= 1/16 idle lanes
+    Batch b = a;
+    b.items = (a.items / a.chunks) * cpad;
+    const dim3 ga(blocks_for(b.items, 256));
+    if (a.epad == 4)
+      launch(apply_kid<MODE>(), k_apply_qa<4, MODE, kApplyQNT>, ga, block, 0, s, b);
+    else
+      launch(apply_kid<MODE>(), k_apply_qa<8, MODE, kApplyQNT>, ga, block, 0, s, b);
+    return true;
+  }
+  const dim3 grid(blocks_for(a.items, 256));
+  if (a.epad == 4)
+    launch(apply_kid<MODE>(), k_apply_q<4, MODE, kApplyQNT, 1>, grid, block, 0, s, a);
+  else
+    launch(apply_kid<MODE>(), k_apply_q<8, MODE, kApplyQNT, 1>, grid, block, 0, s, a);
+  return true;
+}
+
 // k_apply_w needs a wave to span <= 2 groups (>= 64 chunks per row) and all
 // output rows in one descriptor dword (p <= 4); k_apply covers the rest.
 template <int DMAX, int MODE>
@@ -1003,40 +1032,26 @@ static void launch_apply_dm(const Batch& a, hipStream_t s) {
   const dim3 grid(blocks_for(a.items, 256)), block(256);
   if constexpr (DMAX <= 16) {
     if (a.chunks >= 64 && a.epad == 4) {
-      launch(kKReconstruct, k_apply_p<DMAX, MODE, kApplyPNT, 1>, grid, block, 0, s, a);
+      launch(apply_kid<MODE>(), k_apply_p<DMAX, MODE, kApplyPNT, 1>, grid, block, 0, s, a);
       return;
     }
   }
-  if (a.chunks >= 64 && a.epad <= 8) {  // wide codes: streaming inputs
-    const uint32_t cpad = (a.chunks + 63u) & ~63u;
-    if (MODE != 0 && (cpad - a.chunks) * 16u <= cpad) {  // groups wave-aligned at <= 1/16 idle lanes
-      Batch b = a;
-      b.items = (a.items / a.chunks) * cpad;
-      const dim3 ga(blocks_for(b.items, 256));
-      if (a.epad == 4)
-        launch(kKReconstruct, k_apply_qa<4, MODE, kApplyQNT>, ga, block, 0, s, b);
-      else
-        launch(kKReconstruct, k_apply_qa<8, MODE, kApplyQNT>, ga, block, 0, s, b);
-      return;
-    }
-    if (a.epad == 4)
-      launch(kKReconstruct, k_apply_q<4, MODE, kApplyQNT, 1>, grid, block, 0, s, a);
-    else
-      launch(kKReconstruct, k_apply_q<8, MODE, kApplyQNT, 1>, grid, block, 0, s, a);
-    return;
-  }
+  if (launch_apply_stream<MODE>(a, s)) return;  // wide codes: streaming inputs
   if (a.chunks >= 64 && a.epad == 4) {
     Batch b = a;
     b.pass = (a.items + 63u) / 64u * 64u;
-    launch(kKReconstruct, k_apply_w<DMAX, MODE, kApplyNT, 1>, grid, block, 0, s, b);
+    launch(apply_kid<MODE>(), k_apply_w<DMAX, MODE, kApplyNT, 1>, grid, block, 0, s, b);
   }
   else
-    launch(kKReconstruct, k_apply<DMAX, MODE, kApplyNT>, grid, block, 0, s, a);
+    launch(apply_kid<MODE>(), k_apply<DMAX, MODE, kApplyNT>, grid, block, 0, s, a);
 }
 
 template <int MODE>
 static hipError_t launch_apply_mode(int dmax, const Batch& a, hipStream_t s) {
   switch (dmax) {
+    case 0:  // d > 32: the streaming kernels only (the caller checked stream_eligible)
+      if (!launch_apply_stream<MODE>(a, s)) return hipErrorInvalidValue;
+      break;
     case 4: launch_apply_dm<4, MODE>(a, s); break;
     case 8: launch_apply_dm<8, MODE>(a, s); break;
     case 10: launch_apply_dm<10, MODE>(a, s); break;

@@ -194,9 +194,13 @@ struct Layout {
 
 Layout interleaved(const ugo_fec* c, size_t pitch) { return Layout{pitch, uint64_t(c->n) * pitch}; }
 
-bool fast_layout(const ugo_fec* c, const uint8_t* shards, const Layout& L) {
+// The 16-B vector kernels: aligned rows, and either d <= 32 (register-array
+// kernels) or a code the streaming kernels take at any d (rows >= 64 chunks,
+// at most 8 outputs).  Anything else runs the byte kernel.
+bool fast_layout(const ugo_fec* c, const uint8_t* shards, const Layout& L, size_t S) {
+  const bool stream_ok = c->epad <= 8 && (S + 15) / 16 >= 64;
   return (reinterpret_cast<uintptr_t>(shards) % 16 == 0) && (L.rstride % 16 == 0) && (L.gstride % 16 == 0) &&
-         ugo::kern::apply_dmax(c->d) != 0;
+         (ugo::kern::apply_dmax(c->d) != 0 || stream_ok);
 }
 
 // Separate output batch of a reconstruct (ugo_fec_reconstruct_into); none = in place.
@@ -253,7 +257,7 @@ bool layout_disjoint(size_t S, size_t rstride, size_t rows, size_t gstride, size
 
 int encode_dev(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, const Layout& L, hipStream_t s) {
   if (c->p == 0 || groups == 0) return UGO_FEC_OK;
-  const bool fast = fast_layout(c, shards, L);
+  const bool fast = fast_layout(c, shards, L, S);
   ugo::kern::Batch a = base_batch(c, shards, S, L);
   a.desc = c->d_encdesc;
   a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
@@ -320,7 +324,7 @@ int reconstruct_wide(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_
       return UGO_FEC_ERR_HIP;
     host_present = hm.data();
   }
-  const bool fast = fast_layout(c, shards, L) && fast_out(O);
+  const bool fast = fast_layout(c, shards, L, S) && fast_out(O);
   ugo::kern::Batch a = base_batch(c, shards, S, L);
   a.out = O.base;
   a.ogstride = O.L.gstride;
@@ -374,7 +378,7 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
   if (groups == 0) return UGO_FEC_OK;
   if (!present) return UGO_FEC_ERR_INVALID_ARG;
   if (c->n > 64) return reconstruct_wide(c, shards, present, groups, S, L, flags, status, s, O, host_present);
-  const bool fast = fast_layout(c, shards, L) && fast_out(O);
+  const bool fast = fast_layout(c, shards, L, S) && fast_out(O);
   const int mode = c->d_table ? 1 : 2;
   ugo::kern::Batch a = base_batch(c, shards, S, L);
   a.out = O.base;
