@@ -154,7 +154,8 @@ def test_reconstruct_inconsistent_inputs(gpu, table_max, monkeypatch):
                                          (56, 8, 256, 256),  # d+p = 64: the widest presence mask
                                          (24, 8, 2040, 2048),  # 128 chunks: k_apply_qa, no idle lane
                                          (40, 8, 2000, 2000),  # d > 32 on the streaming kernels (qa)
-                                         (50, 4, 1500, 1504)])  # d > 32, 94 chunks: k_apply_q
+                                         (50, 4, 1500, 1504),  # d > 32, 94 chunks: k_apply_q
+                                         (48, 16, 1344, 1344)])  # d > 32, p > 8: outputs in passes of 8
 def test_generic_geometries(gpu, d, p, S, pitch):
     n = d + p
     G = 300
@@ -447,6 +448,7 @@ def _wide_masks(G, n, p, rng):
 
 @pytest.mark.parametrize("d,p,S,G", [(70, 10, 40, 6),    # d > 32: byte kernel, descriptors built on the host
                                      (60, 8, 1104, 4),   # d > 32, 69 chunks: streaming k_apply_q
+                                     (72, 20, 160, 3),   # d > 32, p > 8, 10 chunks: k_apply_qa in passes
                                      (30, 40, 48, 5),    # d <= 32, p > 8: k_apply
                                      (8, 248, 16, 3)])   # 256 shards, upstream's maximum
 def test_more_than_64_shards(gpu, d, p, S, G):

@@ -68,3 +68,18 @@ def test_wide_data_codes_run_the_vector_kernels(gpu):
     enc.reconstruct_batch(sh, masks, S)
     recs, untimed = enc.timing_end()
     assert list(recs["kernel"]) == [1, 3, 2] and untimed == 0
+
+
+@pytest.mark.gpu
+def test_wide_parity_codes_past_32_data_rows_stay_vectorised(gpu):
+    """d > 32 with more than 8 parity rows (and short rows): the wave-aligned
+    kernel folds the outputs in passes; no byte-kernel launch (id 4)."""
+    d, p, n, S, G = 48, 16, 64, 256, 32
+    enc = fec.New(d, p)
+    sh = torch.randint(0, 256, (G, n, S), dtype=torch.uint8, device=gpu)
+    masks = torch.full((G,), -1 ^ 0b111 ^ (1 << 60), dtype=torch.int64, device=gpu)
+    enc.timing_begin(8)
+    enc.encode_batch(sh, S)
+    enc.reconstruct_batch(sh, masks, S)
+    recs, untimed = enc.timing_end()
+    assert list(recs["kernel"]) == [1, 3, 2] and untimed == 0

@@ -51,7 +51,6 @@ __device__ __forceinline__ V4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
   return V4{{v.x, v.y, v.z, v.w}};
 }
 
-typedef const __attribute__((address_space(4))) uint32_t* ctab_t;
 
 // PREP (A/B only, tools/jvariants.hip): 1 = copy a descriptor k_prepare left
 // in pr.desc instead of building it (isolates the cost of the build).

@@ -331,6 +331,35 @@ __device__ __forceinline__ void p_tables(uint32_t* t, const Batch& a, const uint
   }
 }
 
+// Word loads through the constant address space: they stay scalar loads even
+// after stores to global memory in the same kernel (a plain load there loses
+// its no-clobber proof and becomes a per-lane vector load).  Descriptors and
+// tables are never written by a kernel that reads them.
+typedef const __attribute__((address_space(4))) uint32_t* ctab_t;
+
+template <bool C>
+__device__ __forceinline__ uint32_t ldw(const uint8_t* p) {
+  if constexpr (C)
+    return *(ctab_t)(p);
+  else
+    return ld32(p);
+}
+
+// p_tables for a wave-uniform descriptor, constant-space loads when C
+template <bool C>
+__device__ __forceinline__ void p_tables_u(uint32_t* t, const Batch& a, const uint8_t* dS, uint32_t off, int k) {
+  const uint32_t c = (ldw<C>(dS + off) >> (8 * (k & 3))) & 0xffu;
+  if constexpr (C) {
+    const ctab_t tA = (ctab_t)(a.mult) + 8u * c;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) t[q] = tA[q];
+  } else {
+    const uint32_t* tA = a.mult + 8u * c;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) t[q] = tA[q];
+  }
+}
+
 __device__ __forceinline__ void p_sel(const V4& x, uint32_t* s0, uint32_t* s1, uint32_t* s2) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -590,7 +619,9 @@ __global__ __launch_bounds__(256) void k_apply_q(Batch a) {
 // waves/SIMD; the 4-deep ring takes 113 and 4 waves): 533.5 against 550.4 us
 // for the jumbo reconstruct (profiles/r2/jvariants_qa_ring2.jsonl).  Lanes
 // past the row's end load chunk 0 and store nothing.
-template <int EMAX, int MODE, int NT, int RING = 2, int WPE = 1>
+// PASSES: more than EMAX outputs (wide-parity codes past d = 32) are folded
+// EMAX at a time, the inputs re-read per pass (L2-resident by then).
+template <int EMAX, int MODE, int NT, int RING = 2, int WPE = 1, bool PASSES = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_qa(Batch a) {
   static_assert(RING % 2 == 0, "inputs are consumed in pairs");
   const uint32_t cpad = (a.chunks + 63u) & ~63u;
@@ -613,54 +644,67 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint8_t* gp = a.base + g * a.gstride + coff;
   auto load_in = [&](uint32_t k) -> V4 {
     if (k >= a.d) return V4{{0u, 0u, 0u, 0u}};
-    const uint32_t r = (ld32(dA + 4 + (k & ~3u)) >> (8 * (k & 3u))) & 0xffu;
+    const uint32_t r = (ldw<PASSES>(dA + 4 + (k & ~3u)) >> (8 * (k & 3u))) & 0xffu;
     return load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
   };
-  V4 acc[EMAX];
-#pragma unroll
-  for (int i = 0; i < EMAX; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
-  V4 ring[RING];
-#pragma unroll
-  for (int j = 0; j < RING; ++j) ring[j] = load_in(j);
   const uint32_t cbase = 4 + a.dpad + a.epad;
-  for (uint32_t k0 = 0; k0 < a.d; k0 += RING) {
+  // outputs [ob, ob + en) of this pass (one pass of all e outputs unless PASSES)
+  auto run = [&](uint32_t ob, uint32_t en) {
+    V4 acc[EMAX];
 #pragma unroll
-    for (int j = 0; j < RING; j += 2) {
-      const uint32_t k = k0 + j;
-      uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
-      p_sel(ring[j], s0, s1, s2);
-      p_sel(ring[j + 1], r0, r1, r2);
-      ring[j] = load_in(k + RING);
-      ring[j + 1] = load_in(k + RING + 1);
+    for (int i = 0; i < EMAX; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
+    V4 ring[RING];
 #pragma unroll
-      for (int i = 0; i < EMAX; ++i) {
-        if (i >= static_cast<int>(e)) continue;
-        const uint32_t off = cbase + i * a.dpad + (k & ~3u);  // coefficient word of inputs k, k+1
-        const int kb = RING % 4 == 0 ? (j & 3) : static_cast<int>(k & 3u);
-        uint32_t t[5], u[5];
-        p_tables<0>(t, a, dA, dA, off, kb, 0u);
-        p_tables<0>(u, a, dA, dA, off, kb + 1, 0u);
+    for (int j = 0; j < RING; ++j) ring[j] = load_in(j);
+    for (uint32_t k0 = 0; k0 < a.d; k0 += RING) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint32_t y = xor3(acc[i].v[q], perm(t[1], t[0], s0[q]), perm(t[3], t[2], s1[q]));
-          y = xor3(y, perm(0u, t[4], s2[q]), perm(u[1], u[0], r0[q]));
-          acc[i].v[q] = xor3(y, perm(u[3], u[2], r1[q]), perm(0u, u[4], r2[q]));
+      for (int j = 0; j < RING; j += 2) {
+        const uint32_t k = k0 + j;
+        uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
+        p_sel(ring[j], s0, s1, s2);
+        p_sel(ring[j + 1], r0, r1, r2);
+        ring[j] = load_in(k + RING);
+        ring[j + 1] = load_in(k + RING + 1);
+#pragma unroll
+        for (int i = 0; i < EMAX; ++i) {
+          if (i >= static_cast<int>(en)) continue;
+          const uint32_t off = cbase + (ob + i) * a.dpad + (k & ~3u);  // coefficient word of inputs k, k+1
+          const int kb = RING % 4 == 0 ? (j & 3) : static_cast<int>(k & 3u);
+          uint32_t t[5], u[5];
+          if constexpr (PASSES) {  // tables read after the previous pass's stores
+            p_tables_u<true>(t, a, dA, off, kb);
+            p_tables_u<true>(u, a, dA, off, kb + 1);
+          } else {
+            p_tables<0>(t, a, dA, dA, off, kb, 0u);
+            p_tables<0>(u, a, dA, dA, off, kb + 1, 0u);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            uint32_t y = xor3(acc[i].v[q], perm(t[1], t[0], s0[q]), perm(t[3], t[2], s1[q]));
+            y = xor3(y, perm(0u, t[4], s2[q]), perm(u[1], u[0], r0[q]));
+            acc[i].v[q] = xor3(y, perm(u[3], u[2], r1[q]), perm(0u, u[4], r2[q]));
+          }
         }
       }
     }
-  }
-  if (live) {
-    const uint32_t nb = a.S - coff;
-    constexpr int NO = (EMAX + 3) / 4;
-    uint32_t orw[NO];
+    if (live) {
+      const uint32_t nb = a.S - coff;
+      constexpr int NO = (EMAX + 3) / 4;
+      uint32_t orw[NO];
 #pragma unroll
-    for (int w = 0; w < NO; ++w) orw[w] = ld32(dA + 4 + a.dpad + 4 * w);
+      for (int w = 0; w < NO; ++w) orw[w] = ldw<PASSES>(dA + 4 + a.dpad + ob + 4 * w);  // ob % 4 == 0
 #pragma unroll
-    for (int i = 0; i < EMAX; ++i) {
-      if (i >= static_cast<int>(e)) continue;
-      const uint32_t r = (orw[i >> 2] >> (8 * (i & 3))) & 0xffu;
-      store16<NT>(out_row(a, gp, g, coff, r, i), acc[i], nb);
+      for (int i = 0; i < EMAX; ++i) {
+        if (i >= static_cast<int>(en)) continue;
+        const uint32_t r = (orw[i >> 2] >> (8 * (i & 3))) & 0xffu;
+        store16<NT>(out_row(a, gp, g, coff, r, ob + i), acc[i], nb);
+      }
     }
+  };
+  if constexpr (PASSES) {
+    for (uint32_t ob = 0; ob < e; ob += EMAX) run(ob, min(e - ob, static_cast<uint32_t>(EMAX)));
+  } else {
+    run(0u, e);
   }
   if (wst) a.status[g] = 0;
 }
@@ -1049,8 +1093,16 @@ static void launch_apply_dm(const Batch& a, hipStream_t s) {
 template <int MODE>
 static hipError_t launch_apply_mode(int dmax, const Batch& a, hipStream_t s) {
   switch (dmax) {
-    case 0:  // d > 32: the streaming kernels only (the caller checked stream_eligible)
-      if (!launch_apply_stream<MODE>(a, s)) return hipErrorInvalidValue;
+    case 0:  // d > 32: the streaming kernels, any row length and output count
+      if (!launch_apply_stream<MODE>(a, s)) {
+        // rows < 64 chunks or > 8 outputs: wave-aligned groups (idle lanes past
+        // a short row), outputs folded 8 at a time
+        Batch b = a;
+        const uint32_t cpad = (a.chunks + 63u) & ~63u;
+        b.items = (a.items / a.chunks) * cpad;
+        launch(apply_kid<MODE>(), k_apply_qa<8, MODE, kApplyQNT, 2, 1, true>, dim3(blocks_for(b.items, 256)),
+               dim3(256), 0, s, b);
+      }
       break;
     case 4: launch_apply_dm<4, MODE>(a, s); break;
     case 8: launch_apply_dm<8, MODE>(a, s); break;

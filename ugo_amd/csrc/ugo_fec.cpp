@@ -194,13 +194,11 @@ struct Layout {
 
 Layout interleaved(const ugo_fec* c, size_t pitch) { return Layout{pitch, uint64_t(c->n) * pitch}; }
 
-// The 16-B vector kernels: aligned rows, and either d <= 32 (register-array
-// kernels) or a code the streaming kernels take at any d (rows >= 64 chunks,
-// at most 8 outputs).  Anything else runs the byte kernel.
-bool fast_layout(const ugo_fec* c, const uint8_t* shards, const Layout& L, size_t S) {
-  const bool stream_ok = c->epad <= 8 && (S + 15) / 16 >= 64;
-  return (reinterpret_cast<uintptr_t>(shards) % 16 == 0) && (L.rstride % 16 == 0) && (L.gstride % 16 == 0) &&
-         (ugo::kern::apply_dmax(c->d) != 0 || stream_ok);
+// The 16-B vector kernels need aligned rows; every d runs on them (d <= 32:
+// register-array kernels, d > 32: the streaming kernels, which take any row
+// length and output count).  Unaligned layouts run the byte kernel.
+bool fast_layout(const ugo_fec*, const uint8_t* shards, const Layout& L, size_t) {
+  return (reinterpret_cast<uintptr_t>(shards) % 16 == 0) && (L.rstride % 16 == 0) && (L.gstride % 16 == 0);
 }
 
 // Separate output batch of a reconstruct (ugo_fec_reconstruct_into); none = in place.
