@@ -10,6 +10,8 @@ import os
 import numpy as np
 import pytest
 import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
 
 import rs_ref
 from ugo_amd import fec
@@ -583,3 +585,54 @@ def test_reconstruct_into_rejects_bad_outputs(gpu):
     assert lib.ugo_fec_reconstruct_into(*args, o.data_ptr(), pitch, p * pitch, 0, None, None) == 0
     torch.cuda.synchronize()
     assert torch.equal(o[:, 0, :S], torch.zeros_like(o[:, 0, :S]))  # all-zero codeword: row 0 rebuilt as zeros
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(d=st.integers(1, 48), p=st.integers(1, 16), S=st.integers(1, 2100), pad=st.sampled_from([0, 3, 16]),
+       table=st.sampled_from(["16", "0"]), seed=st.integers(0, 2**31 - 1))
+def test_random_geometries_vs_oracle(gpu, d, p, S, pad, table, seed, monkeypatch):
+    """Random codes, shard sizes and pitches (aligned and not, so every launch
+    path -- perm tables, streaming, wave-aligned, passes, masked Horner, byte
+    kernel; table and per-group descriptors -- gets drawn): encode and
+    reconstruct (in place, data-only, into) bit-exact vs the C oracle."""
+    n = d + p
+    if n > 64:
+        return
+    monkeypatch.setenv("UGO_FEC_TABLE_MAX_SHARDS", table)
+    pitch = S + pad
+    G = 48
+    rng = np.random.default_rng(seed)
+    host = rng.integers(0, 256, (G, n, pitch), dtype=np.uint8)
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    enc = fec.New(d, p)
+    t = _dev(host)
+    enc.encode_batch(t, shard_size=S)
+    assert np.array_equal(t.cpu().numpy()[:, :, :S], want[:, :, :S])
+    masks = np.zeros(G, np.uint64)
+    for g in range(G):
+        e = int(rng.integers(0, p + 2))
+        m = (1 << n) - 1
+        for r in rng.choice(n, size=min(e, n), replace=False):
+            m &= ~(1 << int(r))
+        masks[g] = m
+    inp = _erase(want, masks, n)
+    for data_only in (False, True):
+        exp = inp.copy()
+        rc, exp_st = rs_ref.c_reconstruct(d, p, exp, masks, S=S, data_only=data_only)
+        t = _dev(inp)
+        stt = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+        enc.reconstruct_batch(t, _masks_to_dev(masks), shard_size=S, data_only=data_only, status=stt)
+        assert np.array_equal(stt.cpu().numpy(), exp_st)
+        assert np.array_equal(t.cpu().numpy()[:, :, :S], exp[:, :, :S]), (d, p, S, pitch, data_only)
+    out = torch.full((G, p, pitch), 0xA5, dtype=torch.uint8, device="cuda")
+    enc.reconstruct_into(_dev(inp), _masks_to_dev(masks), out, shard_size=S, out_shard_major=False)
+    o = out.cpu().numpy()
+    exp = inp.copy()
+    rc, exp_st = rs_ref.c_reconstruct(d, p, exp, masks, S=S)
+    for g in range(G):
+        if exp_st[g] != 0:
+            continue
+        er = [r for r in range(n) if not (int(masks[g]) >> r) & 1]
+        for i, r in enumerate(er):
+            assert np.array_equal(o[g, i, :S], exp[g, r, :S]), (d, p, S, pitch, g, i)
