@@ -587,7 +587,8 @@ def test_reconstruct_into_rejects_bad_outputs(gpu):
     assert torch.equal(o[:, 0, :S], torch.zeros_like(o[:, 0, :S]))  # all-zero codeword: row 0 rebuilt as zeros
 
 
-@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES", "150")), deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(d=st.integers(1, 48), p=st.integers(1, 16), S=st.integers(1, 2100), pad=st.sampled_from([0, 3, 16]),
        table=st.sampled_from(["16", "0"]), seed=st.integers(0, 2**31 - 1))
 def test_random_geometries_vs_oracle(gpu, d, p, S, pad, table, seed, monkeypatch):
