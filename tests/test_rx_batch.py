@@ -8,9 +8,13 @@ channel; the expected batch is assembled on the CPU from the decrypted
 packets and reconstructed with the C oracle.  Bit-exact comparison of the
 whole planar batch, the presence masks, the per-group status and the stats.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
 
 import fec_ref
 import rc4_ref
@@ -253,3 +257,65 @@ def test_rx_assemble_rejects_pageable_host_memory(gpu):
     present = torch.zeros(8, dtype=torch.int64, device="cuda")
     with pytest.raises(fec.ErrInvalidArg):
         codec.rx_assemble(ring, lens, sh, present, shard_size=1470)
+
+
+@pytest.mark.gpu
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES_RX", "80")), deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(d=st.integers(1, 20), p=st.integers(1, 8), S=st.integers(1, 700), G=st.integers(1, 80),
+       first_group=st.integers(0, 5), loss=st.floats(0, 0.5), dup=st.floats(0, 0.3), junk=st.floats(0, 0.1),
+       encrypt=st.booleans(), seed=st.integers(0, 2**31 - 1))
+def test_rx_assemble_random_rings(gpu, d, p, S, G, first_group, loss, dup, junk, encrypt, seed):
+    """Random codes, shard sizes, windows and channels (loss, duplicates with
+    different payloads, bad flags, short and out-of-window packets, any ring
+    order): presence masks, stats and every placed row equal the per-packet
+    reference path's (first copy of a seqid wins); rows no packet claimed stay
+    untouched."""
+    n = d + p
+    pitch = (S + 15) // 16 * 16
+    slot = (S + 6 + 15) // 16 * 16
+    rng = np.random.default_rng(seed)
+
+    def pkt(seq, flag):
+        L = int(rng.integers(6, S + 7))
+        b = bytearray(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        b[0:4] = seq.to_bytes(4, "little")
+        b[4:6] = flag.to_bytes(2, "little")
+        return bytes(b)
+
+    wire = []
+    for g in range(first_group - 1, first_group + G + 1):  # one group either side of the window
+        if g < 0:
+            continue
+        for r in range(n):
+            if rng.random() < loss:
+                continue
+            for _ in range(1 + (int(rng.integers(1, 3)) if rng.random() < dup else 0)):
+                wire.append(pkt(g * n + r, 0xF1 if r < d else 0xF2))
+            if rng.random() < junk:
+                wire.append(pkt(g * n + r, 0x77))  # bad flag
+    if rng.random() < 0.5:
+        wire.append(b"\x01\x02\x03")  # too short
+    if not wire:
+        return
+    wire = [wire[i] for i in rng.permutation(len(wire))]
+    want, masks, stats = _expected_placement(wire, G, n, S, pitch, first_group)
+    ks = rc4_ref.keystream(KEY, slot)
+    enc = [rc4_ref.xor_stream(KEY, w) if encrypt else w for w in wire]
+    slots, lens = _ring(enc, slot)
+    codec = fec.New(d, p)
+    sh = torch.full((n, G, pitch), 0xAB, dtype=torch.uint8, device="cuda")
+    present = torch.zeros(G, dtype=torch.int64, device="cuda")
+    stt = torch.zeros(5, dtype=torch.int32, device="cuda")
+    pad = torch.frombuffer(bytearray(ks), dtype=torch.uint8).cuda() if encrypt else None
+    codec.rx_assemble(torch.from_numpy(slots).cuda(), torch.from_numpy(lens.view(np.int16)).cuda(), sh, present,
+                      first_group=first_group, shard_size=S, pad=pad, stats=stt)
+    assert stt.cpu().tolist() == stats
+    assert np.array_equal(present.cpu().numpy().view(np.uint64), masks)
+    got = sh.cpu().numpy().transpose(1, 0, 2)
+    for g in range(G):
+        for r in range(n):
+            if (int(masks[g]) >> r) & 1:
+                assert np.array_equal(got[g, r, :S], want[g, r, :S]), (g, r)
+            else:
+                assert (got[g, r] == 0xAB).all(), (g, r)
