@@ -207,7 +207,11 @@ int ugo_fec_rx_assemble(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, c
  * Seqids run from first_seq (a multiple of d+p below paws, as FEC.next always
  * is at a group boundary) and wrap at paws like markFEC.  A group with a
  * length outside [6, max_len] gets status UGO_FEC_ERR_SHARD_SIZE and
- * wire_lens 0.  slot_in, slot_out: multiples of 16, >= round_up(max_len, 16);
+ * wire_lens 0.  A group whose data packets are all header-only (6 bytes) has
+ * an empty parity window: as in the sender loop, whose calcECC then fails, its
+ * data packets go out and no parity does (status UGO_FEC_ERR_SHARD_NO_DATA,
+ * parity wire_lens 0); the batch still spends d+p seqids on it, where the
+ * reference's counter would move by d.  slot_in, slot_out: multiples of 16, >= round_up(max_len, 16);
  * d <= 32. */
 int ugo_fec_tx_assemble(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, const uint16_t* lens,
                         size_t groups, uint32_t first_seq, const uint8_t* pad, size_t max_len,

@@ -213,7 +213,9 @@ def tx_group(fec: FEC, data_pkts, key=None, buf_size=maxPacketSize):
         maxsize = max(maxsize, len(ori))
         out.append(bytes(ori))
     ecc = fec.calcECC(group, fecHeaderSize, maxsize)
-    for k in range(n - d):
+    # calcECC returns nil when Encode fails (every packet header-only: empty
+    # window, ErrShardNoData): the loop then sends no parity (ugo/conn.go:669-673)
+    for k in range(len(ecc) if ecc is not None else 0):
         fec.markFEC(ecc[k])
         out.append(bytes(ecc[k][:maxsize]))
     if key is not None:

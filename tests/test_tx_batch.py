@@ -4,9 +4,13 @@
 (oracle/fec_ref.tx_group: ugo/conn.go:643-685 + ugo/conn.go:634) run with the
 same seqids; then TX -> lossy channel -> RX assembly -> Reconstruct round trip.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
 
 import fec_ref
 from ugo_amd import fec
@@ -203,3 +207,41 @@ def test_tx_rx_round_trip_full_size(gpu):
         L = (lens.view(G, d)[:, k].to(torch.int64) - 6).unsqueeze(1)
         want = torch.where(col.unsqueeze(0) < L, pkt, torch.zeros_like(pkt))
         assert torch.equal(sh[k, :, :S], want), f"data row {k}"
+
+
+@pytest.mark.gpu
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES_TX", "60")), deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(d=st.integers(1, 32), p=st.integers(1, 8), max_len=st.integers(6, 1600), G=st.integers(1, 24),
+       group0=st.integers(0, 40), full=st.floats(0, 1), encrypt=st.booleans(), seed=st.integers(0, 2**31 - 1))
+def test_tx_assemble_random_batches(gpu, d, p, max_len, G, group0, full, encrypt, seed):
+    """Random codes (d <= 32, the TX kernels' range), packet-length limits,
+    length mixes and first seqids: every wire packet and length equals the
+    restated sender loop's."""
+    n = d + p
+    enc = fec.New(d, p)
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(6, max_len + 1, G * d)
+    lens[rng.random(G * d) < full] = max_len
+    pk = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    first_seq = group0 * n
+    slot = (max_len + 15) // 16 * 16
+    key = KEY if encrypt else None
+    st_ = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    wire, wl = _run_gpu(enc, pk, lens, slot, first_seq, key, max_len, status=st_)
+    tx = fec_ref.FEC.new(128, d, p, clock=lambda: 0)
+    for g in range(G):
+        # a group whose packets are all header-only gets no parity (calcECC: empty
+        # window); the reference's next then moves by d only, the batch keeps n
+        # seqids per group (include/ugo_fec.h)
+        tx.next = first_seq + g * n
+        out = fec_ref.tx_group(tx, pk[g * d:(g + 1) * d], key)
+        nowin = all(len(x) == 6 for x in pk[g * d:(g + 1) * d])
+        assert len(out) == (d if nowin else n)
+        assert int(st_[g]) == (fec.ErrShardNoData.code if nowin else 0)
+        for k, w in enumerate(out):
+            i = g * n + k
+            assert wl[i] == len(w), (i, wl[i], len(w))
+            assert wire[i, :len(w)].tobytes() == w, (i, g, k)
+        for k in range(len(out), n):
+            assert wl[g * n + k] == 0

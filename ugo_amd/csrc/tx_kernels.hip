@@ -34,6 +34,8 @@ namespace {
 constexpr uint32_t kTypeData = 0xf1u;  // ugo/constants.go:18
 constexpr uint32_t kTypeFEC = 0xf2u;   // ugo/constants.go:19
 constexpr int8_t kBadLength = 5;       // UGO_FEC_ERR_SHARD_SIZE
+constexpr int8_t kNoData = 4;          // UGO_FEC_ERR_SHARD_NO_DATA
+constexpr uint32_t kFecHeader = 6;     // fecHeaderSize, ugo/fec.go:11
 
 __device__ __forceinline__ uint32_t keep_mask(uint32_t keep, int j) {
   const uint32_t lo = 4u * j;
@@ -176,6 +178,20 @@ __device__ __forceinline__ void tx_cparity(const TxArgs& a, const TxItem& t, con
   (tx_parity_out<NT>(a, t, I, cparity<D, P, I>(x)), ...);
 }
 
+// Every data packet of the group header-only: calcECC's window [6, 6) is
+// empty, its Encode fails (ErrShardNoData, ugo/fec.go:238-241) and the sender
+// loop emits no parity packets (ugo/conn.go:669-673).  The group's data
+// packets go out as usual; status UGO_FEC_ERR_SHARD_NO_DATA, parity wire_lens 0.
+__device__ __forceinline__ bool tx_no_window(const TxArgs& a, const TxItem& t) {
+  if (t.maxsz > kFecHeader) return false;
+  if (t.o == 0) {
+    if (a.status) a.status[t.g] = kNoData;
+    const uint32_t n = a.d + a.p;
+    for (uint32_t i = 0; i < a.p; ++i) a.wire_lens[t.g * n + a.d + i] = 0;
+  }
+  return true;
+}
+
 // (10,3) / (32,8): the compile-time XOR networks of k_encode_c.
 template <int D, int P, int NT = kTxNT, bool SL = kTxSL>
 __global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
@@ -183,7 +199,7 @@ __global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
   if (item >= a.groups * a.chunks) return;
   V4 x[D];
   const TxItem t = tx_data<D, NT, SL>(a, item, x);
-  if (!t.live) return;
+  if (!t.live || tx_no_window(a, t)) return;
   tx_cparity<D, P, NT>(a, t, x, std::make_integer_sequence<int, P>{});
   if (t.o == 0 && a.status) a.status[t.g] = 0;
 }
@@ -196,7 +212,7 @@ __global__ __launch_bounds__(256) void k_tx_var(TxArgs a) {
   if (item >= a.groups * a.chunks) return;
   V4 x[DMAX];
   const TxItem t = tx_data<DMAX, kTxNT, false>(a, item, x);
-  if (!t.live) return;
+  if (!t.live || tx_no_window(a, t)) return;
   constexpr int NW = (DMAX + 3) / 4;
   const uint32_t cbase = 4 + a.dpad + a.epad;
   for (uint32_t i = 0; i < a.p; ++i) {
