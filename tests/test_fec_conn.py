@@ -9,8 +9,12 @@ Both sides see the same packets and the same injected clock; every step's
 (seqid, flag, recovered shards) and len(rx) must match bit for bit.  The
 C++ side computes all Reed-Solomon bytes on the GPU.
 """
+import os
+
 import numpy as np
 import pytest
+from hypothesis import HealthCheck, event, given, settings
+from hypothesis import strategies as st
 
 import fec_ref
 from ugo_amd import fec
@@ -207,3 +211,74 @@ def test_set_batch_flushes_pending_and_rejects_bad_sizes(gpu):
     got = rx_b.set_batch(0)  # back to per call: the pending groups come back first
     assert [bytes(x) for x in got] == want and rx_b.pending() == 0
     del rng
+
+
+def _tx_stream_any(tx, d, p, groups, rng, max_len):
+    """_tx_stream for any (d, p): the sender loop with reused group buffers."""
+    n = d + p
+    packets = []
+    group = [bytearray(fec_ref.maxPacketSize) for _ in range(n)]
+    for _ in range(groups):
+        maxsize = 0
+        for k in range(d):
+            L = int(rng.integers(7, max_len + 1))
+            ori = bytearray(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+            tx.markData(ori)
+            group[k][:L] = ori
+            maxsize = max(maxsize, L)
+            packets.append(bytes(ori))
+        ecc = tx.calcECC(group, fec_ref.fecHeaderSize, maxsize)
+        for k in range(p):
+            tx.markFEC(ecc[k])
+            packets.append(bytes(ecc[k][:maxsize]))
+    return packets
+
+
+@pytest.mark.gpu
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES_CONN", "40")), deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(d=st.integers(1, 12), p=st.integers(1, 5), extra=st.integers(0, 60), groups=st.integers(1, 30),
+       max_len=st.integers(7, fec_ref.maxPacketSize), drop=st.floats(0, 0.6), dup=st.floats(0, 0.3),
+       junk=st.floats(0, 0.1), reorder=st.integers(1, 40), batch=st.sampled_from([0, 0, 1, 3, 16]),
+       seed=st.integers(0, 2**31 - 1))
+def test_fec_object_random_channels(gpu, d, p, extra, groups, max_len, drop, dup, junk, reorder, batch, seed):
+    """Random codes and rxlimits, packet sizes, channels (loss, duplicates,
+    junk flags, reordering windows up to 40 packets, clock jumps past
+    fecExpire) and, with batch > 0, batched recovery: every step's
+    (seqid, flag) and len(rx) match the restated ugo/fec.go, and the recovered
+    shards match -- per call, or (batched) as the same sequence delayed to the
+    flushes."""
+    n = d + p
+    rxlimit = n + extra
+    rng = np.random.default_rng(seed)
+    now = [5_000_000]
+    clock = lambda: now[0]  # noqa: E731
+    tx = fec_ref.FEC.new(rxlimit, d, p, clock)
+    pk = _tx_stream_any(tx, d, p, groups, rng, max_len)
+    wire = _channel(pk, rng, drop=drop, dup=dup, junk=junk, reorder=reorder)
+    rx_c = fec.FecConn(rxlimit, d, p)
+    rx_c.set_clock(clock)
+    if batch:
+        rx_c.set_batch(batch)
+    rx_o = fec_ref.FEC.new(rxlimit, d, p, clock)
+    got, want = [], []
+    for i, pkt in enumerate(wire):
+        now[0] += int(rng.integers(0, 50))
+        if rng.random() < 0.01:
+            now[0] += fec_ref.fecExpire + 1
+        sc, fc, rc = rx_c.input(pkt)
+        so, fo, ro = fec_ref.handle(rx_o, pkt)
+        assert (sc, fc) == (so, fo), i
+        assert rx_c.rx_len() == len(rx_o.rx), i
+        if rc is not None:
+            got += [bytes(x) for x in rc]
+        if ro is not None:
+            want += [bytes(x) for x in ro]
+        if not batch:
+            assert (rc is None) == (ro is None), i
+    if batch:
+        rc = rx_c.flush()
+        if rc is not None:
+            got += [bytes(x) for x in rc]
+    assert got == want
+    event(f"recovered shards: {'none' if not want else ('1-9' if len(want) < 10 else '10+')}")
