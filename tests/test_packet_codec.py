@@ -9,7 +9,11 @@ The reference holds no codec test; the oracle is pinned by the
 hand-derived vectors below (Go's documented uvarint example, the ufloat16
 definition in ugo/utils/float16.go:12-16) and by encode -> decode round trips.
 """
+import os
+
 import numpy as np
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
 import pytest
 import torch
 
@@ -233,3 +237,26 @@ def test_packet_decode_fec_framed_with_rc4(gpu):
     info, ranges, segs = _run(enc, pk, slot, pad_key=KEY, framed=True)
     _check(pk, info, ranges, segs, framed=True)
     assert rc4_ref.keystream(KEY, 8) == fec.rc4_keystream(KEY, 8)
+
+
+@pytest.mark.gpu
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES_PKT", "40")), deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(seed=st.integers(0, 2**31 - 1), max_ranges=st.integers(1, 40), max_segments=st.integers(1, 10),
+       framed=st.booleans(), encrypt=st.booleans())
+def test_packet_decode_random_corpora(gpu, seed, max_ranges, max_segments, framed, encrypt):
+    """Seeded corpora (valid packets, truncations, bit flips, junk), random
+    range / segment caps, FEC framing and RC4 on or off: every packet's status,
+    header fields, ranges and segment views equal the restated decoder's."""
+    enc = fec.New(10, 3)
+    rng = np.random.default_rng(seed)
+    pk = []
+    for i, b in enumerate(_corpus(seed, n_valid=60)):
+        if framed:
+            flag = [0xF1, 0xF1, 0xF2, 0x1234][i % 4]
+            b = int(rng.integers(0, 2**32)).to_bytes(4, "little") + flag.to_bytes(2, "little") + b
+        pk.append(b)
+    slot = max(len(b) for b in pk) + 15 & ~15
+    info, ranges, segs = _run(enc, pk, slot, pad_key=b"1234567890123456" if encrypt else None, framed=framed,
+                              max_ranges=max_ranges, max_segments=max_segments)
+    _check(pk, info, ranges, segs, framed=framed, max_ranges=max_ranges, max_segments=max_segments)
