@@ -637,3 +637,53 @@ def test_random_geometries_vs_oracle(gpu, d, p, S, pad, table, seed, monkeypatch
         er = [r for r in range(n) if not (int(masks[g]) >> r) & 1]
         for i, r in enumerate(er):
             assert np.array_equal(o[g, i, :S], exp[g, r, :S]), (d, p, S, pitch, g, i)
+
+
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES", "150")) // 3, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(d=st.integers(1, 24), p=st.integers(1, 8), S=st.integers(1, 1500), planar=st.booleans(),
+       row_pad=st.sampled_from([0, 16, 48, 4096]), group_pad=st.sampled_from([0, 3, 16, 112]),
+       seed=st.integers(0, 2**31 - 1))
+def test_random_strided_layouts_vs_oracle(gpu, d, p, S, planar, row_pad, group_pad, seed):
+    """Strided batch views (the tensor's own row and group strides, padded
+    either way, group-major or planar) encode and reconstruct like the packed
+    batch, and bytes outside the shards are never written."""
+    n, G = d + p, 40
+    pitch = (S + 15) // 16 * 16
+    rng = np.random.default_rng(seed)
+    packed = rng.integers(0, 256, (G, n, pitch), dtype=np.uint8)
+    want = packed.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    if planar:
+        rs, gs = G * pitch + row_pad, pitch + group_pad
+        if group_pad:
+            rs = G * gs + row_pad
+        shape, strides = (n, G, pitch), (rs, gs, 1)
+        total = (n - 1) * rs + (G - 1) * gs + pitch
+    else:
+        rs, gs = pitch + row_pad, n * (pitch + row_pad) + group_pad
+        shape, strides = (G, n, pitch), (gs, rs, 1)
+        total = (G - 1) * gs + (n - 1) * rs + pitch
+    flat = torch.full((total,), 0x5A, dtype=torch.uint8, device="cuda")
+    view = flat.as_strided(shape, strides)
+    src = torch.as_tensor(packed).cuda()
+    view.copy_(src.transpose(0, 1) if planar else src)
+    untouched = flat.clone()
+    mask_out = torch.ones(total, dtype=torch.bool, device="cuda")
+    mask_out.as_strided(shape, strides)[..., :S] = False  # shard bytes
+    enc = fec.New(d, p)
+    enc.encode_batch(view, shard_size=S, shard_major=planar)
+    got = (view.transpose(0, 1) if planar else view).cpu().numpy()
+    assert np.array_equal(got[:, :, :S], want[:, :, :S])
+    assert torch.equal(flat[mask_out], untouched[mask_out]), "bytes outside the shards were written"
+    masks = np.zeros(G, np.uint64)
+    for g in range(G):
+        m = (1 << n) - 1
+        for r in rng.choice(n, size=int(rng.integers(0, p + 1)), replace=False):
+            m &= ~(1 << int(r))
+        masks[g] = m
+    inp = _erase(want, masks, n)
+    view.copy_(torch.as_tensor(inp).cuda().transpose(0, 1) if planar else torch.as_tensor(inp).cuda())
+    enc.reconstruct_batch(view, _masks_to_dev(masks), shard_size=S, shard_major=planar)
+    got = (view.transpose(0, 1) if planar else view).cpu().numpy()
+    assert np.array_equal(got[:, :, :S], want[:, :, :S])
