@@ -687,3 +687,47 @@ def test_random_strided_layouts_vs_oracle(gpu, d, p, S, planar, row_pad, group_p
     enc.reconstruct_batch(view, _masks_to_dev(masks), shard_size=S, shard_major=planar)
     got = (view.transpose(0, 1) if planar else view).cpu().numpy()
     assert np.array_equal(got[:, :, :S], want[:, :, :S])
+
+
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES", "150")) // 5, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(d=st.integers(1, 40), p=st.integers(1, 12), S=st.integers(1, 1500), pad=st.sampled_from([0, 5, 16]),
+       G=st.integers(1, 200), pinned=st.booleans(), data_only=st.booleans(), seed=st.integers(0, 2**31 - 1))
+def test_random_host_batches_vs_oracle(gpu, d, p, S, pad, G, pinned, data_only, seed):
+    """The host-memory entry points (staged DMA for pageable batches, zero-copy
+    for pinned ones) on random codes and sizes: encode and reconstruct
+    (statuses included) bit-exact vs the oracle."""
+    n = d + p
+    if n > 64:
+        return
+    pitch = S + pad
+    rng = np.random.default_rng(seed)
+    host = rng.integers(0, 256, (G, n, pitch), dtype=np.uint8)
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    enc = fec.New(d, p)
+    if pinned:
+        buf = fec.host_alloc(G * n * pitch).reshape(G, n, pitch)
+    else:
+        buf = np.empty((G, n, pitch), np.uint8)
+    try:
+        buf[:] = host
+        enc.encode_host(buf, S)
+        assert np.array_equal(buf[:, :, :S], want[:, :, :S])
+        masks = np.zeros(G, np.uint64)
+        for g in range(G):
+            m = (1 << n) - 1
+            for r in rng.choice(n, size=min(int(rng.integers(0, p + 2)), n), replace=False):
+                m &= ~(1 << int(r))
+            masks[g] = m
+        inp = _erase(want, masks, n)
+        exp = inp.copy()
+        rc, exp_st = rs_ref.c_reconstruct(d, p, exp, masks, S=S, data_only=data_only)
+        buf[:] = inp
+        stt = np.full(G, -1, np.int8)
+        enc.reconstruct_host(buf, masks, S, data_only=data_only, status=stt)
+        assert np.array_equal(stt, exp_st)
+        assert np.array_equal(buf[:, :, :S], exp[:, :, :S])
+    finally:
+        if pinned:
+            fec.host_free(buf)
