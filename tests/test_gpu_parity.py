@@ -731,3 +731,30 @@ def test_random_host_batches_vs_oracle(gpu, d, p, S, pad, G, pinned, data_only, 
     finally:
         if pinned:
             fec.host_free(buf)
+
+
+@pytest.mark.parametrize("d,p,S,pitch", [(10, 3, 1_000_003, 1_000_016),   # 62,501 chunks per row
+                                         (32, 8, 262_144, 262_144),       # jumbo code, 256-KiB shards
+                                         (10, 3, 70_000, 70_003)])        # > 64 KiB, unaligned: byte kernel
+def test_large_shards_vs_oracle(gpu, d, p, S, pitch):
+    """Shards far past ugo's 1,476 B (sizes are size_t in the ABI): encode and
+    every recoverable erasure count, bit-exact vs the oracle."""
+    n, G = d + p, 4
+    host = _rand(G, n, pitch, S % 1000).numpy()
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    enc = fec.New(d, p)
+    t = _dev(host)
+    enc.encode_batch(t, shard_size=S)
+    assert np.array_equal(t.cpu().numpy()[:, :, :S], want[:, :, :S])
+    rng = np.random.default_rng(S)
+    masks = np.zeros(G, np.uint64)
+    for g in range(G):
+        m = (1 << n) - 1
+        for r in rng.choice(n, size=g * p // (G - 1), replace=False):  # 0 .. p erasures
+            m &= ~(1 << int(r))
+        masks[g] = m
+    inp = _erase(want, masks, n)
+    t = _dev(inp)
+    enc.reconstruct_batch(t, _masks_to_dev(masks), shard_size=S)
+    assert np.array_equal(t.cpu().numpy()[:, :, :S], want[:, :, :S])
