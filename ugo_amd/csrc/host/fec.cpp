@@ -174,11 +174,17 @@ void FEC::recoverGroup(const std::vector<Bytes*>& shards, size_t maxlen, std::ve
       batchS_ = maxlen;
       batchPitch_ = pitch;
       uint8_t* grp = batchBuf_ + pendMask_.size() * n * pitch;
+      // Only the survivors Reconstruct uses -- the first d present rows -- are
+      // staged: the present data rows all come first, so the rows left out are
+      // parity rows, which a data-only recovery never rebuilds.  Same result,
+      // fewer bytes copied.
       uint64_t mask = 0;
-      for (size_t k = 0; k < n; ++k)
+      int kept = 0;
+      for (size_t k = 0; k < n && kept < dataShards_; ++k)
         if (shards[k]) {
           std::memcpy(grp + k * pitch, shards[k]->data(), maxlen);  // shards[k][:maxlen]
           mask |= 1ull << k;
+          ++kept;
         }
       pendMask_.push_back(mask);
       if (pendMask_.size() == static_cast<size_t>(batchCap_)) flushInto(out);
@@ -186,10 +192,16 @@ void FEC::recoverGroup(const std::vector<Bytes*>& shards, size_t maxlen, std::ve
     }
     lastError_ = UGO_FEC_ERR_HIP;  // no pinned batch: recover this group per call
   }
+  // :202 Reconstruct, of which input keeps the data shards (:203-207): the
+  // data-only form over the first d present rows gives those same bytes
   std::vector<Bytes> rs(shardSize_);
-  for (int k = 0; k < shardSize_; ++k)
-    if (shards[k]) rs[k].assign(shards[k]->begin(), shards[k]->begin() + maxlen);  // shards[k][:maxlen]
-  const int err = enc_->Reconstruct(rs);  // :202 -> GPU
+  int kept = 0;
+  for (int k = 0; k < shardSize_ && kept < dataShards_; ++k)
+    if (shards[k]) {
+      rs[k].assign(shards[k]->begin(), shards[k]->begin() + maxlen);  // shards[k][:maxlen]
+      ++kept;
+    }
+  const int err = enc_->ReconstructData(rs);  // -> GPU
   lastError_ = err;
   if (err == UGO_FEC_OK) {
     for (int k = 0; k < dataShards_; ++k)
