@@ -758,3 +758,41 @@ def test_large_shards_vs_oracle(gpu, d, p, S, pitch):
     t = _dev(inp)
     enc.reconstruct_batch(t, _masks_to_dev(masks), shard_size=S)
     assert np.array_equal(t.cpu().numpy()[:, :, :S], want[:, :, :S])
+
+
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES", "150")) // 10, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(d=st.integers(1, 16), p=st.integers(49, 120), S=st.integers(1, 48), pad=st.sampled_from([0, 16]),
+       seed=st.integers(0, 2**31 - 1))
+def test_random_wide_codes_vs_restatement(gpu, d, p, S, pad, seed):
+    """Random codes past 64 shards (multi-word presence masks, host-built
+    descriptors): encode vs the C oracle, reconstruct (in place) vs the
+    independent Python restatement, aligned and unaligned pitches."""
+    n = d + p
+    pitch = (S + 15) // 16 * 16 + pad if pad else S
+    G = 3
+    rng = np.random.default_rng(seed)
+    host = rng.integers(0, 256, (G, n, pitch), dtype=np.uint8)
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    enc = fec.New(d, p)
+    t = _dev(host)
+    enc.encode_batch(t, shard_size=S)
+    assert np.array_equal(t.cpu().numpy()[:, :, :S], want[:, :, :S])
+    M = rs_ref.build_matrix(d, p)
+    words, erased = _wide_masks(G, n, p, rng)
+    inp = want.copy()
+    for g in range(G):
+        for r in erased[g]:
+            inp[g, r] = 0
+    t = _dev(inp)
+    stt = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    enc.reconstruct_batch(t, torch.as_tensor(words.view(np.int64)).cuda(), shard_size=S, status=stt)
+    got = t.cpu().numpy()
+    for g in range(G):
+        rows = [None if r in erased[g] else bytearray(want[g, r, :S].tobytes()) for r in range(n)]
+        err = rs_ref.reconstruct_group(M, d, p, rows)
+        assert int(stt[g]) == (0 if err is None else fec.ErrTooFewShards.code)
+        for r in range(n):
+            exp = bytes(rows[r]) if err is None else inp[g, r, :S].tobytes()
+            assert got[g, r, :S].tobytes() == exp, (g, r)
