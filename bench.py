@@ -179,6 +179,10 @@ def dist_setup(backend: str):
     if world > 1:
         import torch.distributed as dist
 
+        # one node, rendezvous on the loopback address: keep gloo's sockets on
+        # the loopback device too (the container hostname may not resolve)
+        if backend == "gloo" and os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group(backend, init_method="env://")
     return rank, local_rank, world
 
