@@ -282,3 +282,29 @@ def test_fec_object_random_channels(gpu, d, p, extra, groups, max_len, drop, dup
             got += [bytes(x) for x in rc]
     assert got == want
     event(f"recovered shards: {'none' if not want else ('1-9' if len(want) < 10 else '10+')}")
+
+
+@pytest.mark.gpu
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES_CONN", "40")), deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(d=st.integers(1, 12), p=st.integers(1, 5), offset=st.integers(0, 40), width=st.integers(0, 1476),
+       buflen=st.integers(0, 200), seed=st.integers(0, 2**31 - 1))
+def test_calc_ecc_random_windows(gpu, d, p, offset, width, buflen, seed):
+    """calcECC(data, offset, maxlen) on random codes and windows, buffers
+    longer than the window: parity bytes in [offset, maxlen) and every byte
+    outside it equal the restated ugo/fec.go (an empty window: Encode fails,
+    calcECC returns nil and writes nothing)."""
+    n = d + p
+    maxlen = offset + width
+    rng = np.random.default_rng(seed)
+    bufs = [bytearray(rng.integers(0, 256, maxlen + buflen, dtype=np.uint8).tobytes()) for _ in range(n)]
+    ref = [bytearray(b) for b in bufs]
+    f = fec.FecConn(n + 4, d, p)
+    o = fec_ref.FEC.new(n + 4, d, p, clock=lambda: 0)
+    want = o.calcECC(ref, offset, maxlen)
+    if want is None:
+        with pytest.raises(fec.FecError):
+            f.calcECC(bufs, offset, maxlen)
+    else:
+        f.calcECC(bufs, offset, maxlen)
+    assert bufs == ref
