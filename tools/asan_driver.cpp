@@ -97,6 +97,46 @@ void host_round_trip(int d, int p, size_t S, size_t G, bool pinned) {
   ugo_fec_destroy(ctx);
 }
 
+// codes past 64 shards: ceil(n/64) presence words per group, host-built
+// descriptors (round trip as above)
+void host_round_trip_wide(int d, int p, size_t S, size_t G, bool pinned) {
+  const int n = d + p;
+  const size_t W = (n + 63) / 64, pitch = (S + 15) / 16 * 16;
+  ugo_fec* ctx = nullptr;
+  EXPECT(ugo_fec_create(0, d, p, &ctx) == UGO_FEC_OK);
+  if (!ctx) return;
+  const size_t bytes = G * n * pitch;
+  uint8_t* buf = nullptr;
+  std::vector<uint8_t> pageable;
+  if (pinned) {
+    void* v = nullptr;
+    EXPECT(ugo_fec_host_alloc(bytes, &v) == UGO_FEC_OK);
+    buf = static_cast<uint8_t*>(v);
+  } else {
+    pageable.resize(bytes);
+    buf = pageable.data();
+  }
+  for (size_t i = 0; i < bytes; ++i) buf[i] = rb();
+  EXPECT(ugo_fec_encode_host(ctx, buf, G, S, pitch) == UGO_FEC_OK);
+  std::vector<uint8_t> ref(buf, buf + bytes);
+  std::vector<uint64_t> mask(G * W, ~0ull);
+  std::vector<int8_t> st(G, -1);
+  for (size_t g = 0; g < G; ++g) {
+    for (int r = n; r < static_cast<int>(64 * W); ++r) mask[g * W + r / 64] &= ~(1ull << (r % 64));
+    const int e = static_cast<int>(rng() % (p + 1));
+    for (int k = 0; k < e; ++k) {
+      const int r = static_cast<int>(rng() % n);
+      mask[g * W + r / 64] &= ~(1ull << (r % 64));
+      std::memset(buf + (g * n + r) * pitch, 0xA5, S);
+    }
+  }
+  EXPECT(ugo_fec_reconstruct_host(ctx, buf, mask.data(), G, S, pitch, 0, st.data()) == UGO_FEC_OK);
+  for (size_t g = 0; g < G; ++g) EXPECT(st[g] == 0);
+  EXPECT(std::memcmp(buf, ref.data(), bytes) == 0);
+  if (pinned) ugo_fec_host_free(buf);
+  ugo_fec_destroy(ctx);
+}
+
 // the FEC object: TX by markData / calcECC / markFEC over reused buffers, RX
 // over a lossy, duplicating channel per call and batched -- same recovered
 // sequence, and every lost full-length payload comes back
@@ -236,6 +276,8 @@ int main() {
     host_round_trip(4, 2, 77, 7, pinned);
     host_round_trip(32, 8, 9000, 12, pinned);
     host_round_trip(20, 9, 1100, 33, pinned);
+    host_round_trip_wide(70, 10, 64, 5, pinned);
+    host_round_trip_wide(8, 120, 48, 3, pinned);
   }
   fec_object(1);
   fec_object(16);
