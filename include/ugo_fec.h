@@ -94,6 +94,10 @@ int ugo_fec_encode(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_si
  * The shard-major ("planar") batch layout [d+p][groups][pitch] -- row_stride =
  * groups*pitch, group_stride = pitch -- turns every shard index into one
  * sequential HBM stream and is the fastest layout on MI355X.
+ * No two shard slots may overlap: the smaller stride must be >= shard_size and
+ * the larger one must clear a whole run of the smaller ((count - 1) * smaller
+ * + shard_size), else UGO_FEC_ERR_INVALID_ARG before any launch (the same rule
+ * holds for every strided batch below).
  * Fast path: shards, row_stride and group_stride all multiples of 16. */
 int ugo_fec_encode_strided(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_size,
                            size_t row_stride, size_t group_stride, void* stream);

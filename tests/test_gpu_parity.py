@@ -587,6 +587,31 @@ def test_reconstruct_into_rejects_bad_outputs(gpu):
     assert torch.equal(o[:, 0, :S], torch.zeros_like(o[:, 0, :S]))  # all-zero codeword: row 0 rebuilt as zeros
 
 
+def test_overlapping_batch_layouts_rejected(gpu):
+    """Strided batches whose shard slots overlap (kernels would write rows
+    other lanes read) are refused before any launch; the disjoint group-major
+    and planar layouts of the same buffer are accepted."""
+    d, p, S, G = 10, 3, 1350, 4
+    n, pitch = d + p, 1360
+    enc = fec.New(d, p)
+    lib = fec.load_library()
+    t = torch.zeros((G * n + 2, pitch), dtype=torch.uint8, device="cuda")
+    m = _masks_to_dev(np.full(G, (1 << n) - 2, np.uint64))
+    bad = [(pitch, (n - 1) * pitch),       # group g's last row is group g+1's first
+           (2 * pitch, pitch),             # groups interleave into each other's rows
+           (S - 1, n * pitch)]             # rows overlap inside a group
+    good = [(pitch, n * pitch), (G * pitch, pitch)]
+    for rs, gs in bad:
+        assert lib.ugo_fec_encode_strided(enc._h, t.data_ptr(), G, S, rs, gs, None) == fec.ErrInvalidArg.code
+        assert lib.ugo_fec_reconstruct_strided(enc._h, t.data_ptr(), m.data_ptr(), G, S, rs, gs, 0, None,
+                                               None) == fec.ErrInvalidArg.code
+    for rs, gs in good:
+        assert lib.ugo_fec_encode_strided(enc._h, t.data_ptr(), G, S, rs, gs, None) == 0
+        assert lib.ugo_fec_reconstruct_strided(enc._h, t.data_ptr(), m.data_ptr(), G, S, rs, gs, 0, None, None) == 0
+    torch.cuda.synchronize()
+    assert not bool(t.any())  # all-zero codewords stay zero
+
+
 @settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES", "150")), deadline=None, derandomize=True,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(d=st.integers(1, 48), p=st.integers(1, 16), S=st.integers(1, 2100), pad=st.sampled_from([0, 3, 16]),

@@ -15,7 +15,6 @@
 #include <cstring>
 #include <new>
 #include <string>
-#include <string>
 #include <unordered_map>
 #include <vector>
 
@@ -222,17 +221,6 @@ ugo::kern::Batch base_batch(const ugo_fec* c, uint8_t* shards, size_t S, const L
   return a;
 }
 
-int check_batch(const ugo_fec* c, const void* shards, size_t groups, size_t S, const Layout& L) {
-  if (!c) return UGO_FEC_ERR_INVALID_ARG;
-  if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;  // checkShards: all shards empty
-  if (S > 0xffffffffu) return UGO_FEC_ERR_INVALID_ARG;
-  if (groups == 0) return UGO_FEC_OK;  // an empty batch has no layout to check
-  if (c->n > 1 && L.rstride < S) return UGO_FEC_ERR_INVALID_ARG;   // rows would overlap
-  if (groups > 1 && L.gstride < S) return UGO_FEC_ERR_INVALID_ARG;
-  if (groups && !shards) return UGO_FEC_ERR_INVALID_ARG;
-  return UGO_FEC_OK;
-}
-
 // Bytes spanned by `rows` x `groups` slots of S bytes (row r of group g at
 // g*gstride + r*rstride).
 size_t extent(size_t S, size_t rstride, size_t rows, size_t gstride, size_t groups) {
@@ -251,6 +239,17 @@ bool layout_disjoint(size_t S, size_t rstride, size_t rows, size_t gstride, size
   if (ns > 1 && small < S) return false;
   if (nl > 1 && large < (ns - 1) * small + S) return false;
   return true;
+}
+
+int check_batch(const ugo_fec* c, const void* shards, size_t groups, size_t S, const Layout& L) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;  // checkShards: all shards empty
+  if (S > 0xffffffffu) return UGO_FEC_ERR_INVALID_ARG;
+  if (groups == 0) return UGO_FEC_OK;  // an empty batch has no layout to check
+  // no two shard slots may overlap: kernels write rows other lanes read
+  if (!layout_disjoint(S, L.rstride, size_t(c->n), L.gstride, groups)) return UGO_FEC_ERR_INVALID_ARG;
+  if (groups && !shards) return UGO_FEC_ERR_INVALID_ARG;
+  return UGO_FEC_OK;
 }
 
 int encode_dev(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, const Layout& L, hipStream_t s) {
@@ -841,7 +840,7 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
       reinterpret_cast<uintptr_t>(shards) % 16 || row_stride % 16 || group_stride % 16 ||
       (pad && reinterpret_cast<uintptr_t>(pad) % 16) || S > 0xffffffffu)
     return UGO_FEC_ERR_INVALID_ARG;
-  if ((c->n > 1 && row_stride < S) || (groups > 1 && group_stride < S)) return UGO_FEC_ERR_INVALID_ARG;
+  if (!layout_disjoint(S, row_stride, size_t(c->n), group_stride, groups)) return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
   if (!device_view(wire) || !device_view(lens) || !device_view(pad) || !device_view(shards) ||
