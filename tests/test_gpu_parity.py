@@ -610,6 +610,12 @@ def test_overlapping_batch_layouts_rejected(gpu):
         assert lib.ugo_fec_reconstruct_strided(enc._h, t.data_ptr(), m.data_ptr(), G, S, rs, gs, 0, None, None) == 0
     torch.cuda.synchronize()
     assert not bool(t.any())  # all-zero codewords stay zero
+    # the binding's size checks are explicit (they hold under python -O)
+    with pytest.raises(ValueError):
+        enc.reconstruct_batch(t[: G * n].view(G, n, pitch), m[:-1], shard_size=S)
+    with pytest.raises(ValueError):
+        enc.reconstruct_into(t[: G * n].view(G, n, pitch), m, torch.zeros((p, G - 1, pitch), dtype=torch.uint8,
+                                                                          device="cuda"), shard_size=S)
 
 
 @settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES", "150")), deadline=None, derandomize=True,

@@ -458,7 +458,9 @@ int ensure_stage(ugo_fec* c, size_t pitch) {
 // Device view of a buffer a kernel will touch: device (or managed) memory as
 // is, pinned host memory through its device mapping (the kernel then reads or
 // writes it over PCIe: zero-copy, e.g. a recvmmsg ring), anything else --
-// pageable host memory the GPU cannot reach -- rejected instead of faulting.
+// pageable host memory the GPU cannot reach, or another GPU's memory -- rejected
+// instead of faulting.  Called under the context's DeviceGuard, so the current
+// device is the one the kernels run on.
 template <typename T>
 bool device_view(T*& p) {
   if (!p) return true;
@@ -467,8 +469,11 @@ bool device_view(T*& p) {
     (void)hipGetLastError();
     return false;
   }
-  if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged || at.type == hipMemoryTypeUnified)
-    return true;
+  if (at.type == hipMemoryTypeManaged || at.type == hipMemoryTypeUnified) return true;
+  if (at.type == hipMemoryTypeDevice) {
+    int cur = -1;
+    return hipGetDevice(&cur) == hipSuccess && at.device == cur;
+  }
   if (at.type != hipMemoryTypeHost || !at.devicePointer) return false;  // unregistered (pageable) memory
   if (at.devicePointer == at.hostPointer) return true;  // one address for host and device (ROCm)
   auto* base = static_cast<uint8_t*>(at.devicePointer);

@@ -155,6 +155,13 @@ def strerror(code: int) -> str:
     return load_library().ugo_fec_strerror(code).decode()
 
 
+def _require(cond, msg: str = "argument does not match the batch layout the entry point expects"):
+    """Argument checks that guard device memory (sizes the kernels index by):
+    explicit, so they hold under `python -O` too."""
+    if not cond:
+        raise ValueError(msg)
+
+
 def _raise(code: int):
     if code != OK:
         raise _ERRORS.get(code, FecError)(f"{strerror(code)} (status {code})")
@@ -214,14 +221,14 @@ class Encoder:
         last dimension is contiguous: group-major [G, d+p, pitch] or
         shard-major [d+p, G, pitch] (planar); the row and group strides are the
         tensor's own (a padded row stride is a strided view)."""
-        assert shards.dim() == 3 and shards.element_size() == 1 and shards.stride(2) == 1
+        _require(shards.dim() == 3 and shards.element_size() == 1 and shards.stride(2) == 1)
         if shard_major:
             n, G, pitch = shards.shape
             rs, gs = shards.stride(0), shards.stride(1)
         else:
             G, n, pitch = shards.shape
             gs, rs = shards.stride(0), shards.stride(1)
-        assert n == self.Shards, f"expected {self.Shards} rows per group, got {n}"
+        _require(n == self.Shards, f"expected {self.Shards} rows per group, got {n}")
         return G, pitch, rs, gs
 
     def encode_batch(self, shards, shard_size: Optional[int] = None, stream=None, shard_major: bool = False):
@@ -238,7 +245,7 @@ class Encoder:
         non-empty), [G][W] words for d+p > 64 (W = mask_words); status: optional int8
         CUDA tensor [G]."""
         G, pitch, rs, gs = self._geom(shards, shard_major)
-        assert present.is_contiguous() and present.numel() == G * self.mask_words and present.element_size() == 8
+        _require(present.is_contiguous() and present.numel() == G * self.mask_words and present.element_size() == 8)
         S = pitch if shard_size is None else shard_size
         st = None if status is None else status.data_ptr()
         _raise(load_library().ugo_fec_reconstruct_strided(self._h, shards.data_ptr(), present.data_ptr(), G, S, rs,
@@ -252,19 +259,19 @@ class Encoder:
         i-th erased row, ascending) goes to `out`, a contiguous uint8 CUDA tensor
         [p][G][opitch] (out_shard_major) or [G][p][opitch]."""
         G, pitch, rs, gs = self._geom(shards, shard_major)
-        assert present.is_contiguous() and present.numel() == G * self.mask_words and present.element_size() == 8
-        assert out.is_contiguous() and out.element_size() == 1 and out.dim() == 3
+        _require(present.is_contiguous() and present.numel() == G * self.mask_words and present.element_size() == 8)
+        _require(out.is_contiguous() and out.element_size() == 1 and out.dim() == 3)
         p = self.ParityShards
         if out_shard_major:
-            assert out.shape[0] == p and out.shape[1] == G
+            _require(out.shape[0] == p and out.shape[1] == G)
             opitch = out.shape[2]
             ors, ogs = G * opitch, opitch
         else:
-            assert out.shape[0] == G and out.shape[1] == p
+            _require(out.shape[0] == G and out.shape[1] == p)
             opitch = out.shape[2]
             ors, ogs = opitch, p * opitch
         S = pitch if shard_size is None else shard_size
-        assert opitch >= S
+        _require(opitch >= S)
         st = None if status is None else status.data_ptr()
         _raise(load_library().ugo_fec_reconstruct_into(self._h, shards.data_ptr(), present.data_ptr(), G, S, rs, gs,
                                                        out.data_ptr(), ors, ogs,
@@ -280,10 +287,10 @@ class Encoder:
         window, too short, duplicate) or None.  A repeated seqid keeps its first
         copy in ring order (ugo/fec.go:123-129)."""
         if stats is not None:
-            assert stats.numel() >= 5 and stats.element_size() == 4
+            _require(stats.numel() >= 5 and stats.element_size() == 4)
         G, pitch, rs, gs = self._geom(shards, shard_major)
         npk, slot = wire.shape
-        assert wire.is_contiguous() and lens.is_contiguous() and lens.element_size() == 2 and lens.numel() == npk
+        _require(wire.is_contiguous() and lens.is_contiguous() and lens.element_size() == 2 and lens.numel() == npk)
         S = pitch if shard_size is None else shard_size
         _raise(load_library().ugo_fec_rx_assemble(
             self._h, wire.data_ptr(), slot, lens.data_ptr(), npk, None if pad is None else pad.data_ptr(),
@@ -299,13 +306,13 @@ class Encoder:
         status = int8 CUDA [G] or None."""
         d, n = self.DataShards, self.Shards
         npk, slot_in = pkts.shape
-        assert npk % d == 0, "pkts must hold whole groups of d data packets"
+        _require(npk % d == 0, "pkts must hold whole groups of d data packets")
         G = npk // d
-        assert wire.shape[0] == G * n and wire_lens.numel() == G * n and lens.numel() == npk
-        assert pkts.is_contiguous() and wire.is_contiguous() and lens.is_contiguous() and wire_lens.is_contiguous()
-        assert lens.element_size() == 2 and wire_lens.element_size() == 2
+        _require(wire.shape[0] == G * n and wire_lens.numel() == G * n and lens.numel() == npk)
+        _require(pkts.is_contiguous() and wire.is_contiguous() and lens.is_contiguous() and wire_lens.is_contiguous())
+        _require(lens.element_size() == 2 and wire_lens.element_size() == 2)
         if status is not None:
-            assert status.numel() == G and status.element_size() == 1
+            _require(status.numel() == G and status.element_size() == 1)
         _raise(load_library().ugo_fec_tx_assemble(
             self._h, pkts.data_ptr(), slot_in, lens.data_ptr(), G, first_seq,
             None if pad is None else pad.data_ptr(), max_len, wire.data_ptr(), wire.shape[1],
@@ -318,12 +325,12 @@ class Encoder:
         view on the host with PKT_INFO_DTYPE --, ranges int64 [npk, max_ranges, 2],
         segs [npk, max_segments, 16] bytes -- PKT_SEGMENT_DTYPE)."""
         npk, slot = pkts.shape
-        assert pkts.is_contiguous() and lens.is_contiguous() and lens.element_size() == 2 and lens.numel() == npk
+        _require(pkts.is_contiguous() and lens.is_contiguous() and lens.element_size() == 2 and lens.numel() == npk)
         dev = pkts.device
         if out is not None:  # reuse (info, ranges, segs) from an earlier call
             info, ranges, segs = out
-            assert info.shape == (npk, 64) and ranges.shape[0] == npk and segs.shape[0] == npk
-            assert ranges.shape[1] >= max(max_ranges, 1) and segs.shape[1] >= max(max_segments, 1)
+            _require(info.shape == (npk, 64) and ranges.shape[0] == npk and segs.shape[0] == npk)
+            _require(ranges.shape[1] >= max(max_ranges, 1) and segs.shape[1] >= max(max_segments, 1))
         else:
             info = torch.empty((npk, 64), dtype=torch.uint8, device=dev)
             ranges = torch.zeros((npk, max(max_ranges, 1), 2), dtype=torch.int64, device=dev)
@@ -355,9 +362,9 @@ class Encoder:
 
     # ------------------------------------------------------ host-buffer batch
     def encode_host(self, shards: np.ndarray, shard_size: Optional[int] = None):
-        assert shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"] and shards.ndim == 3
+        _require(shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"] and shards.ndim == 3)
         G, n, pitch = shards.shape
-        assert n == self.Shards
+        _require(n == self.Shards)
         S = pitch if shard_size is None else shard_size
         _raise(load_library().ugo_fec_encode_host(self._h, shards.ctypes.data, G, S, pitch))
 
@@ -366,15 +373,15 @@ class Encoder:
         """Returns the aggregate status (0 or the first failing group's code);
         per-group codes go to `status` when given.  Does not raise for
         ErrTooFewShards groups (they are reported and left untouched)."""
-        assert shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"] and shards.ndim == 3
+        _require(shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"] and shards.ndim == 3)
         G, n, pitch = shards.shape
-        assert n == self.Shards
+        _require(n == self.Shards)
         present = np.ascontiguousarray(present, dtype=np.uint64)
-        assert present.size == G * self.mask_words
+        _require(present.size == G * self.mask_words)
         S = pitch if shard_size is None else shard_size
         st = None if status is None else status.ctypes.data
         if status is not None:
-            assert status.dtype == np.int8 and status.size == G
+            _require(status.dtype == np.int8 and status.size == G)
         rc = load_library().ugo_fec_reconstruct_host(self._h, shards.ctypes.data, present.ctypes.data, G, S, pitch,
                                                      RECONSTRUCT_DATA_ONLY if data_only else 0, st)
         if rc not in (OK, ErrTooFewShards.code, ErrSingular.code):
