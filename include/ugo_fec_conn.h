@@ -45,7 +45,10 @@ int ugo_fecconn_set_next(ugo_fecconn* f, uint32_t next);
 /* The RX hook of Conn.handlePacket (ugo/conn.go:394-396): decode(wire) then,
  * when the flag is typeData or typeFEC, input(pkt).  Recovered data shards
  * (ugo/fec.go:203-207) are written to out + i*UGO_FEC_MAX_PACKET (out_cap
- * bytes available); *nrec receives their count and *rec_len their length. */
+ * bytes available); *nrec receives their count and *rec_len their length.
+ * out_cap >= d * UGO_FEC_MAX_PACKET (one group's data shards; batch mode:
+ * below), checked before the packet is consumed: UGO_FEC_ERR_INVALID_ARG and
+ * no state change otherwise. */
 int ugo_fecconn_input(ugo_fecconn* f, const uint8_t* wire, size_t len, uint32_t* seqid, uint16_t* flag,
                       uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len);
 

@@ -213,6 +213,26 @@ def test_set_batch_flushes_pending_and_rejects_bad_sizes(gpu):
     del rng
 
 
+@pytest.mark.gpu
+def test_input_refuses_a_short_output_buffer_before_consuming(gpu):
+    """Per-call input needs room for d recovered shards up front: a shorter
+    buffer is refused and the packet is not taken into the rx queue."""
+    import ctypes
+
+    tx = fec_ref.FEC.new(RXLIMIT, D, P, clock=lambda: 0)
+    pk, _ = _tx_stream(tx, 1, np.random.default_rng(5), True)
+    rx = fec.FecConn(RXLIMIT, D, P)
+    rx.set_clock(lambda: 0)
+    w = (ctypes.c_uint8 * len(pk[0])).from_buffer_copy(pk[0])
+    small = (ctypes.c_uint8 * ((D - 1) * fec.UGO_FEC_MAX_PACKET))()
+    nrec, rlen = ctypes.c_int(), ctypes.c_size_t()
+    st = rx._lib.ugo_fecconn_input(rx._h, ctypes.addressof(w), len(pk[0]), None, None, ctypes.addressof(small),
+                                   len(small), ctypes.byref(nrec), ctypes.byref(rlen))
+    assert st == fec.ErrInvalidArg.code and rx.rx_len() == 0
+    rx.input(pk[0])  # the binding's own buffer holds d shards
+    assert rx.rx_len() == 1
+
+
 def _tx_stream_any(tx, d, p, groups, rng, max_len):
     """_tx_stream for any (d, p): the sender loop with reused group buffers."""
     n = d + p

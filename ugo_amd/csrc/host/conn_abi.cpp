@@ -27,12 +27,16 @@ int emit(const std::vector<ugo::Bytes>& rec, uint8_t* out, size_t out_cap, int* 
   return UGO_FEC_OK;
 }
 
-// In batch mode one call can return a whole batch: the caller's buffer must
-// hold it before anything is consumed.
-bool batch_cap_ok(const ugo_fecconn* f, const uint8_t* out, size_t out_cap) {
-  const size_t cap = static_cast<size_t>(f->fec->batch());
-  if (cap == 0) return true;
-  return out && out_cap >= cap * static_cast<size_t>(f->fec->dataShards()) * ugo::maxPacketSize;
+// The caller's buffer must hold the most one call can return before anything
+// is consumed (a packet taken into the rx queue whose recovered shards then
+// fail to fit would lose them): a whole batch of groups in batch mode, and for
+// input in per-call mode one group's d shards.  set_batch / flush in per-call
+// mode have nothing pending to return.
+bool batch_cap_ok(const ugo_fecconn* f, const uint8_t* out, size_t out_cap, bool per_call_input = false) {
+  size_t groups = static_cast<size_t>(f->fec->batch());
+  if (groups == 0 && per_call_input) groups = 1;
+  if (groups == 0) return true;
+  return out && out_cap >= groups * static_cast<size_t>(f->fec->dataShards()) * ugo::maxPacketSize;
 }
 
 }  // namespace
@@ -99,7 +103,7 @@ int ugo_fecconn_input(ugo_fecconn* f, const uint8_t* wire, size_t len, uint32_t*
   if (!f || !wire || len < ugo::fecHeaderSize) return UGO_FEC_ERR_INVALID_ARG;
   if (nrec) *nrec = 0;
   if (rec_len) *rec_len = 0;
-  if (!batch_cap_ok(f, out, out_cap)) return UGO_FEC_ERR_INVALID_ARG;
+  if (!batch_cap_ok(f, out, out_cap, true)) return UGO_FEC_ERR_INVALID_ARG;
   ugo::fecPacket pkt = f->fec->decode(wire, len);
   if (seqid) *seqid = pkt.seqid;
   if (flag) *flag = pkt.flag;
