@@ -250,6 +250,26 @@ int main(int argc, char** argv) {
   add(k_encode_g<32, 8, 2, 8>, a, enc_bytes, "enc const-network lds-dma 8 rows, nt stores (production since round 2)");
   add(k_encode_g<32, 8, 2, 16>, a, enc_bytes, "enc const-network lds-dma 16 rows, nt stores (round-1 production)");
   add(k_encode_g<32, 8, 0, 8>, a, enc_bytes, "enc const-network lds-dma 8 rows");
+  const size_t kFr = vars.size();
+  add(k_encode_fr<32, 8, 2, 8>, a, enc_bytes, "enc FOUR-RUSSIANS network (blocks of 3), lds-dma 8 rows, nt stores");
+  add(k_encode_fr<32, 8, 2, 8, 256, 8, 3>, a, enc_bytes, "enc FOUR-RUSSIANS network (blocks of 3), lds-dma 8 rows, nt stores, 3 waves/SIMD");
+  add(k_encode_fr<32, 8, 2, 8, 256, 8, 2>, a, enc_bytes, "enc FOUR-RUSSIANS network (blocks of 3), lds-dma 8 rows, nt stores, 2 waves/SIMD");
+  add(k_encode_frs<32, 8, 2, 8, 256, 8, 1>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, lds-dma 8 rows, nt stores");
+  add(k_encode_frs<32, 8, 2, 8, 256, 8, 3>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, lds-dma 8 rows, nt stores, 3 waves/SIMD");
+  add(k_encode_frs<32, 8, 2, 16, 256, 16, 3>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, lds-dma 16 rows, nt stores, 3 waves/SIMD");
+  add(k_encode_frs<32, 8, 2, 12, 256, 12, 3>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, lds-dma 12 rows, nt stores, 3 waves/SIMD");
+  add(k_encode_frs<32, 8, 2, 20, 256, 20, 3>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, lds-dma 20 rows, nt stores, 3 waves/SIMD");
+  {
+    const uint32_t g128 = (a.items + 127) / 128, g64 = (a.items + 63) / 64;
+    vars.push_back({"enc FOUR-RUSSIANS SEQ dwords, lds-dma 16 rows, 128-thread blocks", enc_bytes, [=]() {
+      hipLaunchKernelGGL((k_encode_frs<32, 8, 2, 16, 128, 16, 3>), dim3(g128), dim3(128), 0, 0, a); }, {}});
+    vars.push_back({"enc FOUR-RUSSIANS SEQ dwords, lds-dma 20 rows, 128-thread blocks", enc_bytes, [=]() {
+      hipLaunchKernelGGL((k_encode_frs<32, 8, 2, 20, 128, 20, 3>), dim3(g128), dim3(128), 0, 0, a); }, {}});
+    vars.push_back({"enc FOUR-RUSSIANS SEQ dwords, lds-dma 24 rows, 64-thread blocks", enc_bytes, [=]() {
+      hipLaunchKernelGGL((k_encode_frs<32, 8, 2, 24, 64, 24, 3>), dim3(g64), dim3(64), 0, 0, a); }, {}});
+    vars.push_back({"enc FOUR-RUSSIANS SEQ dwords, lds-dma 32 rows, 64-thread blocks", enc_bytes, [=]() {
+      hipLaunchKernelGGL((k_encode_frs<32, 8, 2, 32, 64, 32, 3>), dim3(g64), dim3(64), 0, 0, a); }, {}});
+  }
   add(k_apply_q<8, 0, 1, 1, 4>, ae, enc_bytes, "enc perm-tables streaming ring4 nt1");
   add(k_apply_q<8, 0, 1, 1, 8>, ae, enc_bytes, "enc perm-tables streaming ring8 nt1");
   add(k_apply_q<8, 0, 3, 1, 4>, ae, enc_bytes, "enc perm-tables streaming ring4 nt3 (generic-code encode, production)");
@@ -341,6 +361,13 @@ int main(int argc, char** argv) {
     vars[2].go();
     CK(hipMemcpy(h2.data(), buf, h.size(), hipMemcpyDeviceToHost));
     printf("{\"check\":\"perm encode == const encode\",\"equal\":%s}\n", same_rows(h1, h2) ? "true" : "false");
+    for (size_t f = kFr; f < kFr + 12; ++f) {
+      CK(hipMemset(buf + size_t(d) * a.rstride, 0, size_t(p) * a.rstride));
+      vars[f].go();
+      CK(hipMemcpy(h2.data(), buf, h.size(), hipMemcpyDeviceToHost));
+      printf("{\"check\":\"%s == const encode\",\"equal\":%s}\n", vars[f].name.c_str(),
+             same_rows(h1, h2) ? "true" : "false");
+    }
     std::vector<uint8_t> h3(h.size());
     vars[4].go();  // reconstruct of a consistent batch rewrites erased rows with the same bytes
     CK(hipMemcpy(h3.data(), buf, h.size(), hipMemcpyDeviceToHost));

@@ -25,7 +25,11 @@
 //
 //  * k_encode_c<D,P> / k_encode_g<D,P>: coefficients are compile-time
 //    (gf::Code<D,P>), so the XOR network is fixed at compile time -- the (10,3)
-//    headline and the (32,8) jumbo geometry (k_encode_g in production).
+//    headline (k_encode_g in production) and the (32,8) jumbo geometry
+//    (k_encode_frs in production: the bit-plane sums Tb in Four-Russians form,
+//    one precomputed XOR combination per block of 3 inputs instead of one
+//    term per input, dword by dword: ~20% fewer VALU for the VALU-bound wide
+//    code, gf_device.hpp cparity_fr_seq).
 //  * k_apply_p<DMAX,MODE>: runtime coefficients through split v_perm_b32
 //    tables (the headline reconstruct), k_apply_q its streaming form for wide
 //    codes, k_apply_qa the wave-aligned streaming form (the jumbo reconstruct:
@@ -128,6 +132,52 @@ __global__ __launch_bounds__(BS) void k_encode_g(Batch a) {
 #pragma unroll
   for (int k = 0; k < GR; ++k) x[k] = lds16(&stage[w][k][lane]);
   cparity_store<D, P, NTS>(l.gp, a.rstride, l.nb, x, std::make_integer_sequence<int, P>{});
+}
+
+// k_encode_g with the network in Four-Russians form (cparity_fr): fewer VALU
+// for wide codes, whose encode is VALU-bound.
+template <int D, int P, int NTS = 0, int GR = D, int BS = 256, int LR = GR, int WPE = 1>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode_fr(Batch a) {
+  static_assert(LR >= GR, "the stage holds at least the staged rows");
+  __shared__ u32x4 stage[BS / 64][LR][64];
+  const uint32_t item = blockIdx.x * BS + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const Loc l = locate(a, item);
+#pragma unroll
+  for (int k = 0; k < GR; ++k) lds_dma16(l.gp + static_cast<uint64_t>(k) * a.rstride, &stage[w][k][0]);
+  V4 x[D];
+#pragma unroll
+  for (int k = GR; k < D; ++k) x[k] = load16<1>(l.gp + static_cast<uint64_t>(k) * a.rstride);
+  lds_dma_wait();
+#pragma unroll
+  for (int k = 0; k < GR; ++k) x[k] = lds16(&stage[w][k][lane]);
+  V4 y[P];
+  cparity_fr<D, P>(y, x);
+#pragma unroll
+  for (int i = 0; i < P; ++i) store16<NTS>(l.gp + static_cast<uint64_t>(D + i) * a.rstride, y[i], l.nb);
+}
+
+// k_encode_fr with the dwords forced in sequence (cparity_fr_seq): staged rows
+// read from LDS per dword, so the live set is one dword's tables.
+template <int D, int P, int NTS = 0, int GR = D, int BS = 256, int LR = GR, int WPE = 1>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode_frs(Batch a) {
+  static_assert(LR >= GR, "the stage holds at least the staged rows");
+  __shared__ u32x4 stage[BS / 64][LR][64];
+  const uint32_t item = blockIdx.x * BS + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const Loc l = locate(a, item);
+#pragma unroll
+  for (int k = 0; k < GR; ++k) lds_dma16(l.gp + static_cast<uint64_t>(k) * a.rstride, &stage[w][k][0]);
+  V4 x[D];
+#pragma unroll
+  for (int k = GR; k < D; ++k) x[k] = load16<1>(l.gp + static_cast<uint64_t>(k) * a.rstride);
+  lds_dma_wait();
+  V4 y[P];
+  cparity_fr_seq<D, P, GR>(y, x, reinterpret_cast<const uint32_t*>(&stage[w][0][lane]));
+#pragma unroll
+  for (int i = 0; i < P; ++i) store16<NTS>(l.gp + static_cast<uint64_t>(D + i) * a.rstride, y[i], l.nb);
 }
 
 // ----------------------------------------------- descriptor-driven kernels
@@ -1008,10 +1058,14 @@ constexpr int kEncNT = 3;    // nontemporal loads and stores
 constexpr int kEncLdsRows = 8;  // (10,3): rows 0-7 by LDS-DMA nt, 8-9 to registers
 constexpr int kEncStageRows = 13;  // (10,3): 52-KiB stage, 3 blocks per CU (see k_encode_g)
 constexpr int kEncJumboNT = 3;  // (32,8): NT loads and stores (578 vs 615 us, tools/jvariants.hip)
-// (32,8): rows 0-7 by LDS-DMA nt.  The round-1 pick of 16 rows (557 vs 571
-// us) lost to 8 rows in 9 of 12 interleaved round-2 runs (medians 565 vs 584 us)
-// (profiles/r2/jvariants_lds_rows_r2.txt)
-constexpr int kEncJumboLdsRows = 8;
+// (32,8): the network in Four-Russians form with the dwords in sequence
+// (k_encode_frs), rows 0-15 by LDS-DMA nt and read from LDS one dword at a
+// time, 133 VGPRs, 2 blocks per CU (64-KiB stage): 519.9 / 524.6 us against
+// 548.9 / 567.2 us for the Horner network k_encode_g with 8 staged rows on two
+// boxes, byte-identical parity (profiles/r2/jvariants_frs*.jsonl).  The
+// Horner network's own pick was 8 staged rows (565 vs 584 us for 16 in 9 of
+// 12 interleaved runs, profiles/r2/jvariants_lds_rows_r2.txt).
+constexpr int kEncJumboLdsRows = 16;
 constexpr int kApplyNT = 3;  // nontemporal loads and stores
 constexpr int kApplyPNT = 3; // k_apply_p: nontemporal loads and stores (cold: 201.0 vs 228.4 us)
 constexpr int kApplyQNT = 3; // k_apply_q (jumbo): NT loads and stores (548 vs 572 us)
@@ -1034,7 +1088,8 @@ hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   if (d == 10 && p == 3)
     launch(kKEncode, k_encode_g<10, 3, kEncNT & 2, kEncLdsRows, 256, kEncStageRows>, grid, block, 0, s, a);
   else if (d == 32 && p == 8)
-    launch(kKEncode, k_encode_g<32, 8, kEncJumboNT & 2, kEncJumboLdsRows>, grid, block, 0, s, a);
+    launch(kKEncode, k_encode_frs<32, 8, kEncJumboNT & 2, kEncJumboLdsRows, 256, kEncJumboLdsRows, 3>, grid, block,
+           0, s, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -271,6 +271,148 @@ __device__ __forceinline__ void cparity_store(uint8_t* gp, uint64_t pitch, uint3
   ((store16<NT>(gp + static_cast<uint64_t>(D + I) * pitch, cparity<D, P, I>(x), nb)), ...);
 }
 
+// ---- the same network in Four-Russians form (wide codes, VALU-bound) ----
+// Inputs in blocks of 3.  Per dword, the 7 nonzero XOR combinations of each
+// block are formed once (4 new values per block: ab, ac, bc, abc), and every
+// bit-plane sum T(I, B) then takes ONE combination per block instead of one
+// term per input: for (32,8) about 9.5 terms instead of 16 per plane, 64
+// planes per dword, against 44 extra XORs per dword for the combinations.
+constexpr int kFrBlock = 3;
+
+template <int D, int P, int I, int B>
+struct FrTerms {
+  static constexpr int NB = (D + kFrBlock - 1) / kFrBlock;
+  struct List {
+    int n;
+    int blk[NB];
+    int idx[NB];
+  };
+  static constexpr List make() {
+    List l{};
+    for (int bl = 0; bl < NB; ++bl) {
+      int v = 0;
+      for (int t = 0; t < kFrBlock; ++t) {
+        const int k = kFrBlock * bl + t;
+        if (k < D && ((gf::Code<D, P>::M.at(D + I, k) >> B) & 1)) v |= 1 << t;
+      }
+      if (v) {
+        l.blk[l.n] = bl;
+        l.idx[l.n] = v;
+        ++l.n;
+      }
+    }
+    return l;
+  }
+  static constexpr List L = make();
+};
+
+template <int D, int P, int I, int B, int J, int NB>
+__device__ __forceinline__ void fr_fold(uint32_t& y, const uint32_t (*c)[8]) {
+  constexpr auto L = FrTerms<D, P, I, B>::L;
+  if constexpr (J + 1 < L.n) {
+    y = xor3(y, c[L.blk[J]][L.idx[J]], c[L.blk[J + 1]][L.idx[J + 1]]);
+    fr_fold<D, P, I, B, J + 2, NB>(y, c);
+  } else if constexpr (J < L.n) {
+    y ^= c[L.blk[J]][L.idx[J]];
+  }
+}
+
+template <int D, int P, int I, int B, int NB>
+__device__ __forceinline__ void fr_horner(uint32_t& y, const uint32_t (*c)[8]) {
+  constexpr auto L = FrTerms<D, P, I, B>::L;
+  if constexpr (any_bit_at_or_above<D, P, I, B + 1>()) {
+    y = xt1(y);
+    fr_fold<D, P, I, B, 0, NB>(y, c);
+  } else if constexpr (L.n > 0) {
+    y = c[L.blk[0]][L.idx[0]];
+    fr_fold<D, P, I, B, 1, NB>(y, c);
+  }
+  if constexpr (B > 0) fr_horner<D, P, I, B - 1, NB>(y, c);
+}
+
+template <int D, int P, int NB, int... I>
+__device__ __forceinline__ void fr_outputs(V4* y, int j, const uint32_t (*c)[8], std::integer_sequence<int, I...>) {
+  ((y[I].v[j] = 0u, fr_horner<D, P, I, 7, NB>(y[I].v[j], c)), ...);
+}
+
+// All P parity chunks of one column chunk, dword by dword (so only one dword's
+// combinations are live at a time).
+template <int D, int P>
+__device__ __forceinline__ void cparity_fr(V4* y, const V4* x) {
+  constexpr int NB = (D + kFrBlock - 1) / kFrBlock;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t c[NB][8];
+#pragma unroll
+    for (int bl = 0; bl < NB; ++bl) {
+      const int k = kFrBlock * bl;
+      const uint32_t a = x[k].v[j];
+      const uint32_t b = k + 1 < D ? x[k + 1].v[j] : 0u;
+      const uint32_t e = k + 2 < D ? x[k + 2].v[j] : 0u;
+      c[bl][0] = 0u;
+      c[bl][1] = a;
+      c[bl][2] = b;
+      c[bl][3] = a ^ b;
+      c[bl][4] = e;
+      c[bl][5] = a ^ e;
+      c[bl][6] = b ^ e;
+      c[bl][7] = xor3(a, b, e);
+    }
+    fr_outputs<D, P, NB>(y, j, c, std::make_integer_sequence<int, P>{});
+  }
+}
+
+// Ordering token: `t` (and anything derived from it) is taken to depend on the
+// 8 outputs of the previous dword, so the next dword's combinations cannot be
+// hoisted above them (the scheduler otherwise builds all four dwords' tables
+// at once: ~300 registers).
+__device__ __forceinline__ void fr_after(uint32_t& t, const V4* y, int j) {
+  asm volatile("" : "+v"(t) : "v"(y[0].v[j]), "v"(y[1].v[j]), "v"(y[2].v[j]), "v"(y[3].v[j]), "v"(y[4].v[j]),
+                              "v"(y[5].v[j]), "v"(y[6].v[j]), "v"(y[7].v[j]));
+}
+
+// cparity_fr for P = 8 with the dwords forced in sequence: rows [0, GR) are read
+// from the wave's LDS stage one dword at a time (addresses behind the token),
+// rows [GR, D) come from registers (each register row's dword passes through
+// the token too).
+template <int D, int P, int GR>
+__device__ __forceinline__ void cparity_fr_seq(V4* y, V4* x, const uint32_t* stage_lane_dw) {
+  static_assert(P == 8, "fr_after takes 8 outputs");
+  constexpr int NB = (D + kFrBlock - 1) / kFrBlock;
+  uint32_t tok = 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j > 0) fr_after(tok, y, j - 1);
+    uint32_t xin[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      if (k < GR) {
+        xin[k] = stage_lane_dw[(k * 64) * 4 + j + tok];  // ds_read_b32, lane's dword j of row k
+      } else {
+        xin[k] = x[k].v[j];
+        if (j > 0) asm volatile("" : "+v"(xin[k]) : "v"(tok));
+      }
+    }
+    uint32_t c[NB][8];
+#pragma unroll
+    for (int bl = 0; bl < NB; ++bl) {
+      const int k = kFrBlock * bl;
+      const uint32_t a = xin[k];
+      const uint32_t b = k + 1 < D ? xin[k + 1] : 0u;
+      const uint32_t e = k + 2 < D ? xin[k + 2] : 0u;
+      c[bl][0] = 0u;
+      c[bl][1] = a;
+      c[bl][2] = b;
+      c[bl][3] = a ^ b;
+      c[bl][4] = e;
+      c[bl][5] = a ^ e;
+      c[bl][6] = b ^ e;
+      c[bl][7] = xor3(a, b, e);
+    }
+    fr_outputs<D, P, NB>(y, j, c, std::make_integer_sequence<int, P>{});
+  }
+}
+
 // y = sum_k c_k * x_k over GF(2^8) with per-lane coefficients: Horner over the
 // coefficient bits; bit b of c_k becomes a lane mask (v_bfe_i32) that enters
 // the 4 dwords of the chunk through v_bitop3 y ^ (x & m).  The mask and its
