@@ -53,3 +53,15 @@ def test_null_arguments_rejected():
     # reconstruct_into: no context, then an empty batch (a no-op whatever the pointers)
     assert lib.ugo_fec_reconstruct_into(None, None, None, 1, 16, 16, 208, None, 16, 48, 0, None, None) == 6
     assert lib.ugo_fec_reconstruct_into(None, None, None, 0, 16, 16, 208, None, 16, 48, 0, None, None) == 6
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: a missing libugofec.so is an ImportError, not a silent
+    switch to another path."""
+    saved = fec._lib
+    fec._lib = None
+    try:
+        with pytest.raises(ImportError, match="not built"):
+            fec.load_library(str(tmp_path / "libugofec.so"))
+    finally:
+        fec._lib = saved
