@@ -827,3 +827,28 @@ def test_random_wide_codes_vs_restatement(gpu, d, p, S, pad, seed):
         for r in range(n):
             exp = bytes(rows[r]) if err is None else inp[g, r, :S].tobytes()
             assert got[g, r, :S].tobytes() == exp, (g, r)
+
+
+@pytest.mark.parametrize("S", [9000, 8999, 8193, 1, 15, 17, 1350, 4096])
+@pytest.mark.parametrize("shard_major", [False, True])
+def test_jumbo_encode_four_russians_vs_oracle(gpu, S, shard_major):
+    """The (32,8) encode runs the compile-time network in Four-Russians form
+    (k_encode_frs): parity bit-exact vs the C oracle for full and partial tail
+    chunks, group-major and planar, and padding past S untouched."""
+    d, p, G = 32, 8, 70
+    n = d + p
+    pitch = (S + 15) // 16 * 16
+    host = _rand(G, n, pitch, 9000 + S).numpy()
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    want[:, d:, S:] = host[:, d:, S:]  # the kernel leaves padding as it was
+    enc = fec.New(d, p)
+    if shard_major:
+        t = _dev(np.ascontiguousarray(host.transpose(1, 0, 2)))
+        enc.encode_batch(t, shard_size=S, shard_major=True)
+        got = t.cpu().numpy().transpose(1, 0, 2)
+    else:
+        t = _dev(host)
+        enc.encode_batch(t, shard_size=S)
+        got = t.cpu().numpy()
+    assert np.array_equal(got, want)
