@@ -134,8 +134,10 @@ __global__ __launch_bounds__(BS) void k_encode_g(Batch a) {
   cparity_store<D, P, NTS>(l.gp, a.rstride, l.nb, x, std::make_integer_sequence<int, P>{});
 }
 
-// k_encode_g with the network in Four-Russians form (cparity_fr): fewer VALU
-// for wide codes, whose encode is VALU-bound.
+// k_encode_g with the network in Four-Russians form (cparity_fr).  A/B only
+// (tools/jvariants.hip): left to itself the scheduler builds all four dwords'
+// tables at once (256 VGPRs + 46 AGPRs, 723-743 us); production runs
+// k_encode_frs below.
 template <int D, int P, int NTS = 0, int GR = D, int BS = 256, int LR = GR, int WPE = 1>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode_fr(Batch a) {
   static_assert(LR >= GR, "the stage holds at least the staged rows");
