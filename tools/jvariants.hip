@@ -344,6 +344,35 @@ int main(int argc, char** argv) {
       vars.push_back({"dec k_prepare + k_apply_qa ring2 (production)", dec_bytes, [=]() {
         launch_prepare(pr, G, 0);
         hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+      // two halves: the second half's descriptor build runs on a side stream
+      // while the first half is applied
+      hipStream_t s2;
+      hipEvent_t ev0, evB;
+      CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+      CK(hipEventCreateWithFlags(&ev0, hipEventDisableTiming));
+      CK(hipEventCreateWithFlags(&evB, hipEventDisableTiming));
+      const uint64_t H = G / 2;
+      Prep pA = pr, pB = pr;
+      pB.g0 = H;
+      Batch aA = ar, aB = ar;
+      aA.items = H * ((a.chunks + 63) / 64 * 64);
+      aB.g0 = H;
+      aB.items = (G - H) * ((a.chunks + 63) / 64 * 64);
+      const uint32_t gA = (aA.items + 255) / 256, gB = (aB.items + 255) / 256;
+      vars.push_back({"dec OVERLAP: prepare(half 2) on a side stream during apply(half 1)", dec_bytes, [=]() {
+        (void)hipEventRecord(ev0, 0);
+        (void)hipStreamWaitEvent(s2, ev0, 0);
+        (void)launch_prepare(pB, static_cast<uint32_t>(G - H), s2);
+        (void)hipEventRecord(evB, s2);
+        (void)launch_prepare(pA, static_cast<uint32_t>(H), 0);
+        hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(gA), dim3(256), 0, 0, aA);
+        (void)hipStreamWaitEvent(0, evB, 0);
+        hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(gB), dim3(256), 0, 0, aB); }, {}});
+      vars.push_back({"dec two halves, one stream (prepare A, apply A, prepare B, apply B)", dec_bytes, [=]() {
+        (void)launch_prepare(pA, static_cast<uint32_t>(H), 0);
+        hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(gA), dim3(256), 0, 0, aA);
+        (void)launch_prepare(pB, static_cast<uint32_t>(G - H), 0);
+        hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(gB), dim3(256), 0, 0, aB); }, {}});
     }
   }
   // encode variants must agree: run const then perm encode over the same data
