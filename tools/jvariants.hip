@@ -258,6 +258,8 @@ int main(int argc, char** argv) {
   add(k_encode_frs<32, 8, 2, 8, 256, 8, 3>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, lds-dma 8 rows, nt stores, 3 waves/SIMD");
   add(k_encode_frs<32, 8, 2, 16, 256, 16, 3>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, lds-dma 16 rows, nt stores, 3 waves/SIMD");
   add(k_encode_frs<32, 8, 2, 12, 256, 12, 3>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, lds-dma 12 rows, nt stores, 3 waves/SIMD");
+  add(k_encode_frs<32, 8, 2, 16, 256, 16, 3, 4>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, BLOCKS OF 4, lds-dma 16 rows, nt stores");
+  add(k_encode_frs<32, 8, 2, 16, 256, 16, 3, 2>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, BLOCKS OF 2, lds-dma 16 rows, nt stores");
   add(k_encode_frs<32, 8, 2, 20, 256, 20, 3>, a, enc_bytes, "enc FOUR-RUSSIANS SEQ dwords, lds-dma 20 rows, nt stores, 3 waves/SIMD");
   {
     const uint32_t g128 = (a.items + 127) / 128, g64 = (a.items + 63) / 64;
@@ -390,7 +392,7 @@ int main(int argc, char** argv) {
     vars[2].go();
     CK(hipMemcpy(h2.data(), buf, h.size(), hipMemcpyDeviceToHost));
     printf("{\"check\":\"perm encode == const encode\",\"equal\":%s}\n", same_rows(h1, h2) ? "true" : "false");
-    for (size_t f = kFr; f < kFr + 12; ++f) {
+    for (size_t f = kFr; f < kFr + 14; ++f) {
       CK(hipMemset(buf + size_t(d) * a.rstride, 0, size_t(p) * a.rstride));
       vars[f].go();
       CK(hipMemcpy(h2.data(), buf, h.size(), hipMemcpyDeviceToHost));

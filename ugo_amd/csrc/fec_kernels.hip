@@ -27,9 +27,9 @@
 //    (gf::Code<D,P>), so the XOR network is fixed at compile time -- the (10,3)
 //    headline (k_encode_g in production) and the (32,8) jumbo geometry
 //    (k_encode_frs in production: the bit-plane sums Tb in Four-Russians form,
-//    one precomputed XOR combination per block of 3 inputs instead of one
-//    term per input, dword by dword: ~20% fewer VALU for the VALU-bound wide
-//    code, gf_device.hpp cparity_fr_seq).
+//    one precomputed XOR combination per block of inputs instead of one term
+//    per input, dword by dword, for the VALU-bound wide code; gf_device.hpp
+//    cparity_fr_seq).
 //  * k_apply_p<DMAX,MODE>: runtime coefficients through split v_perm_b32
 //    tables (the headline reconstruct), k_apply_q its streaming form for wide
 //    codes, k_apply_qa the wave-aligned streaming form (the jumbo reconstruct:
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 
 // k_encode_fr with the dwords forced in sequence (cparity_fr_seq): staged rows
 // read from LDS per dword, so the live set is one dword's tables.
-template <int D, int P, int NTS = 0, int GR = D, int BS = 256, int LR = GR, int WPE = 1>
+template <int D, int P, int NTS = 0, int GR = D, int BS = 256, int LR = GR, int WPE = 1, int BK = kFrBlock>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode_frs(Batch a) {
   static_assert(LR >= GR, "the stage holds at least the staged rows");
   __shared__ u32x4 stage[BS / 64][LR][64];
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   for (int k = GR; k < D; ++k) x[k] = load16<1>(l.gp + static_cast<uint64_t>(k) * a.rstride);
   lds_dma_wait();
   V4 y[P];
-  cparity_fr_seq<D, P, GR>(y, x, reinterpret_cast<const uint32_t*>(&stage[w][0][lane]));
+  cparity_fr_seq<D, P, GR, BK>(y, x, reinterpret_cast<const uint32_t*>(&stage[w][0][lane]));
 #pragma unroll
   for (int i = 0; i < P; ++i) store16<NTS>(l.gp + static_cast<uint64_t>(D + i) * a.rstride, y[i], l.nb);
 }
@@ -1068,6 +1068,10 @@ constexpr int kEncJumboNT = 3;  // (32,8): NT loads and stores (578 vs 615 us, t
 // Horner network's own pick was 8 staged rows (565 vs 584 us for 16 in 9 of
 // 12 interleaved runs, profiles/r2/jvariants_lds_rows_r2.txt).
 constexpr int kEncJumboLdsRows = 16;
+// Four-Russians blocks of 2 inputs (a, b, a^b): more XORs than blocks of 3
+// but 108 instead of 133 VGPRs, 519.4 / 517.9 us against 527.8 / 524.7 (blocks
+// of 4: 532.3) in two interleaved runs (profiles/r2/jvariants_fr_blocks*.jsonl)
+constexpr int kEncJumboFrBlock = 2;
 constexpr int kApplyNT = 3;  // nontemporal loads and stores
 constexpr int kApplyPNT = 3; // k_apply_p: nontemporal loads and stores (cold: 201.0 vs 228.4 us)
 constexpr int kApplyQNT = 3; // k_apply_q (jumbo): NT loads and stores (548 vs 572 us)
@@ -1090,8 +1094,8 @@ hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   if (d == 10 && p == 3)
     launch(kKEncode, k_encode_g<10, 3, kEncNT & 2, kEncLdsRows, 256, kEncStageRows>, grid, block, 0, s, a);
   else if (d == 32 && p == 8)
-    launch(kKEncode, k_encode_frs<32, 8, kEncJumboNT & 2, kEncJumboLdsRows, 256, kEncJumboLdsRows, 3>, grid, block,
-           0, s, a);
+    launch(kKEncode, k_encode_frs<32, 8, kEncJumboNT & 2, kEncJumboLdsRows, 256, kEncJumboLdsRows, 3, kEncJumboFrBlock>,
+           grid, block, 0, s, a);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

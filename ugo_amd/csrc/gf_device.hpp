@@ -279,9 +279,9 @@ __device__ __forceinline__ void cparity_store(uint8_t* gp, uint64_t pitch, uint3
 // planes per dword, against 44 extra XORs per dword for the combinations.
 constexpr int kFrBlock = 3;
 
-template <int D, int P, int I, int B>
+template <int D, int P, int I, int B, int BK = kFrBlock>
 struct FrTerms {
-  static constexpr int NB = (D + kFrBlock - 1) / kFrBlock;
+  static constexpr int NB = (D + BK - 1) / BK;
   struct List {
     int n;
     int blk[NB];
@@ -291,8 +291,8 @@ struct FrTerms {
     List l{};
     for (int bl = 0; bl < NB; ++bl) {
       int v = 0;
-      for (int t = 0; t < kFrBlock; ++t) {
-        const int k = kFrBlock * bl + t;
+      for (int t = 0; t < BK; ++t) {
+        const int k = BK * bl + t;
         if (k < D && ((gf::Code<D, P>::M.at(D + I, k) >> B) & 1)) v |= 1 << t;
       }
       if (v) {
@@ -306,33 +306,34 @@ struct FrTerms {
   static constexpr List L = make();
 };
 
-template <int D, int P, int I, int B, int J, int NB>
-__device__ __forceinline__ void fr_fold(uint32_t& y, const uint32_t (*c)[8]) {
-  constexpr auto L = FrTerms<D, P, I, B>::L;
+template <int D, int P, int I, int B, int J, int NB, int BK = kFrBlock>
+__device__ __forceinline__ void fr_fold(uint32_t& y, const uint32_t (*c)[1 << BK]) {
+  constexpr auto L = FrTerms<D, P, I, B, BK>::L;
   if constexpr (J + 1 < L.n) {
     y = xor3(y, c[L.blk[J]][L.idx[J]], c[L.blk[J + 1]][L.idx[J + 1]]);
-    fr_fold<D, P, I, B, J + 2, NB>(y, c);
+    fr_fold<D, P, I, B, J + 2, NB, BK>(y, c);
   } else if constexpr (J < L.n) {
     y ^= c[L.blk[J]][L.idx[J]];
   }
 }
 
-template <int D, int P, int I, int B, int NB>
-__device__ __forceinline__ void fr_horner(uint32_t& y, const uint32_t (*c)[8]) {
-  constexpr auto L = FrTerms<D, P, I, B>::L;
+template <int D, int P, int I, int B, int NB, int BK = kFrBlock>
+__device__ __forceinline__ void fr_horner(uint32_t& y, const uint32_t (*c)[1 << BK]) {
+  constexpr auto L = FrTerms<D, P, I, B, BK>::L;
   if constexpr (any_bit_at_or_above<D, P, I, B + 1>()) {
     y = xt1(y);
-    fr_fold<D, P, I, B, 0, NB>(y, c);
+    fr_fold<D, P, I, B, 0, NB, BK>(y, c);
   } else if constexpr (L.n > 0) {
     y = c[L.blk[0]][L.idx[0]];
-    fr_fold<D, P, I, B, 1, NB>(y, c);
+    fr_fold<D, P, I, B, 1, NB, BK>(y, c);
   }
-  if constexpr (B > 0) fr_horner<D, P, I, B - 1, NB>(y, c);
+  if constexpr (B > 0) fr_horner<D, P, I, B - 1, NB, BK>(y, c);
 }
 
-template <int D, int P, int NB, int... I>
-__device__ __forceinline__ void fr_outputs(V4* y, int j, const uint32_t (*c)[8], std::integer_sequence<int, I...>) {
-  ((y[I].v[j] = 0u, fr_horner<D, P, I, 7, NB>(y[I].v[j], c)), ...);
+template <int D, int P, int NB, int BK, int... I>
+__device__ __forceinline__ void fr_outputs(V4* y, int j, const uint32_t (*c)[1 << BK],
+                                           std::integer_sequence<int, I...>) {
+  ((y[I].v[j] = 0u, fr_horner<D, P, I, 7, NB, BK>(y[I].v[j], c)), ...);
 }
 
 // All P parity chunks of one column chunk, dword by dword (so only one dword's
@@ -358,7 +359,7 @@ __device__ __forceinline__ void cparity_fr(V4* y, const V4* x) {
       c[bl][6] = b ^ e;
       c[bl][7] = xor3(a, b, e);
     }
-    fr_outputs<D, P, NB>(y, j, c, std::make_integer_sequence<int, P>{});
+    fr_outputs<D, P, NB, kFrBlock>(y, j, c, std::make_integer_sequence<int, P>{});
   }
 }
 
@@ -375,10 +376,10 @@ __device__ __forceinline__ void fr_after(uint32_t& t, const V4* y, int j) {
 // from the wave's LDS stage one dword at a time (addresses behind the token),
 // rows [GR, D) come from registers (each register row's dword passes through
 // the token too).
-template <int D, int P, int GR>
+template <int D, int P, int GR, int BK = kFrBlock>
 __device__ __forceinline__ void cparity_fr_seq(V4* y, V4* x, const uint32_t* stage_lane_dw) {
   static_assert(P == 8, "fr_after takes 8 outputs");
-  constexpr int NB = (D + kFrBlock - 1) / kFrBlock;
+  constexpr int NB = (D + BK - 1) / BK;
   uint32_t tok = 0u;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -393,23 +394,20 @@ __device__ __forceinline__ void cparity_fr_seq(V4* y, V4* x, const uint32_t* sta
         if (j > 0) asm volatile("" : "+v"(xin[k]) : "v"(tok));
       }
     }
-    uint32_t c[NB][8];
+    // c[bl][m] = XOR of the block's inputs t with bit t of m set: each entry
+    // is an earlier entry (lowest bit of m cleared) plus one input
+    uint32_t c[NB][1 << BK];
 #pragma unroll
     for (int bl = 0; bl < NB; ++bl) {
-      const int k = kFrBlock * bl;
-      const uint32_t a = xin[k];
-      const uint32_t b = k + 1 < D ? xin[k + 1] : 0u;
-      const uint32_t e = k + 2 < D ? xin[k + 2] : 0u;
       c[bl][0] = 0u;
-      c[bl][1] = a;
-      c[bl][2] = b;
-      c[bl][3] = a ^ b;
-      c[bl][4] = e;
-      c[bl][5] = a ^ e;
-      c[bl][6] = b ^ e;
-      c[bl][7] = xor3(a, b, e);
+#pragma unroll
+      for (int m = 1; m < (1 << BK); ++m) {
+        const int t = __builtin_ctz(m), k = BK * bl + t;
+        const uint32_t xt = k < D ? xin[k] : 0u;
+        c[bl][m] = (m & (m - 1)) ? (c[bl][m & (m - 1)] ^ xt) : xt;
+      }
     }
-    fr_outputs<D, P, NB>(y, j, c, std::make_integer_sequence<int, P>{});
+    fr_outputs<D, P, NB, BK>(y, j, c, std::make_integer_sequence<int, P>{});
   }
 }
 
