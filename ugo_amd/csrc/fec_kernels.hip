@@ -1062,7 +1062,7 @@ constexpr int kEncStageRows = 13;  // (10,3): 52-KiB stage, 3 blocks per CU (see
 constexpr int kEncJumboNT = 3;  // (32,8): NT loads and stores (578 vs 615 us, tools/jvariants.hip)
 // (32,8): the network in Four-Russians form with the dwords in sequence
 // (k_encode_frs), rows 0-15 by LDS-DMA nt and read from LDS one dword at a
-// time, 133 VGPRs, 2 blocks per CU (64-KiB stage): 519.9 / 524.6 us against
+// time (blocks of 3: 133 VGPRs), 2 blocks per CU (64-KiB stage): 519.9 / 524.6 us against
 // 548.9 / 567.2 us for the Horner network k_encode_g with 8 staged rows on two
 // boxes, byte-identical parity (profiles/r2/jvariants_frs*.jsonl).  The
 // Horner network's own pick was 8 staged rows (565 vs 584 us for 16 in 9 of
