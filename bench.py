@@ -87,11 +87,18 @@ def parse(argv=None):
                     help="process group for the timing barrier and reductions (no data-path collective)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=8.0,
                     help="per leg of the CPU baseline (all cores, 1 core); the 2-erasure leg gets half")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="CPU baseline threads (the GPU box's CPU share is 16; capped at the affinity set)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads; 0 = every usable CPU: min(affinity set, cgroup cpu.max quota)")
     ap.add_argument("--cpu-simd", type=int, default=-1,
                     help="CPU baseline SIMD level: -1 best available, 0 scalar, 1 AVX2, 2 AVX-512 GFNI")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c4-total-groups", type=int, default=4194304,
+                    help="strong leg after the main line: BASELINE configs[3] -- this many groups split over the "
+                         "ranks (contiguous ranges), one cold batch per rank; 0 = off")
+    ap.add_argument("--c4-steps", type=int, default=10, help="timed steps of the strong leg")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the PCIe-inclusive host_path leg (N = 1): pinned-host encode / reconstruct of "
+                         "(10+3)x1350 x 65,536 and (32+8)x9000 x 8,192 groups")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
@@ -272,9 +279,61 @@ def clock_warmup(step, sync, min_ms: float, chunk: int = 5, tol: float = 0.02, m
 
 
 # ------------------------------------------------------------- CPU baseline
+def cgroup_cpu_quota():
+    """CPUs the cgroup CPU controller grants this process: the smallest
+    cpu.max quota/period (cgroup v2) or cfs_quota_us/cfs_period_us (v1) along
+    the process's cgroup path up to the root, as a float; None if no quota is
+    set (or the files are not readable).  Returns (cpus, source)."""
+    best, src = None, None
+
+    def consider(q, per, path):
+        nonlocal best, src
+        if q > 0 and per > 0 and (best is None or q / per < best):
+            best, src = q / per, path
+
+    try:
+        with open("/proc/self/cgroup") as f:
+            lines = f.read().splitlines()
+    except OSError:
+        lines = []
+    for line in lines:
+        parts = line.split(":", 2)
+        if len(parts) != 3:
+            continue
+        _, ctrls, rel = parts
+        if ctrls == "":  # v2 unified hierarchy
+            roots = ["/sys/fs/cgroup"]
+            fname = "cpu.max"
+        elif "cpu" in ctrls.split(","):
+            roots = ["/sys/fs/cgroup/cpu,cpuacct", "/sys/fs/cgroup/cpu"]
+            fname = None
+        else:
+            continue
+        for root in roots:
+            rel_parts = [p for p in rel.split("/") if p]
+            for k in range(len(rel_parts), -1, -1):
+                d = os.path.join(root, *rel_parts[:k])
+                try:
+                    if fname:
+                        with open(os.path.join(d, fname)) as f:
+                            q, per = f.read().split()[:2]
+                        if q != "max":
+                            consider(float(q), float(per), os.path.join(d, fname))
+                    else:
+                        with open(os.path.join(d, "cpu.cfs_quota_us")) as f:
+                            q = float(f.read().strip())
+                        with open(os.path.join(d, "cpu.cfs_period_us")) as f:
+                            per = float(f.read().strip())
+                        consider(q, per, os.path.join(d, "cpu.cfs_quota_us"))
+                except (OSError, ValueError):
+                    continue
+    return best, src
+
+
 def host_info():
-    """CPU model, machine CPU count, this process's CPU share and whether a Go
-    toolchain exists (the reference is Go; BASELINE.md's CPU plan)."""
+    """CPU model, machine CPU count, this process's CPU share (affinity set and
+    cgroup quota) and whether a Go toolchain exists (the reference is Go;
+    BASELINE.md's CPU plan)."""
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -289,8 +348,11 @@ def host_info():
     except AttributeError:  # pragma: no cover
         share = os.cpu_count() or 1
     go = shutil.which("go")
+    quota, quota_src = cgroup_cpu_quota()
+    usable = share if quota is None else max(1, min(share, int(quota)))
     return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": share,
-            "go_toolchain": "present" if go else "absent"}
+            "cgroup_cpu_quota": None if quota is None else round(quota, 2), "cgroup_quota_file": quota_src,
+            "usable_cpus": usable, "go_toolchain": "present" if go else "absent"}
 
 
 def cpu_baseline(args, d, p, S, n):
@@ -312,16 +374,20 @@ def cpu_baseline(args, d, p, S, n):
     rs_ref.load_c_oracle()
     info = host_info()
     level = rs_ref.set_simd(args.cpu_simd)
-    threads = max(1, min(args.cpu_threads, info["affinity_cpus"]))
+    threads = info["usable_cpus"] if args.cpu_threads <= 0 else max(1, min(args.cpu_threads, info["usable_cpus"]))
     rng = np.random.default_rng(args.seed)
 
-    def sample(G, erasures):
-        sh = rng.integers(0, 256, size=(G, n, S), dtype=np.uint8)
+    base = rng.integers(0, 256, size=(1024, n, S), dtype=np.uint8)
+
+    def sample(erasures):
+        """One instance's own batch: a copy of one random base batch (instances
+        never share memory) and its own uniformly random erasure pattern."""
+        G = base.shape[0]
+        erased = rng.random((G, n)).argsort(axis=1)[:, :erasures]
         masks = np.full(G, (1 << n) - 1, np.uint64)
-        for g in range(G):
-            for r in rng.choice(n, erasures, replace=False):
-                masks[g] &= ~np.uint64(1 << int(r))
-        return sh, masks
+        for j in range(erasures):
+            masks &= ~(np.uint64(1) << erased[:, j].astype(np.uint64))
+        return base.copy(), masks
 
     def leg(samples, erasures, seconds):
         """One worker thread per (batch, masks) sample, each a single-threaded
@@ -356,7 +422,7 @@ def cpu_baseline(args, d, p, S, n):
         return round(per_pass * sum(passes) / el / 2**30, 4), sum(passes), el
 
     try:
-        c0 = [sample(1024, 1) for _ in range(threads)]
+        c0 = [sample(1) for _ in range(threads)]
         v_all, n_all, t_all = leg(c0, 1, args.cpu_baseline_seconds)
         v_one, n_one, t_one = leg(c0[:1], 1, args.cpu_baseline_seconds)
         # per call on 1 core (the drop-in per-group path's CPU figure):
@@ -372,7 +438,8 @@ def cpu_baseline(args, d, p, S, n):
             per["encode"].append((t1 - t0) / sh.shape[0] * 1e6)
             per["reconstruct_1loss"].append((t2 - t1) / sh.shape[0] * 1e6)
         per_us = {k: round(sorted(v)[len(v) // 2], 3) for k, v in per.items()}
-        c2 = [sample(4096, args.erasures) for _ in range(threads)]
+        del c0
+        c2 = [sample(args.erasures) for _ in range(threads)]
         v_two, n_two, t_two = leg(c2, args.erasures, args.cpu_baseline_seconds / 2)
     finally:
         rs_ref.set_simd(0)
@@ -386,10 +453,10 @@ def cpu_baseline(args, d, p, S, n):
                      f"reference cannot run: go toolchain {info['go_toolchain']})",
            "single_core": {"value": v_one, "unit": "GiB/s", "cores": 1, "passes": n_one,
                            "seconds": round(t_one, 2), "per_group_us": per_us},
-           "two_erasure_4096": {"value": v_two, "unit": "GiB/s", "cores": threads, "passes": n_two,
-                                "seconds": round(t_two, 2),
-                                "sample": f"{threads} instances x 4096 groups, encode + {args.erasures}-erasure "
-                                          f"reconstruct (the bench's own workload)"},
+           "two_erasure": {"value": v_two, "unit": "GiB/s", "cores": threads, "passes": n_two,
+                           "seconds": round(t_two, 2),
+                           "sample": f"{threads} instances x 1024 groups, encode + {args.erasures}-erasure "
+                                     f"reconstruct (the bench's own workload)"},
            "simd": simd}
     out.update(info)
     return out
@@ -407,6 +474,175 @@ def make_masks(G, n, e, seed, device):
     for j in range(e):
         masks ^= (1 << erased[:, j]).to(torch.int64)
     return masks.to(device), erased
+
+
+def kernel_pass(enc, step, steps, sync):
+    """Kernel-timing pass (`roofline`, `kernels`): `steps` steps with the
+    library's launch timing on -- each launch issued with hipExtLaunchKernel
+    start/stop events (ugo_fec_timing_begin), which carry the dispatch's own
+    timestamps on the launch stream.  The events cost ~5 us per kernel
+    boundary (tools/gap_probe.py: 374.8 vs 364.6 us per step), so no `value`
+    is taken from this pass.  Returns (encode ms, reconstruct ms per step,
+    this pass's wall seconds)."""
+    import numpy as np
+
+    enc.timing_begin(4 * steps + 16)
+    sync()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    wall = time.perf_counter() - t1
+    recs, _untimed = enc.timing_end()
+    kid = recs["kernel"]
+    n_enc = int((kid == 1).sum())
+    n_dec = int(np.isin(kid, (2, 3)).sum())
+    assert n_enc >= steps and n_dec >= steps, (n_enc, n_dec)
+    enc_ms = float(recs["ms"][kid == 1].sum()) / steps
+    dec_ms = float(recs["ms"][np.isin(kid, (2, 3))].sum()) / steps  # apply (+ k_prepare for d+p > 16)
+    return enc_ms, dec_ms, wall
+
+
+def kernel_stats(enc_ms, dec_ms, enc_bytes, dec_bytes, payload):
+    def one(ms, b):
+        return {"avg_ms": round(ms, 5), "bytes_per_launch": b, "GBps": round(b / (ms * 1e-3) / 1e9, 1),
+                "payload_GBps": round(payload / (ms * 1e-3) / 1e9, 1),
+                "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    return {"encode": one(enc_ms, enc_bytes), "reconstruct": one(dec_ms, dec_bytes)}
+
+
+def strong_leg(args, enc, rank, world, dev, stream):
+    """BASELINE configs[3]: --c4-total-groups (4,194,304) groups of the bench's
+    code split over the ranks in contiguous ranges (strong scaling: the total
+    is fixed as N grows), one batch per rank in the planar layout -- at these
+    sizes (9-74 GB per GPU) every step is cold without rotating batches.  Same
+    step as the main line (encode + reconstruct_into), a timed region with
+    barrier + synchronize and max over ranks, a kernel-timing pass, and a
+    full-size round trip (every output equals the erased row it rebuilds; the
+    erased rows stay in the batch, reconstruct_into never reads them --
+    tests/test_large_batches.py zeroes them first at this size)."""
+    import torch
+
+    from ugo_amd.shard import partition
+
+    d, p, S = args.data_shards, args.parity_shards, args.shard_size
+    n, e = d + p, args.erasures
+    pitch = args.pitch or (S + 15) // 16 * 16
+    total = args.c4_total_groups
+    g0, g1 = partition(total, world, rank)
+    G = g1 - g0
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 0xC4 + g0)
+    sh = torch.randint(0, 256, (n, G, pitch), dtype=torch.uint8, device=dev, generator=gen)
+    masks, erased = make_masks(G, n, e, args.seed + 0xC4 + 1000 + rank, dev)
+    out = torch.zeros((p, G, pitch), dtype=torch.uint8, device=dev)
+
+    def step():
+        enc.encode_batch(sh, shard_size=S, stream=stream, shard_major=True)
+        enc.reconstruct_into(sh, masks, out, shard_size=S, stream=stream, shard_major=True)
+
+    sync = torch.cuda.synchronize
+    for _ in range(2):
+        step()
+    sync()
+    elapsed = timed_region(step, args.c4_steps, sync, world)
+    enc_ms, dec_ms, _ = kernel_pass(enc, step, args.c4_steps, sync)
+    elapsed, enc_ms, dec_ms = reduce_max([elapsed, enc_ms, dec_ms], world)
+    view = sh.transpose(0, 1)
+    gi = torch.arange(G, device=dev)
+    es = erased.sort(dim=1).values.to(dev)
+    ok = all(bool(torch.equal(out[j, :, :S], view[gi, es[:, j], :S])) for j in range(e))
+    ok = all_ranks_ok(ok, world)
+    step_bytes = total * (n * S + (d + e) * S)
+    res = {"workload": f"BASELINE configs[3]: {total} groups ({d}+{p})x{S}B total, strong over {world} rank(s): "
+                       f"{G} groups on rank 0, one cold planar batch per rank, encode + {e}-erasure "
+                       f"reconstruct_into",
+           "total_groups": total, "groups_per_rank": G, "steps": args.c4_steps, "scaling": "strong",
+           "value": round(step_bytes * args.c4_steps / elapsed / 2**30, 3), "unit": "GiB/s",
+           "ms_per_step": round(elapsed / args.c4_steps * 1e3, 4),
+           "kernels_rank_max": kernel_stats(enc_ms, dec_ms, G * n * S, G * (d + e) * S, G * d * S),
+           "verify_round_trip_full_size": ok}
+    del sh, out, masks, view
+    torch.cuda.empty_cache()
+    return res
+
+
+def host_path_leg(args, dev_index):
+    """The PCIe-inclusive rate north_star asks for (the path starts and ends in
+    host memory: UDP socket buffers, /root/reference/ugo/conn.go:387-406).
+    Batches in pinned host memory (ugo_fec_host_alloc), group-major as a
+    packet ring lays them out:
+      * (10+3)x1350 x 65,536 groups: ugo_fec_encode_host, then 2 uniformly
+        random erasures per group and ugo_fec_reconstruct_host;
+      * (32+8)x9000 x 8,192 groups (BASELINE configs[4]): encode, then a
+        uniformly random 0..8 erasures per group (mixed patterns) and
+        reconstruct.
+    The encode stages through device buffers (H2D of the data rows -> kernel
+    -> D2H of the parity rows, pipelined over 3 streams); the reconstruct of a
+    pinned batch runs zero-copy on its device mapping.  Each
+    call: 1 untimed + 3 timed, median.  Verified: every rebuilt batch equals
+    the encoded batch it was erased from (compared on the device)."""
+    import numpy as np
+    import torch
+
+    from ugo_amd import fec
+
+    dev = torch.device("cuda", dev_index)
+    res = {}
+    for d, p, S, G, mixed in ((10, 3, 1350, 65536, False), (32, 8, 9000, 8192, True)):
+        n = d + p
+        pitch = (S + 15) // 16 * 16
+        enc = fec.New(d, p, device=dev_index)
+        raw = fec.host_alloc(G * n * pitch)
+        try:
+            buf = raw.reshape(G, n, pitch)
+            gen = torch.Generator(device=dev).manual_seed(args.seed + d)
+            torch.from_numpy(buf).copy_(torch.randint(0, 256, (G, n, pitch), dtype=torch.uint8, device=dev,
+                                                      generator=gen))
+            times = []
+            for k in range(4):
+                t0 = time.perf_counter()
+                enc.encode_host(buf, S)
+                times.append(time.perf_counter() - t0)
+            t_enc = sorted(times[1:])[1]
+            ref = torch.from_numpy(buf).to(dev)
+            rng = np.random.default_rng(args.seed + 7 * d)
+            ranks = rng.random((G, n)).argsort(axis=1).argsort(axis=1)  # rank of row r in a random order
+            ne = rng.integers(0, p + 1, G) if mixed else np.full(G, args.erasures)
+            erased = ranks < ne[:, None]  # ne[g] distinct rows, uniform
+            masks = np.zeros(G, np.uint64)
+            for r in range(n):
+                masks |= (~erased[:, r]).astype(np.uint64) << np.uint64(r)
+            gi, ri = np.nonzero(erased)
+            buf[gi, ri] = 0
+            times = []
+            for k in range(4):
+                t0 = time.perf_counter()
+                rc = enc.reconstruct_host(buf, masks, S)
+                times.append(time.perf_counter() - t0)
+                assert rc == 0, rc
+            t_rec = sorted(times[1:])[1]
+            ok = bool(torch.equal(torch.from_numpy(buf).to(dev)[:, :, :S], ref[:, :, :S]))
+            del ref
+            e_tot = int(ne.sum())
+            lossy = int((ne > 0).sum())
+            b_enc = G * n * S
+            b_rec = lossy * d * S + e_tot * S
+            key = f"{d}+{p}x{S}"
+            res[key] = {
+                "groups": G, "erasures": "U[0,%d] per group" % p if mixed else f"{args.erasures} per group",
+                "encode_ms": round(t_enc * 1e3, 3), "encode_GBps": round(b_enc / t_enc / 1e9, 2),
+                "encode_pcie_GBps": round(G * (d * pitch + p * S) / t_enc / 1e9, 2),
+                "reconstruct_ms": round(t_rec * 1e3, 3), "reconstruct_GBps": round(b_rec / t_rec / 1e9, 2),
+                "reconstruct_pcie_GBps": round(b_rec / t_rec / 1e9, 2),
+                "verify_round_trip": ok}
+        finally:
+            fec.host_free(raw)
+            enc.close()
+    res["note"] = ("pinned host batches, group-major; GBps = algorithmic bytes ((d+p)*S encode, (d+e)*S per lossy "
+                   "group reconstruct) / wall time of the synchronous call; pcie_GBps = bytes crossing PCIe (encode: "
+                   "d padded rows in + p rows out, staged; reconstruct: d survivor rows in + e rows out, zero-copy)")
+    return res
 
 
 def run_rank(args):
@@ -475,25 +711,9 @@ def run_rank(args):
     elapsed = timed_region(step, args.steps, sync, world)
 
     # 2. Kernel-timing pass (`roofline`, `kernels`): the same K steps again with
-    #    the library's launch timing on -- each launch issued with
-    #    hipExtLaunchKernel start/stop events (ugo_fec_timing_begin), which carry
-    #    the dispatch's own timestamps on the launch stream.  The events cost
-    #    ~5 us per kernel boundary (tools/gap_probe.py: 374.8 vs 364.6 us per
-    #    step), so the value pass above runs without them.
-    enc.timing_begin(4 * args.steps + 16)
-    sync()
-    t1 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync()
-    elapsed_timing_pass = time.perf_counter() - t1
-    recs, untimed = enc.timing_end()
-    kid = recs["kernel"]
-    n_enc = int((kid == 1).sum())
-    n_dec = int(np.isin(kid, (2, 3)).sum())
-    assert n_enc >= args.steps and n_dec >= args.steps, (n_enc, n_dec)
-    enc_ms = float(recs["ms"][kid == 1].sum()) / args.steps
-    dec_ms = float(recs["ms"][np.isin(kid, (2, 3))].sum()) / args.steps  # apply (+ k_prepare for d+p > 16)
+    #    per-launch start/stop events (kernel_pass); the value pass above runs
+    #    without them.
+    enc_ms, dec_ms, elapsed_timing_pass = kernel_pass(enc, step, args.steps, sync)
 
     elapsed, enc_ms_max, dec_ms_max = reduce_max([elapsed, enc_ms, dec_ms], world)
 
@@ -532,18 +752,17 @@ def run_rank(args):
         verify = {"round_trip_full_size": ok_rt, "encode_idempotent": ok_idem}
         verify["all_ranks_ok"] = all_ranks_ok(ok_rt and ok_idem, world)
 
+    # 3. Secondary legs, after the main line's measurement (nothing in them
+    #    feeds `value`): BASELINE configs[3] strong over the ranks, and at N = 1
+    #    the PCIe-inclusive host path (configs[4] among it).
+    batches = outs = shards = view = None
+    torch.cuda.empty_cache()
+    strong = strong_leg(args, enc, rank, world, dev, stream) if args.c4_total_groups > 0 else None
+    host = host_path_leg(args, dev_index) if (world == 1 and not args.no_host_path) else None
+
     if rank == 0:
         payload = G * d * S  # klauspost's convention: data bytes per call (BASELINE.md secondary column)
-        kern = {
-            "encode": {"avg_ms": round(enc_ms, 5), "bytes_per_launch": enc_bytes,
-                       "GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),
-                       "payload_GBps": round(payload / (enc_ms * 1e-3) / 1e9, 1),
-                       "frac": round(enc_bytes / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-            "reconstruct": {"avg_ms": round(dec_ms, 5), "bytes_per_launch": dec_bytes,
-                            "GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
-                            "payload_GBps": round(payload / (dec_ms * 1e-3) / 1e9, 1),
-                            "frac": round(dec_bytes / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-        }
+        kern = kernel_stats(enc_ms, dec_ms, enc_bytes, dec_bytes, payload)
         dom = "encode" if enc_ms >= dec_ms else "reconstruct"
         traffic = None
         try:
@@ -552,6 +771,9 @@ def run_rank(args):
             traffic = tj.get(key)
         except Exception:
             pass
+        traffic_note = ("traffic: HBM bytes per launch from the committed rocprofv3 PMC passes "
+                        f"({os.path.relpath(args.traffic_json, ROOT)}, (2*FETCH_SIZE + WRITE_SIZE)*1024 per "
+                        "MI355X_MICROARCH.md), not counters read in this run") if traffic else None
         ach = kern[dom]["GBps"]
         roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -559,7 +781,8 @@ def run_rank(args):
                         f" per group x {G} groups) / avg kernel duration over a kernel-timing pass of the same "
                         f"{args.steps} steps right after the timed region, from hipExtLaunchKernel start/stop "
                         f"events on the launch stream (ms_per_step of that pass: "
-                        f"{elapsed_timing_pass / args.steps * 1e3:.4f})"}
+                        f"{elapsed_timing_pass / args.steps * 1e3:.4f})"
+                        + (f"; {traffic_note}" if traffic_note else "")}
         if scaling == "strong":
             workload = f"{total_groups} groups total, strong: {G} groups on rank 0"
         else:
@@ -578,6 +801,7 @@ def run_rank(args):
                        "batches_per_gpu": nb, "decode": args.decode,
                        "parallelism": f"dp{world} (independent packet groups, no collective)"},
             "clock_warmup_ms": round(cw_ms, 1), "clock_warmup_steps": cw_steps, "clock_settled": cw_settled,
+            "untimed_steps_total": cw_steps + args.warmup,
             "pct_hbm_roofline": round(step_bytes_all / world * args.steps / elapsed / (HBM_PEAK_GBS * 1e9), 4),
             "roofline": roof, "kernels": kern, "verify": verify,
         }
@@ -585,6 +809,10 @@ def run_rank(args):
             out["config"]["ranks_per_device"] = ranks_per_device
             out["note"] = (f"{world} ranks on {ndev} device(s): a launcher rehearsal, not an {world}-GPU "
                            f"measurement")
+        if strong is not None:
+            out["strong_c4"] = strong
+        if host is not None:
+            out["host_path"] = host
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, d, p, S, n)
         print(json.dumps(out), flush=True)

@@ -122,5 +122,33 @@ def test_partition_covers_exactly_once():
 
 def test_host_info_fields():
     info = bench.host_info()
-    assert set(info) == {"cpu_model", "nproc", "affinity_cpus", "go_toolchain"}
+    assert set(info) == {"cpu_model", "nproc", "affinity_cpus", "cgroup_cpu_quota", "cgroup_quota_file",
+                         "usable_cpus", "go_toolchain"}
     assert info["go_toolchain"] in ("present", "absent") and info["affinity_cpus"] >= 1
+    # the CPU baseline runs on every usable CPU: the affinity set, capped by a cgroup quota if one is set
+    assert 1 <= info["usable_cpus"] <= info["affinity_cpus"]
+    if info["cgroup_cpu_quota"] is not None:
+        assert info["usable_cpus"] == max(1, min(info["affinity_cpus"], int(info["cgroup_cpu_quota"])))
+
+
+def test_cgroup_quota_parsing(tmp_path, monkeypatch):
+    """cpu.max (v2) along the process's cgroup path: the smallest quota wins."""
+    root = tmp_path / "cg"
+    (root / "a" / "b").mkdir(parents=True)
+    (root / "cpu.max").write_text("max 100000\n")
+    (root / "a" / "cpu.max").write_text("1600000 100000\n")
+    (root / "a" / "b" / "cpu.max").write_text("3200000 100000\n")
+    real_open = open
+
+    def fake_open(path, *a, **k):
+        path = str(path)
+        if path == "/proc/self/cgroup":
+            import io
+            return io.StringIO("0::/a/b\n")
+        if path.startswith("/sys/fs/cgroup"):
+            path = str(root) + path[len("/sys/fs/cgroup"):]
+        return real_open(path, *a, **k)
+
+    monkeypatch.setattr("builtins.open", fake_open)
+    q, src = bench.cgroup_cpu_quota()
+    assert q == 16.0 and src.endswith("a/cpu.max")

@@ -16,6 +16,7 @@
 #include <new>
 #include <string>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "fec_kernels.hpp"
@@ -34,6 +35,16 @@ constexpr size_t kZeroCopyEncodeBytes = size_t(4) << 20;  // pinned encode batch
 constexpr uint32_t kMaxItems = 0x7fffffffu;
 
 inline size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Groups per launch: a launch's work-item count is a uint32.  The vector
+// kernels may pad every group to a whole number of waves (k_apply_qa: rows
+// rounded up to 64 chunks), so a slice is sized from the padded count --
+// otherwise a short-row code (e.g. 1 chunk per row, padded to 64) would wrap
+// groups * 64 past 2^32 and leave most of the slice unwritten.
+inline size_t slice_groups(uint32_t chunks, bool fast) {
+  const size_t per_group = fast ? round_up(chunks, 64) : chunks;
+  return std::max<size_t>(1, kMaxItems / per_group);
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -63,6 +74,7 @@ struct ugo_fec {
   // freed on the call's own stream, so calls on different streams never share
   // a workspace
   hipMemPool_t pool = nullptr;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> scratch_ev;  // per stream: behind its last scratch free
   // host-path staging
   hipStream_t streams[kStreams] = {};
   uint8_t* d_stage[kStreams] = {};
@@ -179,10 +191,12 @@ void free_ctx(ugo_fec* c) {
     (void)hipFree(c->d_status[i]);
     if (c->streams[i]) (void)hipStreamDestroy(c->streams[i]);
   }
-  if (c->pool) {
-    (void)hipDeviceSynchronize();  // async frees still queued on user streams
-    (void)hipMemPoolDestroy(c->pool);
+  // this context's async scratch frees still queued on the callers' streams
+  for (auto& se : c->scratch_ev) {
+    (void)hipEventSynchronize(se.second);
+    (void)hipEventDestroy(se.second);
   }
+  if (c->pool) (void)hipMemPoolDestroy(c->pool);
   delete c;
 }
 
@@ -258,7 +272,7 @@ int encode_dev(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, const Layou
   ugo::kern::Batch a = base_batch(c, shards, S, L);
   a.desc = c->d_encdesc;
   a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
-  const size_t per = std::max<size_t>(1, kMaxItems / a.chunks);
+  const size_t per = slice_groups(a.chunks, fast);
   for (size_t g0 = 0; g0 < groups; g0 += per) {
     const size_t gn = std::min(per, groups - g0);
     a.g0 = g0;
@@ -296,7 +310,22 @@ int scratch_alloc(ugo_fec* c, size_t bytes, hipStream_t s, void** out) {
   return hip_status(hipMallocFromPoolAsync(out, bytes ? bytes : 16, c->pool, s));
 }
 
-int scratch_free(void* ptr, hipStream_t s) { return ptr ? hip_status(hipFreeAsync(ptr, s)) : UGO_FEC_OK; }
+// Frees scratch on its stream and records, per stream, an event behind the
+// free: destroying the context waits for exactly those events (its own
+// scratch frees), not for every stream on the device -- other contexts'
+// in-flight batches do not stall a destroy.
+int scratch_free(ugo_fec* c, void* ptr, hipStream_t s) {
+  if (!ptr) return UGO_FEC_OK;
+  if (hipFreeAsync(ptr, s) != hipSuccess) return UGO_FEC_ERR_HIP;
+  hipEvent_t ev = nullptr;
+  for (auto& se : c->scratch_ev)
+    if (se.first == s) ev = se.second;
+  if (!ev) {
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return UGO_FEC_ERR_HIP;
+    c->scratch_ev.emplace_back(s, ev);
+  }
+  return hip_status(hipEventRecord(ev, s));
+}
 
 bool fast_out(const OutBatch& O) {
   return !O.base || (reinterpret_cast<uintptr_t>(O.base) % 16 == 0 && O.L.rstride % 16 == 0 && O.L.gstride % 16 == 0);
@@ -329,17 +358,18 @@ int reconstruct_wide(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_
   a.status = status;
   a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
   a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
-  const size_t per = std::min<size_t>(std::max<size_t>(1, kMaxItems / a.chunks), 65536);
+  const size_t per = std::min<size_t>(slice_groups(a.chunks, fast), 65536);
   const size_t stride = c->desc_stride;
   std::vector<uint8_t> hd(std::min(per, groups) * stride);
   uint8_t* work = nullptr;
   int st = scratch_alloc(c, hd.size() + 64, s, reinterpret_cast<void**>(&work));
   if (st) return st;
   struct Release {
+    ugo_fec* c;
     uint8_t* p;
     hipStream_t s;
-    ~Release() { (void)scratch_free(p, s); }
-  } release{work, s};
+    ~Release() { (void)scratch_free(c, p, s); }
+  } release{c, work, s};
   for (size_t g0 = 0; g0 < groups; g0 += per) {
     const size_t gn = std::min(per, groups - g0);
     for (size_t g = 0; g < gn; ++g) {
@@ -385,7 +415,7 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
   a.status = status;
   a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
   a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
-  size_t per = std::max<size_t>(1, kMaxItems / a.chunks);
+  size_t per = slice_groups(a.chunks, fast);
   uint8_t* work = nullptr;
   if (mode == 2) {
     // per-group descriptors, bounded workspace (<= 64 Ki groups per slice)
@@ -394,10 +424,11 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
     if (st) return st;
   }
   struct Release {  // the workspace goes back to the pool after this call's kernels
+    ugo_fec* c;
     uint8_t* p;
     hipStream_t s;
-    ~Release() { (void)scratch_free(p, s); }
-  } release{work, s};
+    ~Release() { (void)scratch_free(c, p, s); }
+  } release{c, work, s};
   for (size_t g0 = 0; g0 < groups; g0 += per) {
     const size_t gn = std::min(per, groups - g0);
     a.g0 = g0;
@@ -889,7 +920,7 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   f.fixup = 1;
   if (!st) st = hip_status(ugo::kern::launch_rx_claim(f, s));
   if (!st) st = hip_status(ugo::kern::launch_rx_scatter(f, s));
-  const int fr = scratch_free(scratch, s);
+  const int fr = scratch_free(c, scratch, s);
   return st ? st : fr;
 }
 
