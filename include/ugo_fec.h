@@ -47,7 +47,9 @@ extern "C" {
  *    stats grew a fifth counter (duplicates). */
 /* 3: reconstruct entry points accept d+p > 64 with ceil((d+p)/64) presence
  *    words per group (one word, as before, for d+p <= 64). */
-#define UGO_FEC_ABI_VERSION 3
+/* 4: ugo_fec_rx_assemble keeps the first copy of a seqid across calls into one
+ *    batch too (a (group, row) already present at call entry is not written). */
+#define UGO_FEC_ABI_VERSION 4
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
  * that ugo/fec.go logs and swallows (ugo/fec.go:60-63, 208-210, 239-241). */
@@ -184,14 +186,14 @@ int ugo_fec_check_shards(int n, const size_t* lens, int nil_ok, size_t* shard_si
  *    by what it puts in a ring and by [first_group, first_group + groups):
  *    packets of groups outside that window are counted out-of-window and
  *    dropped, as a packet older than rxlimit arrivals or fecExpire is;
- *  - duplicates are only resolved within one call: a seqid placed by an
- *    earlier call into the same batch is overwritten by this call's first
- *    copy, which stats then counts as a duplicate (give each window its own
- *    batch, or one call per batch).
+ *  - the same holds across calls into one batch: a packet whose (group, row)
+ *    bit is already set in `present` when the call starts -- placed by an
+ *    earlier call -- is a duplicate and writes nothing, so the earlier call's
+ *    copy stays, as the queued packet does in input;
  * Placement is optimistic: the extra claim and re-place passes run (inside
  * the call, gated on the device) only when the window holds a duplicate.
- * The engine takes (groups*(d+p)*4) bytes of stream-ordered scratch per call.
- * npackets < 2^32 - 1. */
+ * The engine takes (groups*(8 + (d+p)*4)) bytes of stream-ordered scratch per
+ * call (the presence snapshot and the claim words).  npackets < 2^32 - 1. */
 int ugo_fec_rx_assemble(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, const uint16_t* lens,
                         size_t npackets, const uint8_t* pad, uint64_t first_group, size_t groups,
                         uint8_t* shards, size_t shard_size, size_t row_stride, size_t group_stride,

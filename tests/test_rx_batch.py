@@ -248,6 +248,76 @@ def test_rx_assemble_first_copy_wins(gpu, encrypt, S, slot):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("encrypt,S,slot", [(True, 1470, 1488), (False, 3000, 3024)])
+def test_rx_assemble_first_copy_wins_across_calls(gpu, encrypt, S, slot):
+    """Several calls fill ONE batch (windows of one packet stream), with
+    same-seqid, different-payload copies in later windows than the first: the
+    batch keeps the first copy of the whole stream, as ugo's input keeps the
+    queued packet (ugo/fec.go:123-129), and each call counts the later copies
+    as duplicates.  The expected batch is the restated per-packet path run over
+    the concatenated windows; the stats of a call are that path's counts over
+    its own window, given what the earlier windows queued."""
+    d, p, n = 10, 3, 13
+    pitch = (S + 15) // 16 * 16
+    G = 256
+    rng = np.random.default_rng(91)
+    maxlen = min(S + 6, slot)
+
+    def pkt(seq, flag):
+        L = int(rng.integers(6, maxlen + 1))
+        b = bytearray(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        b[0:4] = seq.to_bytes(4, "little")
+        b[4:6] = flag.to_bytes(2, "little")
+        return bytes(b)
+
+    stream = []
+    for g in range(G):
+        for r in range(n):
+            if rng.random() < 0.15:
+                continue
+            seq = g * n + r
+            copies = 1 + int(rng.integers(0, 3)) if rng.random() < 0.4 else 1
+            stream += [pkt(seq, 0xF1 if r < d else 0xF2) for _ in range(copies)]
+    order = rng.permutation(len(stream))
+    stream = [stream[i] for i in order]
+    cuts = [0, len(stream) // 5, len(stream) // 2, len(stream) * 4 // 5, len(stream)]
+    windows = [stream[a:b] for a, b in zip(cuts, cuts[1:])]
+    # a window whose packets ALL repeat seqids of earlier windows, with new payloads
+    windows.append([pkt(int.from_bytes(w[:4], "little"), int.from_bytes(w[4:6], "little"))
+                    for w in windows[0][:200]])
+    want, masks, _ = _expected_placement(stream + windows[-1], G, n, S, pitch, 0)
+    want_stats = []
+    for k in range(len(windows)):
+        prior = [w for win in windows[:k] for w in win]
+        _, _, s_all = _expected_placement(prior + windows[k], G, n, S, pitch, 0)
+        _, _, s_prior = _expected_placement(prior, G, n, S, pitch, 0)
+        want_stats.append([a - b for a, b in zip(s_all, s_prior)])
+    assert want_stats[-1][4] == 200 and want_stats[-1][0] == 0
+    assert sum(s[4] for s in want_stats[1:4]) > 50  # cross-window copies in the middle windows too
+
+    ks = rc4_ref.keystream(KEY, slot)
+    pad = torch.frombuffer(bytearray(ks), dtype=torch.uint8).cuda() if encrypt else None
+    codec = fec.New(d, p)
+    sh = torch.full((n, G, pitch), 0xAB, dtype=torch.uint8, device="cuda")
+    present = torch.zeros(G, dtype=torch.int64, device="cuda")
+    for k, win in enumerate(windows):
+        enc = [rc4_ref.xor_stream(KEY, w) if encrypt else w for w in win]
+        slots, lens = _ring(enc, slot)
+        st = torch.zeros(5, dtype=torch.int32, device="cuda")
+        codec.rx_assemble(torch.from_numpy(slots).cuda(), torch.from_numpy(lens.view(np.int16)).cuda(), sh,
+                          present, shard_size=S, pad=pad, stats=st)
+        assert st.cpu().tolist() == want_stats[k], k
+    assert np.array_equal(present.cpu().numpy().view(np.uint64), masks)
+    got = sh.cpu().numpy().transpose(1, 0, 2)
+    for g in range(G):
+        for r in range(n):
+            if (int(masks[g]) >> r) & 1:
+                assert np.array_equal(got[g, r, :S], want[g, r, :S]), (g, r)
+            else:
+                assert (got[g, r] == 0xAB).all(), (g, r)
+
+
+@pytest.mark.gpu
 def test_rx_assemble_rejects_pageable_host_memory(gpu):
     """A ring the GPU cannot reach is refused up front, not faulted on."""
     codec = fec.New(10, 3)

@@ -11,6 +11,11 @@
 //                   shard (the 11th triggers Reconstruct on the GPU)
 //   input_batch_B   the same lossy stream with ugo_fecconn_set_batch(B):
 //                   one launch per B lossy groups, flush included
+//   shim_*          the cgo shim of INTEGRATION.md §2, call for call (GoShim
+//                   below: check_shards, copy into the pinned stage at the
+//                   16-B pitch, *_host with groups = 1, copy out): Encode of a
+//                   1470-B calcECC window, Reconstruct / ReconstructData of a
+//                   1476-B input group with one lost data shard
 //
 // Prints one JSON line per case: median / p10 / p90 microseconds per group
 // (per call for calc_ecc and encode_host_g1) over `reps` repetitions.
@@ -71,6 +76,59 @@ std::vector<std::vector<uint8_t>> stream(uint32_t base, int groups, int drop, st
   return out;
 }
 
+// INTEGRATION.md §2's Go shim in C++, statement for statement (Go slices ->
+// std::vector; a nil / empty shard -> an empty vector).
+struct GoShim {
+  ugo_fec* ctx = nullptr;
+  int d = 0, p = 0;
+  void* stage = nullptr;
+  size_t stageN = 0;
+  static size_t pitch(size_t S) { return (S + 15) & ~size_t(15); }
+  uint8_t* staging(size_t n) {
+    if (n > stageN) {
+      if (stage) ugo_fec_host_free(stage);
+      ugo_fec_host_alloc(n, &stage);
+      stageN = n;
+    }
+    return static_cast<uint8_t*>(stage);
+  }
+  int check(const std::vector<std::vector<uint8_t>>& shards, bool nilOK, size_t* S) {
+    const int n = d + p;
+    if (static_cast<int>(shards.size()) != n) return UGO_FEC_ERR_TOO_FEW_SHARDS;
+    std::vector<size_t> lens(n);
+    for (int i = 0; i < n; ++i) lens[i] = shards[i].size();
+    return ugo_fec_check_shards(n, lens.data(), nilOK ? 1 : 0, S);
+  }
+  int Encode(std::vector<std::vector<uint8_t>>& shards) {
+    size_t S = 0;
+    if (int st = check(shards, false, &S)) return st;
+    const size_t n = d + p, P = pitch(S);
+    uint8_t* buf = staging(n * P);
+    for (int k = 0; k < d; ++k) std::memcpy(buf + k * P, shards[k].data(), S);
+    if (int st = ugo_fec_encode_host(ctx, buf, 1, S, P)) return st;
+    for (size_t k = d; k < n; ++k) std::memcpy(shards[k].data(), buf + k * P, S);
+    return UGO_FEC_OK;
+  }
+  int reconstruct(std::vector<std::vector<uint8_t>>& shards, unsigned flags) {
+    size_t S = 0;
+    if (int st = check(shards, true, &S)) return st;
+    const size_t n = d + p, P = pitch(S);
+    uint8_t* buf = staging(n * P);
+    uint64_t mask[4] = {0, 0, 0, 0};
+    for (size_t r = 0; r < n; ++r)
+      if (!shards[r].empty()) {
+        mask[r / 64] |= 1ull << (r % 64);
+        std::memcpy(buf + r * P, shards[r].data(), S);
+      }
+    int8_t status = 0;
+    if (int st = ugo_fec_reconstruct_host(ctx, buf, mask, 1, S, P, flags, &status)) return st;
+    const size_t limit = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? d : n;
+    for (size_t r = 0; r < limit; ++r)
+      if (shards[r].empty()) shards[r].assign(buf + r * P, buf + r * P + S);
+    return UGO_FEC_OK;
+  }
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -117,6 +175,45 @@ int main(int argc, char** argv) {
     report("encode_host_g1", t, "us per call (one group)");
     ugo_fec_host_free(p);
     ugo_fec_destroy(ctx);
+  }
+
+  // the cgo shim's call sequence
+  {
+    GoShim shim;
+    shim.d = D;
+    shim.p = P;
+    check(ugo_fec_create(0, D, P, &shim.ctx), "create");
+    auto group = [&](size_t S) {
+      std::vector<std::vector<uint8_t>> g(N, std::vector<uint8_t>(S));
+      for (auto& b : g)
+        for (auto& x : b) x = static_cast<uint8_t>(rng());
+      return g;
+    };
+    auto time_case = [&](const char* name, size_t S, auto&& call) {
+      auto g = group(S);
+      check(shim.Encode(g), "shim encode");
+      for (int i = 0; i < 200; ++i) call(g);
+      std::vector<double> t;
+      for (int i = 0; i < reps; ++i) {
+        const auto t0 = clk::now();
+        call(g);
+        t.push_back(us_since(t0));
+      }
+      report(name, t, "us per call (one group)");
+    };
+    time_case("shim_encode_1470", PKT - 6, [&](auto& g) { check(shim.Encode(g), "shim encode"); });
+    time_case("shim_reconstruct_1476_1loss", PKT, [&](auto& g) {
+      auto w = g;
+      w[3].clear();
+      check(shim.reconstruct(w, 0), "shim reconstruct");
+    });
+    time_case("shim_reconstruct_data_1476_1loss", PKT, [&](auto& g) {
+      auto w = g;
+      w[3].clear();
+      check(shim.reconstruct(w, UGO_FEC_RECONSTRUCT_DATA_ONLY), "shim reconstruct data");
+    });
+    if (shim.stage) ugo_fec_host_free(shim.stage);
+    ugo_fec_destroy(shim.ctx);
   }
 
   // input: lossless / lossy per call / lossy batched

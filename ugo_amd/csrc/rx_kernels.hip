@@ -15,8 +15,12 @@
 //
 // Duplicates: input drops a packet whose seqid is already queued, so the
 // first arrival of a seqid is the one kept (ugo/fec.go:123-129).  A batch is
-// one window of arrivals in ring order, and the first copy in ring order must
-// win.  Duplicates are rare, so placement is optimistic: the place kernel
+// filled by one or more calls, each a window of arrivals in ring order; the
+// first copy wins, across calls as within one.  Across calls: the call's
+// first launch snapshots the presence masks (8 B per group), and a packet
+// whose bit was already set there belongs to a seqid an earlier call placed --
+// it is a duplicate and writes nothing.  Within a call the first copy in ring
+// order must win.  Duplicates are rare, so placement is optimistic: the place kernel
 // writes every accepted packet and learns from its presence atomicOr whether
 // the (group, row) was already taken; if any was, a flag is set and three
 // gated kernels -- which return at once when it is not -- fill the claim
@@ -120,6 +124,7 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
     const uint64_t grp = seqid / a.n;
     if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
     const uint64_t gs = grp - a.first_group;
+    if (!why && a.prev && ((a.prev[gs] >> row) & 1ull)) why = 4;  // placed by an earlier call
     if (!why && a.win && a.win[gs * a.n + row] != static_cast<uint32_t>(i)) why = 4;  // not the first copy
     const bool ok = why == 0;
     uint8_t* dst = a.shards + row * a.rstride + gs * a.gstride;
@@ -247,6 +252,8 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
     // only waited for at the stores (a duplicate's payload is loaded, then dropped)
     uint32_t claim = static_cast<uint32_t>(i);
     if (acc && a.win) claim = a.win[(grp - a.first_group) * a.n + row];
+    uint64_t before = 0;  // presence at call entry: set = an earlier call placed this seqid
+    if (acc && a.prev) before = a.prev[grp - a.first_group];
     const uint32_t L = acc ? min(len - 6u, a.S) : 0u;  // payload bytes kept
     const uint32_t lim = acc ? L + 6u : 0u;            // packet bytes [0, lim) are needed
     u32x4 A[NP];
@@ -264,6 +271,7 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
       }
     }
     if (acc && claim != static_cast<uint32_t>(i)) why = 4;  // a later copy of a claimed seqid
+    if (acc && ((before >> row) & 1ull)) why = 4;           // a copy of an earlier call's seqid
     const bool ok = why == 0;
     uint8_t* dst = a.shards + row * a.rstride + (grp - a.first_group) * a.gstride;
 #pragma unroll
@@ -346,13 +354,30 @@ __global__ __launch_bounds__(256) void k_rx_claim(RxArgs a) {
     if (flag != 0xf1u && flag != 0xf2u) continue;
     const uint64_t grp = seqid / a.n;
     if (grp < a.first_group || grp >= a.first_group + a.groups) continue;
-    atomicMin(&a.win[(grp - a.first_group) * a.n + seqid % a.n], static_cast<uint32_t>(i));
+    const uint32_t row = seqid % a.n;
+    if (a.prev && ((a.prev[grp - a.first_group] >> row) & 1ull)) continue;  // an earlier call's seqid
+    atomicMin(&a.win[(grp - a.first_group) * a.n + row], static_cast<uint32_t>(i));
   }
 }
 
 __global__ __launch_bounds__(256) void k_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate) {
   if (gate && *gate == 0u) return;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < words; i += gridDim.x * 256ull) win[i] = 0xffffffffu;
+}
+
+__global__ __launch_bounds__(256) void k_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups,
+                                                  uint32_t* dup) {
+  const uint64_t t = blockIdx.x * 256ull + threadIdx.x;
+  if (t == 0) *dup = 0u;
+  for (uint64_t g = t; g < groups; g += gridDim.x * 256ull) prev[g] = present[g];
+}
+
+hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, hipStream_t s) {
+  uint64_t blocks = (groups + 255) / 256;
+  if (blocks == 0) blocks = 1;
+  if (blocks > 1024u) blocks = 1024u;
+  launch(kKRx, k_rx_begin, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, present, prev, groups, dup);
+  return hipGetLastError();
 }
 
 hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, hipStream_t s) {

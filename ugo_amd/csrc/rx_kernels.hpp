@@ -17,6 +17,8 @@ struct RxArgs {
   uint32_t* win;           // [groups][n] first packet index per (group, row) (k_rx_claim), or null
   uint32_t* dup;           // optimistic pass: set to 1 when a packet finds its presence bit set, or null
   const uint32_t* gate;    // if non-null, the kernel does nothing unless *gate != 0
+  const uint64_t* prev;    // presence masks at call entry (launch_rx_begin's snapshot), or null: a packet
+                           // whose bit was already set there is a duplicate of an earlier call's copy
   uint32_t fixup;          // re-place pass: claim winners only, no stats, presence already set
   uint64_t npk;
   uint64_t slot;
@@ -31,6 +33,8 @@ struct RxArgs {
 // Claims every (group, row) for its first packet in ring order (atomicMin of
 // the packet index into a.win, which launch_rx_fill sets to 0xffffffff), then
 // places the winners.  a.win == null places every accepted packet.
+// Call entry: *dup = 0 and prev[g] = present[g] for every group (one launch).
+hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, hipStream_t s);
 hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, hipStream_t s);
 hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s);
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s);

@@ -902,14 +902,19 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   // (rx_kernels.hip): place everything, flag a (group, row) taken twice, and
   // only then -- gated on the flag, on the device -- claim and re-place.
   const hipStream_t s = static_cast<hipStream_t>(stream);
+  // scratch: presence snapshot [groups] u64 | claim words [groups][n] u32 | dup flag
   const uint64_t words = groups * uint64_t(c->n);
   void* scratch = nullptr;
-  int st = scratch_alloc(c, words * sizeof(uint32_t) + 16, s, &scratch);
+  int st = scratch_alloc(c, groups * sizeof(uint64_t) + words * sizeof(uint32_t) + 16, s, &scratch);
   if (st) return st;
-  uint32_t* win = static_cast<uint32_t*>(scratch);
+  uint64_t* prev = static_cast<uint64_t*>(scratch);
+  uint32_t* win = reinterpret_cast<uint32_t*>(prev + groups);
   uint32_t* dup = win + words;
-  if (hipMemsetAsync(dup, 0, sizeof(uint32_t), s) != hipSuccess) st = UGO_FEC_ERR_HIP;
+  // call entry: dup = 0 and the presence snapshot -- a (group, row) an earlier
+  // call placed keeps that call's copy (ugo/fec.go:123-129 keeps the first)
+  st = hip_status(ugo::kern::launch_rx_begin(present, prev, groups, dup, s));
   a.dup = dup;
+  a.prev = prev;
   if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
   if (!st) st = hip_status(ugo::kern::launch_rx_fill(win, words, dup, s));
   ugo::kern::RxArgs f = a;  // the gated claim and re-place of the first copies
