@@ -49,7 +49,8 @@ extern "C" {
  *    words per group (one word, as before, for d+p <= 64). */
 /* 4: ugo_fec_rx_assemble keeps the first copy of a seqid across calls into one
  *    batch too (a (group, row) already present at call entry is not written). */
-#define UGO_FEC_ABI_VERSION 4
+/* 5: ugo_fec_reconstruct_rows (row-pointer batches) and ugo_fec_device_address. */
+#define UGO_FEC_ABI_VERSION 5
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
  * that ugo/fec.go logs and swallows (ugo/fec.go:60-63, 208-210, 239-241). */
@@ -134,6 +135,31 @@ int ugo_fec_reconstruct_into(ugo_fec* ctx, const uint8_t* shards, const uint64_t
                              size_t shard_size, size_t row_stride, size_t group_stride, uint8_t* out,
                              size_t out_row_stride, size_t out_group_stride, unsigned flags,
                              int8_t* status, void* stream);
+
+/* Reconstruct from a table of row pointers: the rows of a group need not sit
+ * in a batch.  Row r of group g is rows[g*(d+p) + r], a DEVICE address
+ * (device memory, or pinned host memory through its device mapping -- see
+ * ugo_fec_device_address; the kernels then read it over PCIe in place, e.g. a
+ * pool of received packet buffers).  Entries of absent rows are not read.
+ * Presence, survivors, outputs, flags and status as ugo_fec_reconstruct_into
+ * (Encoder.Reconstruct, ugo/fec.go:202, with erased shards nil and filled in
+ * fresh buffers): output i of group g -- the i-th erased row, ascending --
+ * goes to out + g*out_group_stride + i*out_row_stride, i < p (DATA_ONLY:
+ * i < min(d, p), the most data rows a recoverable group can miss).  The survivor rows a
+ * group uses must be 16-B aligned and non-null, else that group gets status
+ * UGO_FEC_ERR_INVALID_ARG (checked on the device) and is not written.
+ * `rows`, `present`, `status`, `out`: device or pinned host memory; out
+ * 16-B aligned with strides % 16 == 0; d+p <= 64.  Asynchronous on `stream`.
+ * rows[] may be overwritten, and the rows it points to reused, only after
+ * the stream has passed this call. */
+int ugo_fec_reconstruct_rows(ugo_fec* ctx, const uint8_t* const* rows, const uint64_t* present, size_t groups,
+                             size_t shard_size, uint8_t* out, size_t out_row_stride, size_t out_group_stride,
+                             unsigned flags, int8_t* status, void* stream);
+
+/* The device address of p (device memory of ctx's GPU: p itself; pinned host
+ * memory: its device mapping, which on ROCm is the host address), or
+ * UGO_FEC_ERR_INVALID_ARG for memory ctx's GPU cannot reach (pageable). */
+int ugo_fec_device_address(const ugo_fec* ctx, const void* p, void** dev);
 
 /* ---- host-buffer batch (synchronous) ------------------------------------
  * Same contracts with HOST pointers: the engine stages through its own device

@@ -57,21 +57,33 @@ int ugo_fecconn_input(ugo_fecconn* f, const uint8_t* wire, size_t len, uint32_t*
 int ugo_fecconn_calc_ecc(ugo_fecconn* f, uint8_t* const* bufs, const size_t* lens, int n, int offset,
                          int maxlen);
 
-/* Batched recovery (a GPU extension; ugo has none).  With groups > 0, input
- * does not Reconstruct each recoverable lossy group (ugo/fec.go:196-217) on
- * its own: the group's shards[k][:maxlen] are copied into a pinned batch that
- * is recovered in ONE launch when it holds `groups` groups (inside the
- * ugo_fecconn_input call that completes it) or on ugo_fecconn_flush.  The
- * recovered data shards then come back group by group in completion order,
- * each group's in index order -- the concatenation of what per-call input
- * returns, delayed.  The rx queue, buffer pool, dedupe, expiry and rxlimit
- * trim are unchanged.  In this mode ugo_fecconn_input and ugo_fecconn_flush
- * need out_cap >= groups * d * UGO_FEC_MAX_PACKET (checked before anything
- * is consumed).  groups = 0 restores per-call recovery (the default).  Both
- * calls first flush what is pending into out (same capacity rule, the old
- * batch size's).  UGO_FEC_ERR_INVALID_ARG for groups < 0 or d+p > 64. */
+/* Batched recovery (a GPU extension; ugo has none).  The pool buffers decode
+ * fills live in pinned host memory, and a lost group's survivors are read by
+ * the GPU where they are (ugo_fec_reconstruct_rows), never copied into a
+ * batch.  With groups > 0, input does not Reconstruct each recoverable lossy
+ * group (ugo/fec.go:196-217) on its own: the group is recorded, and the batch
+ * is recovered in ONE launch when it holds `groups` groups, or on
+ * ugo_fecconn_flush.  The recovered data shards come back group by group in
+ * completion order, each group's in index order -- the concatenation of what
+ * per-call input returns, delayed.  The rx queue, buffer pool (LIFO order and
+ * bytes, stale tails included), dedupe, expiry and rxlimit trim are unchanged.
+ *   flags 0: a full batch is recovered inside the ugo_fecconn_input call that
+ *     fills it, and its shards come back from that call;
+ *   UGO_FECCONN_BATCH_OVERLAP: that launch runs on while input goes on with
+ *     the next batch, and its shards come back from the input call that fills
+ *     the NEXT batch (or from ugo_fecconn_flush): one batch later, the GPU time
+ *     off the packet path.
+ * Output capacity (checked before anything is consumed): ugo_fecconn_input
+ * needs out_cap >= groups * d * UGO_FEC_MAX_PACKET (per-call mode: d packets),
+ * ugo_fecconn_flush and ugo_fecconn_set_batch[_ex] that much for the current
+ * mode's pending groups (OVERLAP: twice that).  groups = 0 restores per-call
+ * recovery (the default).  Both calls first flush what is pending into out.
+ * UGO_FEC_ERR_INVALID_ARG for groups < 0, unknown flags or d+p > 64. */
+#define UGO_FECCONN_BATCH_OVERLAP 1u
 int ugo_fecconn_set_batch(ugo_fecconn* f, int groups, uint8_t* out, size_t out_cap, int* nrec,
                           size_t* rec_len);
+int ugo_fecconn_set_batch_ex(ugo_fecconn* f, int groups, unsigned flags, uint8_t* out, size_t out_cap, int* nrec,
+                             size_t* rec_len);
 int ugo_fecconn_flush(ugo_fecconn* f, uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len);
 /* Lossy groups staged and not yet recovered. */
 int ugo_fecconn_pending(const ugo_fecconn* f, size_t* groups);

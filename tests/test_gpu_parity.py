@@ -852,3 +852,93 @@ def test_jumbo_encode_four_russians_vs_oracle(gpu, S, shard_major):
         enc.encode_batch(t, shard_size=S)
         got = t.cpu().numpy()
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("d,p,S,where,data_only", [
+    (10, 3, 1476, "pinned", True),    # the FEC object's batched recovery: pooled 1476-B buffers
+    (10, 3, 1476, "pinned", False),
+    (10, 3, 1470, "device", False),
+    (20, 4, 1000, "device", False),   # d+p > 16: per-group descriptors (k_prepare)
+    (5, 3, 17, "pinned", True),       # a 1-byte tail chunk
+    (40, 8, 300, "device", False),    # d > 8 inputs and e up to 8 outputs in one pass each
+])
+def test_reconstruct_rows_vs_oracle(gpu, d, p, S, where, data_only):
+    """ugo_fec_reconstruct_rows: every row of every group at its own address in
+    a shuffled pool of slots (device memory, or pinned host memory read in
+    place over PCIe), absent rows NULL, erased rows' old slots holding garbage.
+    Recovered rows, statuses and untouched slots vs the oracle."""
+    n, G = d + p, 300
+    rng = np.random.default_rng(d * 1000 + S)
+    data = rng.integers(0, 256, (G, n, S), dtype=np.uint8)
+    rs_ref.c_encode(d, p, data)
+    ne = rng.integers(0, p + 2, G)  # p+1 erasures: too few shards
+    masks = np.full(G, (1 << n) - 1, np.uint64)
+    for g in range(G):
+        for r in rng.choice(n, int(ne[g]), replace=False):
+            masks[g] &= ~np.uint64(1 << int(r))
+    sp = (S + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+    nslots = G * n + 37
+    slot_of = rng.permutation(nslots)[:G * n].reshape(G, n)
+    enc = fec.New(d, p)
+    pool_host = rng.integers(0, 256, (nslots, sp), dtype=np.uint8)
+    for g in range(G):
+        for r in range(n):
+            if (int(masks[g]) >> r) & 1:
+                pool_host[slot_of[g, r], :S] = data[g, r]
+    keep = []
+    if where == "pinned":
+        raw = fec.host_alloc(nslots * sp)
+        keep.append(raw)
+        pool = raw.reshape(nslots, sp)
+        pool[:] = pool_host
+        base = enc.device_address(pool.ctypes.data)
+        rows_raw = fec.host_alloc(G * n * 8)
+        keep.append(rows_raw)
+        rows = rows_raw.view(np.int64).reshape(G, n)
+        pres_raw = fec.host_alloc(G * 8)
+        keep.append(pres_raw)
+        present = pres_raw.view(np.uint64)
+        present[:] = masks
+    else:
+        pool = torch.from_numpy(pool_host).cuda()
+        base = pool.data_ptr()
+        rows = np.zeros((G, n), np.int64)
+        present = _masks_to_dev(masks)
+    try:
+        for g in range(G):
+            for r in range(n):
+                rows[g, r] = base + int(slot_of[g, r]) * sp if (int(masks[g]) >> r) & 1 else 0
+        bad_g = int(np.nonzero((ne > 0) & (ne <= p))[0][0])  # a recoverable group with a misaligned survivor
+        first_present = next(r for r in range(n) if (int(masks[bad_g]) >> r) & 1)
+        rows[bad_g, first_present] += 1
+        rows_arg = rows if where == "pinned" else torch.from_numpy(rows).cuda()
+        out = torch.full((p, G, sp), 0xA5, dtype=torch.uint8, device="cuda")
+        st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+        enc.reconstruct_rows(rows_arg, present, out, S, data_only=data_only, status=st)
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        stv = st.cpu().numpy()
+        want_rc = data.copy()
+        erased = _erase(want_rc, masks, n)
+        rc, want_st = rs_ref.c_reconstruct(d, p, erased, masks, data_only=data_only)
+        for g in range(G):
+            er = [r for r in range(n) if not (int(masks[g]) >> r) & 1]
+            if g == bad_g:
+                assert stv[g] == 6 and (o[:, g] == 0xA5).all(), g
+                continue
+            assert stv[g] == want_st[g], (g, stv[g], want_st[g])
+            if want_st[g] != 0:
+                assert (o[:, g] == 0xA5).all(), g
+                continue
+            outs = [r for r in er if r < d] if data_only else er
+            for i, r in enumerate(outs):
+                assert np.array_equal(o[i, g, :S], data[g, r]), (g, i, r)
+                assert (o[i, g, S:] == 0xA5).all(), (g, i)  # padding of the output slot untouched
+            assert (o[len(outs):, g] == 0xA5).all(), g
+        # the pool is only read
+        now = pool if where == "pinned" else pool.cpu().numpy()
+        assert np.array_equal(np.asarray(now), pool_host)
+    finally:
+        del pool
+        for k in keep:
+            fec.host_free(k)

@@ -11,6 +11,8 @@
 //                   shard (the 11th triggers Reconstruct on the GPU)
 //   input_batch_B   the same lossy stream with ugo_fecconn_set_batch(B):
 //                   one launch per B lossy groups, flush included
+//   input_batch_B_overlap  the same with UGO_FECCONN_BATCH_OVERLAP (each batch
+//                   recovered while the next fills), flush included
 //   shim_*          the cgo shim of INTEGRATION.md §2, call for call (GoShim
 //                   below: check_shards, copy into the pinned stage at the
 //                   16-B pitch, *_host with groups = 1, copy out): Encode of a
@@ -41,12 +43,13 @@ double us_since(clk::time_point t0) {
   return std::chrono::duration<double, std::micro>(clk::now() - t0).count();
 }
 
-void report(const char* name, std::vector<double> v, const char* unit, double extra = -1.0) {
+void report(const char* name, std::vector<double> v, const char* unit, double extra = -1.0, double mean = -1.0) {
   std::sort(v.begin(), v.end());
   const auto q = [&](double f) { return v[std::min(v.size() - 1, static_cast<size_t>(f * v.size()))]; };
   std::printf("{\"case\": \"%s\", \"median_us\": %.3f, \"p10_us\": %.3f, \"p90_us\": %.3f, \"unit\": \"%s\", \"reps\": %zu",
               name, q(0.5), q(0.1), q(0.9), unit, v.size());
   if (extra >= 0) std::printf(", \"groups_per_rep\": %.0f", extra);
+  if (mean >= 0) std::printf(", \"mean_us\": %.3f", mean);
   std::printf("}\n");
   std::fflush(stdout);
 }
@@ -218,20 +221,28 @@ int main(int argc, char** argv) {
 
   // input: lossless / lossy per call / lossy batched
   std::vector<uint8_t> out(size_t(4096) * D * PKT);
-  auto run = [&](const char* name, int drop, int batch) {
+  auto run = [&](const char* name, int drop, int batch, unsigned flags = 0) {
     const int gpr = std::max(64, batch);  // groups per repetition
     const int nrep = std::max(10, reps / gpr);
     ugo_fecconn* f = nullptr;
     check(ugo_fecconn_new(RXLIMIT, D, P, 0, &f), "new");
     int nrec = 0;
     size_t rl = 0;
-    check(ugo_fecconn_set_batch(f, batch, out.data(), out.size(), &nrec, &rl), "set_batch");
+    check(ugo_fecconn_set_batch_ex(f, batch, flags, out.data(), out.size(), &nrec, &rl), "set_batch");
     uint32_t base = 0;
     std::vector<double> t;
     long recovered = 0;
-    for (int r = -3; r < nrep; ++r) {  // 3 untimed repetitions
-      const auto pk = stream(base, gpr, drop, rng);
+    // batched: one continuous stream, flushed once at its end (a flush per
+    // repetition would wait for every batch the moment it is launched);
+    // per call: repetitions timed one by one
+    std::vector<std::vector<std::vector<uint8_t>>> reps_pk;
+    for (int r = 0; r < nrep + 3; ++r) {
+      reps_pk.push_back(stream(base, gpr, drop, rng));
       base += static_cast<uint32_t>(gpr * N);
+    }
+    double total = 0;
+    for (int r = -3; r < nrep; ++r) {  // 3 untimed repetitions
+      const auto& pk = reps_pk[r + 3];
       const auto t0 = clk::now();
       for (const auto& w : pk) {
         uint32_t seq;
@@ -239,16 +250,24 @@ int main(int argc, char** argv) {
         check(ugo_fecconn_input(f, w.data(), w.size(), &seq, &flag, out.data(), out.size(), &nrec, &rl), "input");
         recovered += nrec;
       }
-      check(ugo_fecconn_flush(f, out.data(), out.size(), &nrec, &rl), "flush");
-      recovered += nrec;
-      if (r >= 0) t.push_back(us_since(t0) / gpr);
+      if (batch == 0 || r == -1 || r == nrep - 1) {
+        check(ugo_fecconn_flush(f, out.data(), out.size(), &nrec, &rl), "flush");
+        recovered += nrec;
+      }
+      const double us = us_since(t0);
+      if (r >= 0) {
+        t.push_back(us / gpr);
+        total += us;
+      }
     }
     const long want = drop >= 0 && drop < D ? static_cast<long>(nrep + 3) * gpr : 0;
     if (recovered != want) {
       std::fprintf(stderr, "%s: recovered %ld shards, expected %ld\n", name, recovered, want);
       std::exit(1);
     }
-    report(name, t, "us per group (all its input calls)", gpr);
+    report(name, t, batch ? "us per group (all its input calls; repetitions of one stream, the last one "
+                            "with the final flush)" : "us per group (all its input calls)", gpr,
+           total / (double(nrep) * gpr));
     ugo_fecconn_free(f);
   };
   run("input_lossless", -1, 0);
@@ -256,5 +275,8 @@ int main(int argc, char** argv) {
   run("input_batch_16", 3, 16);
   run("input_batch_64", 3, 64);
   run("input_batch_256", 3, 256);
+  run("input_batch_16_overlap", 3, 16, UGO_FECCONN_BATCH_OVERLAP);
+  run("input_batch_64_overlap", 3, 64, UGO_FECCONN_BATCH_OVERLAP);
+  run("input_batch_256_overlap", 3, 256, UGO_FECCONN_BATCH_OVERLAP);
   return 0;
 }

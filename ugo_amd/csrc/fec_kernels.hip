@@ -761,6 +761,145 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (wst) a.status[g] = 0;
 }
 
+// 64-bit wave-uniform value into SGPRs.
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// k_apply_qa with its per-product overhead cut (round 3, the jumbo
+// reconstruct).  The ISA of k_apply_qa showed three VALU costs beside the
+// 3 v_perm + 1.5 v_bitop3 per product dword:
+//   OPT & 1: the descriptor pointer came out of a VALU division (group =
+//            wave offset / padded row), lived in VGPRs, and every scalar
+//            coefficient load paid two v_readfirstlane: now made SGPR once;
+//   OPT & 2: each input load computed its 64-bit address per lane (v_mov +
+//            v_mad_u64_u32 + v_add): now the row base is uniform (SGPRs) and
+//            the lane adds a 32-bit offset (the global saddr form);
+//   OPT & 4: the 2-deep input ring was rotated by 8 v_mov per pair: now the
+//            loop is unrolled over two pairs, each loaded into its own
+//            registers.
+template <int EMAX, int MODE, int NT, int OPT = 7, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_qb(Batch a) {
+  const uint32_t cpad = (a.chunks + 63u) & ~63u;
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  if (wfirst >= a.items) return;  // a.items = groups * cpad here
+  const uint32_t gl = (OPT & 1) ? __builtin_amdgcn_readfirstlane(wfirst / cpad) : wfirst / cpad;
+  const uint64_t g = a.g0 + gl;
+  const uint8_t* dA = desc_for<MODE>(a, g);
+  // OPT & 1: descriptor words and coefficient tables through the constant
+  // address space from an SGPR base (a plain pointer made uniform by
+  // readfirstlane turns them into flat / per-lane vector loads)
+  const uint64_t dU = (OPT & 1) ? rfl64(reinterpret_cast<uint64_t>(dA)) : 0;
+  auto dword = [&](uint32_t off) -> uint32_t {
+    if constexpr (OPT & 1)
+      return *(ctab_t)(dU + off);
+    else
+      return ld32(dA + off);
+  };
+  const uint32_t hA = dword(0);
+  const uint32_t st = (hA >> 16) & 0xffu;
+  const uint32_t e = st ? 0u : (a.data_only ? ((hA >> 8) & 0xffu) : (hA & 0xffu));
+  const uint32_t c = blockIdx.x * 256u + threadIdx.x - gl * cpad;
+  const bool live = c < a.chunks;
+  const bool wst = MODE != 0 && a.status != nullptr && c == 0;
+  if (e == 0) {  // wave-uniform
+    if (wst) a.status[g] = static_cast<int8_t>(st);
+    return;
+  }
+  const uint32_t coff = live ? c * 16u : 0u;
+  const uint8_t* gbase = a.base + g * a.gstride;  // wave-uniform
+  auto load_in = [&](uint32_t k) -> V4 {
+    if (k >= a.d) return V4{{0u, 0u, 0u, 0u}};
+    const uint32_t r = (dword(4 + (k & ~3u)) >> (8 * (k & 3u))) & 0xffu;
+    if constexpr (OPT & 2) {
+      const uint8_t* rb = gbase + static_cast<uint64_t>(r) * a.rstride;  // SGPRs
+      uint32_t co = coff;
+      asm("" : "+v"(co));  // opaque per load: gbase + coff is not hoisted into a 64-bit VGPR pair
+      return load16<NT>(rb + co);
+    } else {
+      return load16<NT>(gbase + coff + static_cast<uint64_t>(r) * a.rstride);
+    }
+  };
+  auto tables = [&](uint32_t* t, uint32_t off, int kb) {
+    const uint32_t cf = (dword(off) >> (8 * (kb & 3))) & 0xffu;
+    if constexpr (OPT & 1) {
+      const ctab_t tA = (ctab_t)(a.mult) + 8u * cf;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) t[q] = tA[q];
+    } else {
+      const uint32_t* tA = a.mult + 8u * cf;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) t[q] = tA[q];
+    }
+  };
+  const uint32_t cbase = 4 + a.dpad + a.epad;
+  V4 acc[EMAX];
+#pragma unroll
+  for (int i = 0; i < EMAX; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
+  // fold the pair (k, k+1) whose selectors are s, r into the accumulators
+  auto fold = [&](uint32_t k, const uint32_t* s0, const uint32_t* s1, const uint32_t* s2, const uint32_t* r0,
+                  const uint32_t* r1, const uint32_t* r2, int kb) {
+#pragma unroll
+    for (int i = 0; i < EMAX; ++i) {
+      if (i >= static_cast<int>(e)) continue;
+      const uint32_t off = cbase + i * a.dpad + (k & ~3u);  // coefficient word of inputs k, k+1
+      uint32_t t[5], u[5];
+      tables(t, off, kb);
+      tables(u, off, kb + 1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t y = xor3(acc[i].v[q], perm(t[1], t[0], s0[q]), perm(t[3], t[2], s1[q]));
+        y = xor3(y, perm(0u, t[4], s2[q]), perm(u[1], u[0], r0[q]));
+        acc[i].v[q] = xor3(y, perm(u[3], u[2], r1[q]), perm(0u, u[4], r2[q]));
+      }
+    }
+  };
+  if constexpr (OPT & 4) {
+    // k0 % 4 == 0: pair A = inputs k0, k0+1 (coefficient bytes 0, 1 of the word),
+    // pair B = k0+2, k0+3 (bytes 2, 3); A's next pair is loaded after A's selectors
+    V4 a0 = load_in(0), a1 = load_in(1);
+    for (uint32_t k0 = 0; k0 < a.d; k0 += 4) {
+      uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
+      p_sel(a0, s0, s1, s2);
+      p_sel(a1, r0, r1, r2);
+      const V4 b0 = load_in(k0 + 2), b1 = load_in(k0 + 3);
+      fold(k0, s0, s1, s2, r0, r1, r2, 0);
+      p_sel(b0, s0, s1, s2);
+      p_sel(b1, r0, r1, r2);
+      a0 = load_in(k0 + 4);
+      a1 = load_in(k0 + 5);
+      fold(k0 + 2, s0, s1, s2, r0, r1, r2, 2);
+    }
+  } else {
+    V4 ring[2] = {load_in(0), load_in(1)};
+    for (uint32_t k = 0; k < a.d; k += 2) {
+      uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
+      p_sel(ring[0], s0, s1, s2);
+      p_sel(ring[1], r0, r1, r2);
+      ring[0] = load_in(k + 2);
+      ring[1] = load_in(k + 3);
+      fold(k, s0, s1, s2, r0, r1, r2, static_cast<int>(k & 3u));
+    }
+  }
+  if (live) {
+    const uint32_t nb = a.S - coff;
+    constexpr int NO = (EMAX + 3) / 4;
+    uint32_t orw[NO];
+#pragma unroll
+    for (int w = 0; w < NO; ++w) orw[w] = dword(4 + a.dpad + 4 * w);
+    uint8_t* gp = const_cast<uint8_t*>(gbase) + coff;
+#pragma unroll
+    for (int i = 0; i < EMAX; ++i) {
+      if (i >= static_cast<int>(e)) continue;
+      const uint32_t r = (orw[i >> 2] >> (8 * (i & 3))) & 0xffu;
+      store16<NT>(out_row(a, gp, g, coff, r, i), acc[i], nb);
+    }
+  }
+  if (wst) a.status[g] = 0;
+}
+
 // generic: any alignment / stride / d (<= 255); 4 columns per lane, byte I/O
 __device__ __forceinline__ uint32_t gfmul_var(uint32_t cbyte, uint32_t x) {
   uint32_t t = 0;
@@ -802,6 +941,109 @@ __global__ __launch_bounds__(256) void k_apply_bytes(Batch a) {
     uint8_t* dst = out_row(a, gp, g, c * 4u, orow[i], i);
     for (uint32_t j = 0; j < nb; ++j) dst[j] = static_cast<uint8_t>(acc >> (8 * j));
   }
+}
+
+// ------------------------------------------------------------ k_apply_rows
+// Reconstruct from a row-pointer table (ugo_fec_reconstruct_rows): row r of
+// group g is rows[g*(d+p) + r], a device address anywhere -- typically a
+// pooled packet buffer in pinned host memory, read over PCIe in place (the
+// FEC object's batched recovery: no copy of the survivors into a batch).
+// One 16-byte chunk per thread; survivors in blocks of 16 (their loads issued
+// together: over PCIe each load is microseconds of latency), products by the
+// v_perm split tables; outputs folded 8 per pass; recovered rows go to the
+// caller's output batch, output i = the i-th erased row (ascending).  A group
+// whose survivor pointers are not 16-B aligned gets UGO_FEC_ERR_INVALID_ARG
+// and is not touched.  Latency / PCIe-bound: batches of tens of groups.
+__device__ __forceinline__ V4 load_part(const uint8_t* p, uint32_t nb) {
+  if (nb >= 16u) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+    return V4{{v.x, v.y, v.z, v.w}};
+  }
+  V4 x{{0u, 0u, 0u, 0u}};  // tail chunk: bytes [0, nb), unrolled (a runtime index would put x in scratch)
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (static_cast<uint32_t>(j) < nb) x.v[j >> 2] |= static_cast<uint32_t>(p[j]) << (8 * (j & 3));
+  return x;
+}
+
+// Wave-aligned groups (item = group * cpad + chunk, cpad = chunks rounded up to
+// 64, as k_apply_qa): everything but the row bytes is wave-uniform and read
+// with scalar loads -- descriptor, row pointers, coefficient tables.  Per-lane
+// reads of those (a wave spanning two groups) chained ~30 dependent vector
+// loads per lane and cost 28 us for one group against 6 us for the batch
+// kernel on a staged copy (rocprofv3, profiles/r3/).
+typedef const __attribute__((address_space(4))) uint64_t* ctab64_t;
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_apply_rows(Batch a) {
+  const uint32_t cpad = (a.chunks + 63u) & ~63u;
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  if (wfirst >= a.items) return;  // a.items = groups * cpad
+  const uint32_t gl = __builtin_amdgcn_readfirstlane(wfirst / cpad);
+  const uint64_t g = a.g0 + gl;
+  const uint64_t dU = rfl64(reinterpret_cast<uint64_t>(desc_for<MODE>(a, g)));
+  auto dword = [&](uint32_t off) -> uint32_t { return *(ctab_t)(dU + off); };
+  auto dbyte = [&](uint32_t off) -> uint32_t { return (dword(off & ~3u) >> (8u * (off & 3u))) & 0xffu; };
+  const uint32_t hdr = dword(0);
+  const uint32_t st = (hdr >> 16) & 0xffu;
+  const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
+  const uint32_t c = blockIdx.x * 256u + threadIdx.x - gl * cpad;
+  const bool live = c < a.chunks;
+  const bool wst = a.status != nullptr && c == 0;
+  if (st != 0 || e == 0) {  // wave-uniform
+    if (wst) a.status[g] = static_cast<int8_t>(st);
+    return;
+  }
+  const uint64_t rpU = reinterpret_cast<uint64_t>(a.rows + g * a.n);  // the group's row pointers
+  const uint32_t cbase = 4 + a.dpad + a.epad;
+  const uint32_t off = live ? c * 16u : 0u;
+  const uint32_t nb = live ? min(16u, a.S - off) : 16u;
+  // Survivors in blocks of 16: the block's pointers (scalar loads, over PCIe
+  // when the table is pinned host memory) checked, then its 16 row loads
+  // issued together.  A null or misaligned pointer is never dereferenced: the
+  // group gets UGO_FEC_ERR_INVALID_ARG and writes nothing.
+  bool bad = false;
+  for (uint32_t i0 = 0; i0 < e; i0 += 8u) {
+    V4 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
+    for (uint32_t k0 = 0; k0 < a.d; k0 += 16u) {
+      uint64_t ptr[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) ptr[j] = (k0 + j < a.d) ? *((ctab64_t)rpU + dbyte(4 + k0 + j)) : 16u;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) bad |= (ptr[j] & 15u) != 0 || ptr[j] == 0;
+      if (bad) break;  // wave-uniform
+      V4 x[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        x[j] = (k0 + j < a.d) ? load_part(reinterpret_cast<const uint8_t*>(ptr[j]) + off, nb)
+                              : V4{{0u, 0u, 0u, 0u}};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (k0 + j >= a.d) continue;
+        uint32_t s0[4], s1[4], s2[4];
+        p_sel(x[j], s0, s1, s2);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (i0 + i >= e) continue;
+          const ctab_t t = (ctab_t)(a.mult) + 8u * dbyte(cbase + (i0 + i) * a.dpad + k0 + j);
+#pragma unroll
+          for (int w = 0; w < 4; ++w)
+            acc[i].v[w] = xor3(acc[i].v[w], perm(t[1], t[0], s0[w]), perm(t[3], t[2], s1[w])) ^ perm(0u, t[4], s2[w]);
+        }
+      }
+    }
+    if (bad) break;
+    if (live) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i0 + i >= e) continue;
+        store16<0>(a.out + g * a.ogstride + static_cast<uint64_t>(i0 + i) * a.orstride + off, acc[i], nb);
+      }
+    }
+  }
+  if (wst) a.status[g] = static_cast<int8_t>(bad ? 6 : 0);  // 6: UGO_FEC_ERR_INVALID_ARG
 }
 
 // ------------------------------------------------------------- k_prepare
@@ -1192,6 +1434,18 @@ hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s) {
     case 0: launch(kKBytes, k_apply_bytes<0>, grid, block, 0, s, a); break;
     case 1: launch(kKBytes, k_apply_bytes<1>, grid, block, 0, s, a); break;
     case 2: launch(kKBytes, k_apply_bytes<2>, grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_apply_rows(int mode, const Batch& a, hipStream_t s) {
+  Batch b = a;  // wave-aligned groups
+  b.items = (a.items / a.chunks) * ((a.chunks + 63u) & ~63u);
+  const dim3 grid(blocks_for(b.items, 256)), block(256);
+  switch (mode) {
+    case 1: launch(kKReconstruct, k_apply_rows<1>, grid, block, 0, s, b); break;
+    case 2: launch(kKReconstruct, k_apply_rows<2>, grid, block, 0, s, b); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -32,6 +32,8 @@ struct Batch {
   uint8_t* out;             // reconstruct: null = erased rows rebuilt in place; else output i
   uint64_t ogstride;        //   (i-th erased row, ascending) of group g at out + g*ogstride + i*orstride
   uint64_t orstride;
+  const uint64_t* rows;     // k_apply_rows: row r of group g at rows[g*n + r] (device addresses)
+  uint32_t n;               // k_apply_rows: d + p
 };
 
 struct Prep {
@@ -56,6 +58,7 @@ hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s);
 hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s);
 hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s);
 hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s);
+hipError_t launch_apply_rows(int mode, const Batch& a, hipStream_t s);  // MODE 1 / 2, output batch required
 
 
 

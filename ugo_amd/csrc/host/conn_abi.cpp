@@ -32,9 +32,8 @@ int emit(const std::vector<ugo::Bytes>& rec, uint8_t* out, size_t out_cap, int* 
 // fail to fit would lose them): a whole batch of groups in batch mode, and for
 // input in per-call mode one group's d shards.  set_batch / flush in per-call
 // mode have nothing pending to return.
-bool batch_cap_ok(const ugo_fecconn* f, const uint8_t* out, size_t out_cap, bool per_call_input = false) {
-  size_t groups = static_cast<size_t>(f->fec->batch());
-  if (groups == 0 && per_call_input) groups = 1;
+bool batch_cap_ok(const ugo_fecconn* f, const uint8_t* out, size_t out_cap, bool is_flush = false) {
+  const size_t groups = f->fec->maxReturnGroups(is_flush);
   if (groups == 0) return true;
   return out && out_cap >= groups * static_cast<size_t>(f->fec->dataShards()) * ugo::maxPacketSize;
 }
@@ -103,7 +102,7 @@ int ugo_fecconn_input(ugo_fecconn* f, const uint8_t* wire, size_t len, uint32_t*
   if (!f || !wire || len < ugo::fecHeaderSize) return UGO_FEC_ERR_INVALID_ARG;
   if (nrec) *nrec = 0;
   if (rec_len) *rec_len = 0;
-  if (!batch_cap_ok(f, out, out_cap, true)) return UGO_FEC_ERR_INVALID_ARG;
+  if (!batch_cap_ok(f, out, out_cap)) return UGO_FEC_ERR_INVALID_ARG;
   ugo::fecPacket pkt = f->fec->decode(wire, len);
   if (seqid) *seqid = pkt.seqid;
   if (flag) *flag = pkt.flag;
@@ -119,20 +118,28 @@ int ugo_fecconn_input(ugo_fecconn* f, const uint8_t* wire, size_t len, uint32_t*
   return f->fec->lastError() == UGO_FEC_ERR_HIP ? UGO_FEC_ERR_HIP : UGO_FEC_OK;
 }
 
-int ugo_fecconn_set_batch(ugo_fecconn* f, int groups, uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len) {
+int ugo_fecconn_set_batch_ex(ugo_fecconn* f, int groups, unsigned flags, uint8_t* out, size_t out_cap, int* nrec,
+                             size_t* rec_len) {
   if (nrec) *nrec = 0;
   if (rec_len) *rec_len = 0;
-  if (!f || groups < 0 || (groups > 0 && f->fec->dataShards() + f->fec->parityShards() > 64))
+  if (!f || groups < 0 || (groups > 0 && f->fec->dataShards() + f->fec->parityShards() > 64) ||
+      (flags & ~UGO_FECCONN_BATCH_OVERLAP))
     return UGO_FEC_ERR_INVALID_ARG;
-  if (!batch_cap_ok(f, out, out_cap)) return UGO_FEC_ERR_INVALID_ARG;
-  std::vector<ugo::Bytes> rec = f->fec->setBatch(groups);
-  return emit(rec, out, out_cap, nrec, rec_len);
+  if (!batch_cap_ok(f, out, out_cap, true)) return UGO_FEC_ERR_INVALID_ARG;  // what is pending comes back
+  std::vector<ugo::Bytes> rec = f->fec->setBatch(groups, flags);
+  const int st = emit(rec, out, out_cap, nrec, rec_len);
+  if (st) return st;
+  return f->fec->lastError() == UGO_FEC_ERR_HIP ? UGO_FEC_ERR_HIP : UGO_FEC_OK;
+}
+
+int ugo_fecconn_set_batch(ugo_fecconn* f, int groups, uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len) {
+  return ugo_fecconn_set_batch_ex(f, groups, 0, out, out_cap, nrec, rec_len);
 }
 
 int ugo_fecconn_flush(ugo_fecconn* f, uint8_t* out, size_t out_cap, int* nrec, size_t* rec_len) {
   if (nrec) *nrec = 0;
   if (rec_len) *rec_len = 0;
-  if (!f || !batch_cap_ok(f, out, out_cap)) return UGO_FEC_ERR_INVALID_ARG;
+  if (!f || !batch_cap_ok(f, out, out_cap, true)) return UGO_FEC_ERR_INVALID_ARG;
   std::vector<ugo::Bytes> rec = f->fec->flush();
   const int st = emit(rec, out, out_cap, nrec, rec_len);
   if (st) return st;

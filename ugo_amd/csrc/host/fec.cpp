@@ -1,12 +1,32 @@
 // fec.cpp -- see fec.hpp.  Control logic mirrors ugo/fec.go line by line in
 // behaviour; every byte of Reed-Solomon arithmetic runs on the GPU through
-// reedsolomon::Encoder (the C-ABI), none on the CPU.
+// the C-ABI (ugo_fec_reconstruct_rows over the pinned pool, reedsolomon::
+// Encoder for calcECC), none on the CPU.
 #include "fec.hpp"
 
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 namespace ugo {
+
+namespace {
+
+constexpr size_t kSlabSlots = 256;  // pool slots per pinned slab (372 KiB)
+
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
 
 uint32_t currentMs() {  // ugo/fec.go:73-75
   using namespace std::chrono;
@@ -30,6 +50,7 @@ std::unique_ptr<FEC> FEC::newFEC(int rxlimit, int dataShards, int parityShards, 
   f->dataShards_ = dataShards;
   f->parityShards_ = parityShards;
   f->shardSize_ = dataShards + parityShards;
+  f->device_ = device;
   f->paws_ = (0xffffffffu / uint32_t(f->shardSize_) - 1) * uint32_t(f->shardSize_);  // :58
   int err = 0;
   f->enc_ = reedsolomon::New(dataShards, parityShards, &err, device);  // :59
@@ -38,21 +59,83 @@ std::unique_ptr<FEC> FEC::newFEC(int rxlimit, int dataShards, int parityShards, 
   return f;
 }
 
-Bytes* FEC::poolGet() {
+// ------------------------------------------------------------------- pool
+
+// A physical slot: from the free list, else a new slab.  Pinned slabs are
+// GPU-visible (slotDev_ != 0); if pinned memory runs out, plain memory keeps
+// the pool working and lost groups then recover through copies (recoverGroup).
+uint32_t FEC::newSlot(bool zero) {
+  if (slotFree_.empty()) {
+    void* p = nullptr;
+    bool pinned = ugo_fec_host_alloc(kSlabSlots * kSlotStride, &p) == UGO_FEC_OK;
+    if (!pinned) p = std::aligned_alloc(16, kSlabSlots * kSlotStride);
+    if (!p) std::abort();  // out of host memory, as Go's make would panic
+    auto* base = static_cast<uint8_t*>(p);
+    uint64_t dev = 0;
+    if (pinned) {
+      void* d = nullptr;
+      if (ugo_fec_device_address(enc_->handle(), base, &d) == UGO_FEC_OK) dev = reinterpret_cast<uint64_t>(d);
+    }
+    slabs_.push_back(base);
+    slabPinned_.push_back(pinned ? 1 : 0);
+    const uint32_t first = static_cast<uint32_t>(slotPtr_.size());
+    for (size_t i = 0; i < kSlabSlots; ++i) {
+      slotPtr_.push_back(base + i * kSlotStride);
+      slotDev_.push_back(dev ? dev + i * kSlotStride : 0);
+      slotHeld_.push_back(0);
+      slotOrphan_.push_back(0);
+    }
+    for (size_t i = kSlabSlots; i-- > 0;) slotFree_.push_back(first + static_cast<uint32_t>(i));
+  }
+  const uint32_t s = slotFree_.back();
+  slotFree_.pop_back();
+  if (zero) std::memset(slotPtr_[s], 0, maxPacketSize);  // make([]byte, maxPacketSize)
+  return s;
+}
+
+PoolBuf* FEC::poolGet() {  // xmitBuf.Get(): the most recently Put buffer first
   if (!poolFree_.empty()) {
-    Bytes* b = poolFree_.back();
+    PoolBuf* b = poolFree_.back();
     poolFree_.pop_back();
     return b;
   }
-  poolAll_.push_back(std::make_unique<Bytes>(maxPacketSize, 0));
+  poolAll_.push_back(std::make_unique<PoolBuf>());
+  poolAll_.back()->slot = newSlot(true);
   return poolAll_.back().get();
 }
 
-void FEC::poolPut(Bytes* b) { poolFree_.push_back(b); }
+void FEC::poolPut(PoolBuf* b) { poolFree_.push_back(b); }
 
-void FEC::dropBuffer(Bytes* b) {
+// The bytes decode is about to overwrite (head [0, n)): if a pending batch
+// still has to read this buffer's slot, the buffer moves to a fresh slot and
+// takes its tail [n, maxPacketSize) along -- the bytes Go's reused buffer
+// would still hold -- and the old slot is freed when that batch is done.
+uint8_t* FEC::writable(PoolBuf* b, size_t n) {
+  const uint32_t old = b->slot;
+  if (slotHeld_[old]) {
+    const uint32_t s = newSlot(false);
+    std::memcpy(slotPtr_[s] + n, slotPtr_[old] + n, maxPacketSize - n);
+    slotOrphan_[old] = 1;
+    b->slot = s;
+  }
+  return slotPtr_[b->slot];
+}
+
+void FEC::releaseSlot(uint32_t s) {
+  slotHeld_[s] = 0;
+  if (slotOrphan_[s]) {
+    slotOrphan_[s] = 0;
+    slotFree_.push_back(s);
+  }
+}
+
+void FEC::dropBuffer(PoolBuf* b) {
   for (size_t i = poolAll_.size(); i-- > 0;)
     if (poolAll_[i].get() == b) {
+      if (slotHeld_[b->slot])
+        slotOrphan_[b->slot] = 1;
+      else
+        slotFree_.push_back(b->slot);
       poolAll_.erase(poolAll_.begin() + static_cast<long>(i));
       return;
     }
@@ -63,9 +146,10 @@ fecPacket FEC::decode(const uint8_t* data, size_t len) {  // :78-89
   pkt.seqid = getLE32(data);
   pkt.flag = getLE16(data + 4);
   pkt.ts = clock_();
-  Bytes* buf = poolGet();
-  const size_t n = len > fecHeaderSize ? std::min(buf->size(), len - fecHeaderSize) : 0;
-  if (n) std::memcpy(buf->data(), data + fecHeaderSize, n);  // copy(buf, data[6:]); stale tail kept
+  PoolBuf* buf = poolGet();
+  const size_t n = len > fecHeaderSize ? std::min(maxPacketSize, len - fecHeaderSize) : 0;
+  uint8_t* dst = writable(buf, n);
+  if (n) std::memcpy(dst, data + fecHeaderSize, n);  // copy(buf, data[6:]); stale tail kept
   pkt.data = buf;
   return pkt;
 }
@@ -122,7 +206,7 @@ std::vector<Bytes> FEC::input(fecPacket pkt) {  // :107-226
   if (static_cast<int>(rx_.size()) >= dataShards_ && shardBegin < shardEnd) {  // :158
     int numshard = 0, numDataShard = 0, first = -1;
     size_t maxlen = 0;
-    std::vector<Bytes*> shards(shardSize_, nullptr);
+    std::vector<PoolBuf*> shards(shardSize_, nullptr);
     for (int i = searchBegin; i <= searchEnd; ++i) {  // :170-188
       const uint32_t seqid = rx_[i].seqid;
       if (seqid > shardEnd) break;
@@ -131,7 +215,7 @@ std::vector<Bytes> FEC::input(fecPacket pkt) {  // :107-226
         numshard++;
         if (rx_[i].flag == typeData) numDataShard++;
         if (numshard == 1) first = i;
-        if (rx_[i].data->size() > maxlen) maxlen = rx_[i].data->size();
+        maxlen = maxPacketSize;  // len(rx[i].data): every pool buffer is maxPacketSize long
       }
     }
     if (numDataShard == dataShards_) {  // no loss :190-195
@@ -150,55 +234,167 @@ std::vector<Bytes> FEC::input(fecPacket pkt) {  // :107-226
   return recovered;
 }
 
-// The recoverable branch of input (ugo/fec.go:196-217).  Per call: reslice
-// to maxlen, Reconstruct (:202, on the GPU), append the erased data shards in
-// index order (:203-207).  Batched: the same bytes are staged and recovered
-// with the rest of the batch (flushInto), so the result is identical.
-void FEC::recoverGroup(const std::vector<Bytes*>& shards, size_t maxlen, std::vector<Bytes>& out) {
-  if (batchCap_ > 0) {
-    const size_t n = static_cast<size_t>(shardSize_);
-    const size_t pitch = (maxlen + 15) / 16 * 16;
-    if (!pendMask_.empty() && maxlen != batchS_) flushInto(out);  // one shard size per batch
-    const size_t need = static_cast<size_t>(batchCap_) * n * pitch;
-    if (need > batchBytes_) {  // pendMask_ is empty here
-      if (batchBuf_) ugo_fec_host_free(batchBuf_);
-      batchBuf_ = nullptr;
-      batchBytes_ = 0;
-      void* p = nullptr;
-      if (ugo_fec_host_alloc(need, &p) == UGO_FEC_OK) {
-        batchBuf_ = static_cast<uint8_t*>(p);
-        batchBytes_ = need;
+// --------------------------------------------------------------- recovery
+
+bool FEC::ensureGpu() {
+  if (stream_) return true;
+  DevGuard g(device_);
+  if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+    stream_ = nullptr;
+    return false;
+  }
+  return true;
+}
+
+void FEC::freeBatch(Batch& b) {
+  if (b.mem) ugo_fec_host_free(b.mem);
+  if (b.done) (void)hipEventDestroy(b.done);
+  b = Batch{};
+}
+
+// Pinned [rows | masks | status | out] for `cap` groups (empty batch only).
+bool FEC::ensureBatch(Batch& b, size_t cap) {
+  if (b.mem && b.cap >= cap) return true;
+  const size_t n = static_cast<size_t>(shardSize_), slots = outSlots();
+  const size_t o_rows = 0, o_masks = o_rows + cap * n * 8, o_status = o_masks + cap * 8;
+  const size_t o_out = (o_status + cap + 15) / 16 * 16, bytes = o_out + cap * slots * kSlotStride;
+  hipEvent_t ev = b.done;
+  b.done = nullptr;
+  freeBatch(b);
+  b.done = ev;
+  void* p = nullptr;
+  if (ugo_fec_host_alloc(bytes, &p) != UGO_FEC_OK) return false;
+  if (!b.done) {
+    DevGuard g(device_);
+    if (hipEventCreateWithFlags(&b.done, hipEventDisableTiming) != hipSuccess) {
+      ugo_fec_host_free(p);
+      b.done = nullptr;
+      return false;
+    }
+  }
+  b.mem = static_cast<uint8_t*>(p);
+  b.cap = cap;
+  b.rows = reinterpret_cast<uint64_t*>(b.mem + o_rows);
+  b.masks = reinterpret_cast<uint64_t*>(b.mem + o_masks);
+  b.status = reinterpret_cast<int8_t*>(b.mem + o_status);
+  b.out = b.mem + o_out;
+  return true;
+}
+
+// Record one recoverable group: the first d present rows (the survivors
+// Reconstruct uses; input keeps only data shards, :203-207, so the rows left
+// out are parity rows a data-only recovery never rebuilds) by their slots'
+// device addresses.  False if a survivor's slot is not GPU-visible.
+bool FEC::stage(Batch& b, const std::vector<PoolBuf*>& shards, size_t maxlen) {
+  const size_t n = static_cast<size_t>(shardSize_);
+  uint64_t* row = b.rows + b.groups * n;
+  uint64_t mask = 0;
+  int kept = 0;
+  for (size_t k = 0; k < n && kept < dataShards_; ++k)
+    if (shards[k] && !slotDev_[shards[k]->slot]) return false;
+  for (size_t k = 0; k < n; ++k) {
+    row[k] = 0;
+    if (shards[k] && kept < dataShards_) {
+      const uint32_t s = shards[k]->slot;
+      row[k] = slotDev_[s];  // shards[k][:maxlen], read in place
+      mask |= 1ull << k;
+      ++kept;
+      if (!slotHeld_[s]) {
+        slotHeld_[s] = 1;
+        b.held.push_back(s);
       }
     }
-    if (batchBuf_) {
-      batchS_ = maxlen;
-      batchPitch_ = pitch;
-      uint8_t* grp = batchBuf_ + pendMask_.size() * n * pitch;
-      // Only the survivors Reconstruct uses -- the first d present rows -- are
-      // staged: the present data rows all come first, so the rows left out are
-      // parity rows, which a data-only recovery never rebuilds.  Same result,
-      // fewer bytes copied.
-      uint64_t mask = 0;
-      int kept = 0;
-      for (size_t k = 0; k < n && kept < dataShards_; ++k)
-        if (shards[k]) {
-          std::memcpy(grp + k * pitch, shards[k]->data(), maxlen);  // shards[k][:maxlen]
-          mask |= 1ull << k;
-          ++kept;
+  }
+  b.masks[b.groups] = mask;
+  b.S = maxlen;
+  ++b.groups;
+  return true;
+}
+
+bool FEC::launch(Batch& b) {
+  DevGuard g(device_);
+  int st = ugo_fec_reconstruct_rows(enc_->handle(), reinterpret_cast<const uint8_t* const*>(b.rows), b.masks,
+                                    b.groups, b.S, b.out, kSlotStride, outSlots() * kSlotStride,
+                                    UGO_FEC_RECONSTRUCT_DATA_ONLY, b.status, stream_);
+  if (st == UGO_FEC_OK && hipEventRecord(b.done, stream_) != hipSuccess) st = UGO_FEC_ERR_HIP;
+  lastError_ = st;
+  b.err = st;
+  b.inflight = true;  // collect() waits (if launched) and releases the slots either way
+  return st == UGO_FEC_OK;
+}
+
+// Wait for a launched batch and append its recovered data shards, group by
+// group, each group's erased data rows in index order.  A group whose status
+// is not OK yields nothing, as a failing per-call Reconstruct does (:208-210).
+void FEC::collect(Batch& b, std::vector<Bytes>& out) {
+  if (!b.inflight) return;
+  const bool ok = b.err == UGO_FEC_OK && hipEventSynchronize(b.done) == hipSuccess;
+  if (!ok) lastError_ = b.err ? b.err : UGO_FEC_ERR_HIP;
+  const size_t d = static_cast<size_t>(dataShards_);
+  if (ok) {
+    for (size_t g = 0; g < b.groups; ++g) {
+      if (b.status[g] != 0) continue;
+      const uint8_t* grp = b.out + g * outSlots() * kSlotStride;
+      size_t i = 0;
+      for (size_t k = 0; k < d; ++k)
+        if (!((b.masks[g] >> k) & 1ull)) {
+          out.emplace_back(grp + i * kSlotStride, grp + i * kSlotStride + b.S);
+          ++i;
         }
-      pendMask_.push_back(mask);
-      if (pendMask_.size() == static_cast<size_t>(batchCap_)) flushInto(out);
+    }
+  }
+  for (uint32_t s : b.held) releaseSlot(s);
+  b.held.clear();
+  b.groups = 0;
+  b.inflight = false;
+}
+
+// The filled current batch: launched and (flags 0) collected now, or
+// (kBatchOverlap) left running while the previous one is collected.
+void FEC::launchCurrent(std::vector<Bytes>& out) {
+  Batch& b = batch_[cur_];
+  if (b.groups == 0) return;
+  if (!(batchFlags_ & kBatchOverlap)) {
+    launch(b);
+    collect(b, out);
+    return;
+  }
+  Batch& prev = batch_[cur_ ^ 1];
+  collect(prev, out);  // older shards first
+  launch(b);
+  cur_ ^= 1;
+}
+
+// The recoverable branch of input (ugo/fec.go:196-217): reslice to maxlen,
+// Reconstruct (:202, on the GPU), append the erased data shards in index
+// order (:203-207).  Per call: a one-group launch over the pool slots, waited
+// for here.  Batched: the group joins the current batch.
+void FEC::recoverGroup(const std::vector<PoolBuf*>& shards, size_t maxlen, std::vector<Bytes>& out) {
+  if (ensureGpu()) {
+    if (batchCap_ > 0) {
+      Batch& b = batch_[cur_];
+      if (b.groups && maxlen != b.S) launchCurrent(out);  // one shard size per batch
+      Batch& c = batch_[cur_];
+      if (stage(c, shards, maxlen)) {
+        if (c.groups == static_cast<size_t>(batchCap_)) launchCurrent(out);
+        return;
+      }
+      flushInto(out);  // the copy path below returns at once: pending groups first, in order
+    } else if (ensureBatch(batch_[0], 1) && batch_[0].groups == 0 && stage(batch_[0], shards, maxlen)) {
+      launch(batch_[0]);
+      collect(batch_[0], out);
       return;
     }
-    lastError_ = UGO_FEC_ERR_HIP;  // no pinned batch: recover this group per call
   }
-  // :202 Reconstruct, of which input keeps the data shards (:203-207): the
-  // data-only form over the first d present rows gives those same bytes
+  // no GPU-visible pool slot (pinned memory ran out) or no stream: this group
+  // through the encoder's own staging -- the data-only form over the first d
+  // present rows gives the same bytes as Reconstruct's data rows
   std::vector<Bytes> rs(shardSize_);
   int kept = 0;
   for (int k = 0; k < shardSize_ && kept < dataShards_; ++k)
     if (shards[k]) {
-      rs[k].assign(shards[k]->begin(), shards[k]->begin() + maxlen);  // shards[k][:maxlen]
+      const uint8_t* src = slotPtr_[shards[k]->slot];
+      rs[k].assign(src, src + maxlen);  // shards[k][:maxlen]
       ++kept;
     }
   const int err = enc_->ReconstructData(rs);  // -> GPU
@@ -209,26 +405,14 @@ void FEC::recoverGroup(const std::vector<Bytes*>& shards, size_t maxlen, std::ve
   }  // else: logged and swallowed upstream (:208-210)
 }
 
-// One launch over the pending groups (data rows only: input returns data
-// shards, :203-207).  A group whose status is not OK yields nothing, as a
-// failing per-call Reconstruct does.
 void FEC::flushInto(std::vector<Bytes>& out) {
-  const size_t G = pendMask_.size();
-  if (G == 0) return;
-  const size_t n = static_cast<size_t>(shardSize_);
-  std::vector<int8_t> st(G, 0);
-  const int err = enc_->ReconstructBatch(batchBuf_, pendMask_.data(), G, batchS_, batchPitch_,
-                                         UGO_FEC_RECONSTRUCT_DATA_ONLY, st.data());
-  lastError_ = err;
-  if (err != UGO_FEC_ERR_HIP) {
-    for (size_t g = 0; g < G; ++g) {
-      if (st[g] != 0) continue;
-      const uint8_t* grp = batchBuf_ + g * n * batchPitch_;
-      for (int k = 0; k < dataShards_; ++k)
-        if (!((pendMask_[g] >> k) & 1ull)) out.emplace_back(grp + k * batchPitch_, grp + k * batchPitch_ + batchS_);
-    }
+  Batch& prev = batch_[cur_ ^ 1];
+  collect(prev, out);  // an overlapped batch still running: older shards first
+  Batch& b = batch_[cur_];
+  if (b.groups) {
+    launch(b);
+    collect(b, out);
   }
-  pendMask_.clear();
 }
 
 std::vector<Bytes> FEC::flush() {
@@ -237,20 +421,54 @@ std::vector<Bytes> FEC::flush() {
   return out;
 }
 
-std::vector<Bytes> FEC::setBatch(int groups) {
+size_t FEC::pending() const {
+  return batch_[0].groups + batch_[1].groups;
+}
+
+size_t FEC::maxReturnGroups(bool isFlush) const {
+  const size_t cap = static_cast<size_t>(batchCap_);
+  if (cap == 0) return isFlush ? 0 : 1;
+  // overlap: the previous batch (input), or the previous and the current (flush)
+  if (batchFlags_ & kBatchOverlap) return isFlush ? 2 * cap : cap;
+  return cap;
+}
+
+std::vector<Bytes> FEC::setBatch(int groups, unsigned flags) {
   std::vector<Bytes> out;
-  if (groups < 0 || (groups > 0 && shardSize_ > 64)) {
+  if (groups < 0 || (groups > 0 && shardSize_ > 64) || (flags & ~kBatchOverlap)) {
     lastError_ = UGO_FEC_ERR_INVALID_ARG;
     return out;
   }
   flushInto(out);
-  batchCap_ = groups;
   lastError_ = UGO_FEC_OK;
+  if (groups > 0) {
+    if (!ensureGpu() || !ensureBatch(batch_[0], size_t(groups)) ||
+        ((flags & kBatchOverlap) && !ensureBatch(batch_[1], size_t(groups)))) {
+      lastError_ = UGO_FEC_ERR_HIP;
+      return out;
+    }
+  }
+  batchCap_ = groups;
+  batchFlags_ = groups > 0 ? flags : 0;
+  cur_ = 0;
   return out;
 }
 
 FEC::~FEC() {
-  if (batchBuf_) ugo_fec_host_free(batchBuf_);
+  for (Batch& b : batch_) {
+    if (b.inflight && b.done) (void)hipEventSynchronize(b.done);
+    freeBatch(b);
+  }
+  if (stream_) {
+    DevGuard g(device_);
+    (void)hipStreamDestroy(stream_);
+  }
+  for (size_t i = 0; i < slabs_.size(); ++i) {
+    if (slabPinned_[i])
+      ugo_fec_host_free(slabs_[i]);
+    else
+      std::free(slabs_[i]);
+  }
 }
 
 std::vector<Bytes*> FEC::calcECC(std::vector<Bytes>& data, int offset, int maxlen) {  // :228-243

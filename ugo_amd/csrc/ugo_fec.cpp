@@ -839,6 +839,89 @@ int ugo_fec_reconstruct(ugo_fec* c, uint8_t* shards, const uint64_t* present, si
                                      stream);
 }
 
+int ugo_fec_reconstruct_rows(ugo_fec* c, const uint8_t* const* rows, const uint64_t* present, size_t groups,
+                             size_t S, uint8_t* out, size_t out_row_stride, size_t out_group_stride, unsigned flags,
+                             int8_t* status, void* stream) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
+  if (groups == 0) return UGO_FEC_OK;
+  if (S > 0xffffffffu || c->n > 64 || !rows || !present || !out) return UGO_FEC_ERR_INVALID_ARG;
+  // output slots per group: p, or with DATA_ONLY min(d, p) (at most that many data rows are erased)
+  const size_t oslots = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? size_t(std::min(c->d, c->p)) : size_t(c->p);
+  if (reinterpret_cast<uintptr_t>(out) % 16 || out_row_stride % 16 || out_group_stride % 16 ||
+      !layout_disjoint(S, out_row_stride, oslots, out_group_stride, groups))
+    return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(rows) || !device_view(present) || !device_view(status) || !device_view(out))
+    return UGO_FEC_ERR_INVALID_ARG;
+  TimerScope ts(c);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const int mode = c->d_table ? 1 : 2;
+  ugo::kern::Batch a = base_batch(c, nullptr, S, Layout{0, 0});
+  a.rows = reinterpret_cast<const uint64_t*>(rows);
+  a.n = static_cast<uint32_t>(c->n);
+  a.out = out;
+  a.ogstride = out_group_stride;
+  a.orstride = out_row_stride;
+  a.present = present;
+  a.status = status;
+  a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
+  a.chunks = static_cast<uint32_t>((S + 15) / 16);
+  size_t per = slice_groups(a.chunks, true);
+  uint8_t* work = nullptr;
+  if (mode == 2) {
+    per = std::min<size_t>(per, 65536);
+    const int st = scratch_alloc(c, std::min(per, groups) * c->desc_stride + 64, s, reinterpret_cast<void**>(&work));
+    if (st) return st;
+  }
+  struct Release {
+    ugo_fec* c;
+    uint8_t* p;
+    hipStream_t s;
+    ~Release() { (void)scratch_free(c, p, s); }
+  } release{c, work, s};
+  for (size_t g0 = 0; g0 < groups; g0 += per) {
+    const size_t gn = std::min(per, groups - g0);
+    a.g0 = g0;
+    a.items = static_cast<uint32_t>(gn * a.chunks);
+    if (mode == 1) {
+      a.desc = c->d_table;
+    } else {
+      ugo::kern::Prep pr{};
+      pr.desc = work;
+      pr.present = present;
+      pr.M = c->d_M;
+      pr.gf_exp = c->d_gf;
+      pr.gf_log = c->d_gf + 512;
+      pr.g0 = g0;
+      pr.g_desc0 = g0;
+      pr.nmask = a.nmask;
+      pr.desc_stride = c->desc_stride;
+      pr.d = static_cast<uint32_t>(c->d);
+      pr.n = static_cast<uint32_t>(c->n);
+      pr.dpad = c->dpad;
+      pr.epad = c->epad;
+      if (ugo::kern::launch_prepare(pr, static_cast<uint32_t>(gn), s) != hipSuccess) return UGO_FEC_ERR_HIP;
+      a.desc = work;
+      a.g_desc0 = g0;
+    }
+    if (ugo::kern::launch_apply_rows(mode, a, s) != hipSuccess) return UGO_FEC_ERR_HIP;
+  }
+  return UGO_FEC_OK;
+}
+
+int ugo_fec_device_address(const ugo_fec* c, const void* p, void** dev) {
+  if (!c || !dev) return UGO_FEC_ERR_INVALID_ARG;
+  *dev = nullptr;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  const uint8_t* q = static_cast<const uint8_t*>(p);
+  if (!q || !device_view(q)) return UGO_FEC_ERR_INVALID_ARG;
+  *dev = const_cast<uint8_t*>(q);
+  return UGO_FEC_OK;
+}
+
 int ugo_fec_encode_host(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
   if (pitch < S) return S == 0 ? UGO_FEC_ERR_SHARD_NO_DATA : UGO_FEC_ERR_INVALID_ARG;

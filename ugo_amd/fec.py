@@ -135,6 +135,8 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_rc4_keystream.argtypes = [vp, sz, vp, sz]
     lib.ugo_fec_tx_assemble.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp, vp]
     lib.ugo_fec_packet_decode.argtypes = [vp, vp, sz, vp, sz, vp, u, vp, vp, sz, vp, sz, vp]
+    lib.ugo_fec_reconstruct_rows.argtypes = [vp, vp, vp, sz, sz, vp, sz, sz, u, vp, vp]
+    lib.ugo_fec_device_address.argtypes = [vp, vp, ctypes.POINTER(vp)]
     lib.ugo_fec_timing_begin.argtypes = [vp, sz]
     lib.ugo_fec_timing_end.argtypes = [vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     _lib = lib
@@ -277,6 +279,39 @@ class Encoder:
                                                        out.data_ptr(), ors, ogs,
                                                        RECONSTRUCT_DATA_ONLY if data_only else 0, st,
                                                        _stream_handle(stream)))
+
+    def reconstruct_rows(self, rows, present, out, shard_size: int, data_only=False, status=None, stream=None,
+                         out_shard_major: bool = True):
+        """Reconstruct from a row-pointer table (include/ugo_fec.h
+        ugo_fec_reconstruct_rows): rows = int64 tensor [G, d+p] of device
+        addresses (device tensor, or pinned host memory as a numpy array /
+        CPU tensor viewed through ugo_fec_device_address), present = [G] masks
+        (device tensor or pinned numpy array), out = contiguous uint8 CUDA
+        tensor [p][G][opitch] (out_shard_major) or [G][p][opitch]."""
+        G = present.shape[0]
+        _require(rows.shape[0] == G and rows.shape[1] == self.Shards and self.Shards <= 64)
+        p = self.ParityShards
+        _require(out.dim() == 3 and out.is_contiguous() and out.element_size() == 1)
+        if out_shard_major:
+            _require(out.shape[0] == p and out.shape[1] == G)
+            ors, ogs = G * out.shape[2], out.shape[2]
+        else:
+            _require(out.shape[0] == G and out.shape[1] == p)
+            ors, ogs = out.shape[2], p * out.shape[2]
+        _require(out.shape[2] >= shard_size)
+
+        def ptr(x):
+            return None if x is None else (x.ctypes.data if isinstance(x, np.ndarray) else x.data_ptr())
+
+        _raise(load_library().ugo_fec_reconstruct_rows(self._h, ptr(rows), ptr(present), G, shard_size, ptr(out),
+                                                       ors, ogs, RECONSTRUCT_DATA_ONLY if data_only else 0,
+                                                       ptr(status), _stream_handle(stream)))
+
+    def device_address(self, addr: int) -> int:
+        """ugo_fec_device_address: the device address of host/device pointer addr."""
+        out = ctypes.c_void_p()
+        _raise(load_library().ugo_fec_device_address(self._h, ctypes.c_void_p(addr), ctypes.byref(out)))
+        return out.value or 0
 
     def rx_assemble(self, wire, lens, shards, present, first_group: int = 0, shard_size: Optional[int] = None,
                     pad=None, stats=None, stream=None, shard_major: bool = True):
@@ -476,6 +511,7 @@ def _bind_conn(lib):
     lib.ugo_fecconn_calc_ecc.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(sz), i, i, i]
     lib.ugo_fecconn_rx_len.argtypes = [vp, ctypes.POINTER(sz)]
     lib.ugo_fecconn_set_batch.argtypes = [vp, i, vp, sz, ctypes.POINTER(i), ctypes.POINTER(sz)]
+    lib.ugo_fecconn_set_batch_ex.argtypes = [vp, i, ctypes.c_uint, vp, sz, ctypes.POINTER(i), ctypes.POINTER(sz)]
     lib.ugo_fecconn_flush.argtypes = [vp, vp, sz, ctypes.POINTER(i), ctypes.POINTER(sz)]
     lib.ugo_fecconn_pending.argtypes = [vp, ctypes.POINTER(sz)]
     lib._conn_bound = True
@@ -546,17 +582,20 @@ class FecConn:
                                            ctypes.byref(nrec), ctypes.byref(rlen)))
         return seq.value, flag.value, self._recovered(nrec, rlen)
 
-    def set_batch(self, groups: int):
+    def set_batch(self, groups: int, overlap: bool = False):
         """Batched recovery (include/ugo_fec_conn.h): recoverable lossy groups are
-        recovered `groups` at a time in one launch; 0 = per call.  Returns the
-        recovered shards of groups that were pending (list | None)."""
+        recovered `groups` at a time in one launch; 0 = per call.  overlap: the
+        launch runs while input goes on, its shards come back one batch later
+        (UGO_FECCONN_BATCH_OVERLAP).  Returns the recovered shards of groups that
+        were pending (list | None)."""
         nrec, rlen = ctypes.c_int(), ctypes.c_size_t()
-        need = max(groups, 1) * self.dataShards * UGO_FEC_MAX_PACKET
+        need = max(groups, 1) * (2 if overlap else 1) * self.dataShards * UGO_FEC_MAX_PACKET
         new_out = (ctypes.c_uint8 * max(need, len(self._out)))()
         old_out, self._out = self._out, new_out
         try:
-            _raise(self._lib.ugo_fecconn_set_batch(self._h, groups, ctypes.addressof(self._out), len(self._out),
-                                                   ctypes.byref(nrec), ctypes.byref(rlen)))
+            _raise(self._lib.ugo_fecconn_set_batch_ex(self._h, groups, 1 if overlap else 0,
+                                                      ctypes.addressof(self._out), len(self._out),
+                                                      ctypes.byref(nrec), ctypes.byref(rlen)))
         except Exception:
             self._out = old_out
             raise
