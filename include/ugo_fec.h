@@ -145,9 +145,12 @@ int ugo_fec_reconstruct_into(ugo_fec* ctx, const uint8_t* shards, const uint64_t
  * (Encoder.Reconstruct, ugo/fec.go:202, with erased shards nil and filled in
  * fresh buffers): output i of group g -- the i-th erased row, ascending --
  * goes to out + g*out_group_stride + i*out_row_stride, i < p (DATA_ONLY:
- * i < min(d, p), the most data rows a recoverable group can miss).  The survivor rows a
- * group uses must be 16-B aligned and non-null, else that group gets status
- * UGO_FEC_ERR_INVALID_ARG (checked on the device) and is not written.
+ * i < min(d, p), the most data rows a recoverable group can miss).  The
+ * survivor rows a group uses must be 16-B aligned and non-null, else that
+ * group gets status UGO_FEC_ERR_INVALID_ARG (checked on the device) and is
+ * not written; each must be readable for round_up(shard_size, 16) bytes (the
+ * kernel loads whole 16-B chunks; bytes past shard_size never reach an
+ * output, and output bytes past shard_size are not written).
  * `rows`, `present`, `status`, `out`: device or pinned host memory; out
  * 16-B aligned with strides % 16 == 0; d+p <= 64.  Asynchronous on `stream`.
  * rows[] may be overwritten, and the rows it points to reused, only after

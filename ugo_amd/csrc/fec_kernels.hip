@@ -954,37 +954,56 @@ __global__ __launch_bounds__(256) void k_apply_bytes(Batch a) {
 // caller's output batch, output i = the i-th erased row (ascending).  A group
 // whose survivor pointers are not 16-B aligned gets UGO_FEC_ERR_INVALID_ARG
 // and is not touched.  Latency / PCIe-bound: batches of tens of groups.
-__device__ __forceinline__ V4 load_part(const uint8_t* p, uint32_t nb) {
-  if (nb >= 16u) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(p);
-    return V4{{v.x, v.y, v.z, v.w}};
-  }
-  V4 x{{0u, 0u, 0u, 0u}};  // tail chunk: bytes [0, nb), unrolled (a runtime index would put x in scratch)
-#pragma unroll
-  for (int j = 0; j < 16; ++j)
-    if (static_cast<uint32_t>(j) < nb) x.v[j >> 2] |= static_cast<uint32_t>(p[j]) << (8 * (j & 3));
-  return x;
+typedef const __attribute__((address_space(1))) u32x4* gptr16_t;
+
+// One 16-byte chunk of a row (rows are readable in whole 16-B granules: the
+// reconstruct_rows contract), through a global-space pointer (a generic one
+// would make it a flat load).
+__device__ __forceinline__ V4 load_row16(uint64_t p) {
+  const u32x4 v = *(gptr16_t)(p);
+  return V4{{v.x, v.y, v.z, v.w}};
 }
 
 // Wave-aligned groups (item = group * cpad + chunk, cpad = chunks rounded up to
 // 64, as k_apply_qa): everything but the row bytes is wave-uniform and read
-// with scalar loads -- descriptor, row pointers, coefficient tables.  Per-lane
-// reads of those (a wave spanning two groups) chained ~30 dependent vector
-// loads per lane and cost 28 us for one group against 6 us for the batch
-// kernel on a staged copy (rocprofv3, profiles/r3/).
+// with scalar loads -- descriptor, row pointers, coefficient tables.  The
+// kernel is latency-bound (tens of groups per launch, rows over PCIe), so its
+// code is kept small: outputs in a rolled loop, one accumulator, the
+// survivors' selectors recomputed per output.  Fully unrolled over 16 inputs
+// x 8 outputs (10 K instructions) it took 14 us for ONE group even with
+// every buffer in HBM: cold instruction fetch, not memory (tools/rows_probe.py,
+// profiles/r3/rows_probe.jsonl).
 typedef const __attribute__((address_space(4))) uint64_t* ctab64_t;
+
+// acc ^= sum over the block's inputs j of c(i, k0 + j) * x[j]
+template <int NB>
+__device__ __forceinline__ void rows_fold(V4& acc, const V4* x, const Batch& a, uint64_t dU, uint32_t coff_i,
+                                          uint32_t k0) {
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    if (k0 + j >= a.d) continue;
+    uint32_t s0[4], s1[4], s2[4];
+    p_sel(x[j], s0, s1, s2);
+    const uint32_t o = coff_i + k0 + j;
+    const uint32_t cf = (*(ctab_t)(dU + (o & ~3u)) >> (8u * (o & 3u))) & 0xffu;
+    const ctab_t t = (ctab_t)(a.mult) + 8u * cf;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      acc.v[w] = xor3(acc.v[w], perm(t[1], t[0], s0[w]), perm(t[3], t[2], s1[w])) ^ perm(0u, t[4], s2[w]);
+  }
+}
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_apply_rows(Batch a) {
+  constexpr int NB = 16;  // inputs per block (d <= 16: one block, loaded once)
   const uint32_t cpad = (a.chunks + 63u) & ~63u;
   const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
   if (wfirst >= a.items) return;  // a.items = groups * cpad
   const uint32_t gl = __builtin_amdgcn_readfirstlane(wfirst / cpad);
   const uint64_t g = a.g0 + gl;
   const uint64_t dU = rfl64(reinterpret_cast<uint64_t>(desc_for<MODE>(a, g)));
-  auto dword = [&](uint32_t off) -> uint32_t { return *(ctab_t)(dU + off); };
-  auto dbyte = [&](uint32_t off) -> uint32_t { return (dword(off & ~3u) >> (8u * (off & 3u))) & 0xffu; };
-  const uint32_t hdr = dword(0);
+  auto dbyte = [&](uint32_t off) -> uint32_t { return (*(ctab_t)(dU + (off & ~3u)) >> (8u * (off & 3u))) & 0xffu; };
+  const uint32_t hdr = *(ctab_t)(dU);
   const uint32_t st = (hdr >> 16) & 0xffu;
   const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
   const uint32_t c = blockIdx.x * 256u + threadIdx.x - gl * cpad;
@@ -994,56 +1013,41 @@ __global__ __launch_bounds__(256) void k_apply_rows(Batch a) {
     if (wst) a.status[g] = static_cast<int8_t>(st);
     return;
   }
-  const uint64_t rpU = reinterpret_cast<uint64_t>(a.rows + g * a.n);  // the group's row pointers
+  const ctab64_t rp = (ctab64_t)(a.rows + g * a.n);  // the group's row pointers (scalar loads)
+  // every survivor pointer checked before anything is read or written: a null
+  // or misaligned one fails the group (UGO_FEC_ERR_INVALID_ARG, 6), untouched
+  uint64_t bad = 0;
+  for (uint32_t k = 0; k < a.d; ++k) {
+    const uint64_t q = rp[dbyte(4 + k)];
+    bad |= (q & 15u) | (q == 0);
+  }
+  if (bad) {
+    if (wst) a.status[g] = 6;
+    return;
+  }
   const uint32_t cbase = 4 + a.dpad + a.epad;
   const uint32_t off = live ? c * 16u : 0u;
   const uint32_t nb = live ? min(16u, a.S - off) : 16u;
-  // Survivors in blocks of 16: the block's pointers (scalar loads, over PCIe
-  // when the table is pinned host memory) checked, then its 16 row loads
-  // issued together.  A null or misaligned pointer is never dereferenced: the
-  // group gets UGO_FEC_ERR_INVALID_ARG and writes nothing.
-  bool bad = false;
-  for (uint32_t i0 = 0; i0 < e; i0 += 8u) {
-    V4 acc[8];
+  auto load_block = [&](V4* x, uint32_t k0) {  // the block's row loads, issued together
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
-    for (uint32_t k0 = 0; k0 < a.d; k0 += 16u) {
-      uint64_t ptr[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) ptr[j] = (k0 + j < a.d) ? *((ctab64_t)rpU + dbyte(4 + k0 + j)) : 16u;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) bad |= (ptr[j] & 15u) != 0 || ptr[j] == 0;
-      if (bad) break;  // wave-uniform
-      V4 x[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        x[j] = (k0 + j < a.d) ? load_part(reinterpret_cast<const uint8_t*>(ptr[j]) + off, nb)
-                              : V4{{0u, 0u, 0u, 0u}};
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        if (k0 + j >= a.d) continue;
-        uint32_t s0[4], s1[4], s2[4];
-        p_sel(x[j], s0, s1, s2);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (i0 + i >= e) continue;
-          const ctab_t t = (ctab_t)(a.mult) + 8u * dbyte(cbase + (i0 + i) * a.dpad + k0 + j);
-#pragma unroll
-          for (int w = 0; w < 4; ++w)
-            acc[i].v[w] = xor3(acc[i].v[w], perm(t[1], t[0], s0[w]), perm(t[3], t[2], s1[w])) ^ perm(0u, t[4], s2[w]);
-        }
+    for (int j = 0; j < NB; ++j)
+      x[j] = (k0 + j < a.d) ? load_row16(rp[dbyte(4 + k0 + j)] + off) : V4{{0u, 0u, 0u, 0u}};
+  };
+  V4 x[NB];
+  if (a.d <= static_cast<uint32_t>(NB)) load_block(x, 0);
+  for (uint32_t i = 0; i < e; ++i) {
+    V4 acc{{0u, 0u, 0u, 0u}};
+    if (a.d <= static_cast<uint32_t>(NB)) {
+      rows_fold<NB>(acc, x, a, dU, cbase + i * a.dpad, 0);
+    } else {
+      for (uint32_t k0 = 0; k0 < a.d; k0 += NB) {  // wide codes: the rows re-read per output
+        load_block(x, k0);
+        rows_fold<NB>(acc, x, a, dU, cbase + i * a.dpad, k0);
       }
     }
-    if (bad) break;
-    if (live) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if (i0 + i >= e) continue;
-        store16<0>(a.out + g * a.ogstride + static_cast<uint64_t>(i0 + i) * a.orstride + off, acc[i], nb);
-      }
-    }
+    if (live) store16<0>(a.out + g * a.ogstride + static_cast<uint64_t>(i) * a.orstride + off, acc, nb);
   }
-  if (wst) a.status[g] = static_cast<int8_t>(bad ? 6 : 0);  // 6: UGO_FEC_ERR_INVALID_ARG
+  if (wst) a.status[g] = 0;
 }
 
 // ------------------------------------------------------------- k_prepare
@@ -1358,10 +1362,13 @@ static bool launch_apply_stream(const Batch& a, hipStream_t s) {
     Batch b = a;
     b.items = (a.items / a.chunks) * cpad;
     const dim3 ga(blocks_for(b.items, 256));
+    // k_apply_qb: k_apply_qa with its per-product overhead cut (uniform
+    // descriptor in SGPRs, saddr loads, unrolled ring): jumbo reconstruct
+    // 524.0 vs 535.5 us (profiles/r3/qaprobe_r3e.jsonl)
     if (a.epad == 4)
-      launch(apply_kid<MODE>(), k_apply_qa<4, MODE, kApplyQNT>, ga, block, 0, s, b);
+      launch(apply_kid<MODE>(), k_apply_qb<4, MODE, kApplyQNT, 7>, ga, block, 0, s, b);
     else
-      launch(apply_kid<MODE>(), k_apply_qa<8, MODE, kApplyQNT>, ga, block, 0, s, b);
+      launch(apply_kid<MODE>(), k_apply_qb<8, MODE, kApplyQNT, 7>, ga, block, 0, s, b);
     return true;
   }
   const dim3 grid(blocks_for(a.items, 256));

@@ -367,8 +367,8 @@ void FEC::launchCurrent(std::vector<Bytes>& out) {
 
 // The recoverable branch of input (ugo/fec.go:196-217): reslice to maxlen,
 // Reconstruct (:202, on the GPU), append the erased data shards in index
-// order (:203-207).  Per call: a one-group launch over the pool slots, waited
-// for here.  Batched: the group joins the current batch.
+// order (:203-207).  Per call: recoverOne.  Batched: the group joins the
+// current batch, its survivors read in place.
 void FEC::recoverGroup(const std::vector<PoolBuf*>& shards, size_t maxlen, std::vector<Bytes>& out) {
   if (ensureGpu()) {
     if (batchCap_ > 0) {
@@ -380,9 +380,7 @@ void FEC::recoverGroup(const std::vector<PoolBuf*>& shards, size_t maxlen, std::
         return;
       }
       flushInto(out);  // the copy path below returns at once: pending groups first, in order
-    } else if (ensureBatch(batch_[0], 1) && batch_[0].groups == 0 && stage(batch_[0], shards, maxlen)) {
-      launch(batch_[0]);
-      collect(batch_[0], out);
+    } else if (recoverOne(shards, maxlen, out)) {
       return;
     }
   }
@@ -403,6 +401,41 @@ void FEC::recoverGroup(const std::vector<PoolBuf*>& shards, size_t maxlen, std::
     for (int k = 0; k < dataShards_; ++k)
       if (!shards[k]) out.push_back(std::move(rs[k]));
   }  // else: logged and swallowed upstream (:208-210)
+}
+
+// Per call: the survivors are copied into a pinned one-group stage and
+// recovered zero-copy (ugo_fec_reconstruct_host), waited for here.  For a
+// single group this beats reading them in place (ugo_fec_reconstruct_rows):
+// 7.3 vs 12.2 us of kernel, the extra row-pointer round trip over PCIe and the
+// larger kernel outweighing the 15 KB copy (profiles/r3/rows_probe2.jsonl).
+bool FEC::recoverOne(const std::vector<PoolBuf*>& shards, size_t maxlen, std::vector<Bytes>& out) {
+  const size_t n = static_cast<size_t>(shardSize_);
+  const size_t pitch = (maxlen + 15) / 16 * 16;
+  if (!one_ || oneBytes_ < n * pitch) {
+    if (one_) ugo_fec_host_free(one_);
+    one_ = nullptr;
+    oneBytes_ = 0;
+    void* p = nullptr;
+    if (ugo_fec_host_alloc(n * pitch, &p) != UGO_FEC_OK) return false;
+    one_ = static_cast<uint8_t*>(p);
+    oneBytes_ = n * pitch;
+  }
+  uint64_t mask = 0;
+  int kept = 0;
+  for (size_t k = 0; k < n && kept < dataShards_; ++k)
+    if (shards[k]) {
+      std::memcpy(one_ + k * pitch, slotPtr_[shards[k]->slot], maxlen);  // shards[k][:maxlen]
+      mask |= 1ull << k;
+      ++kept;
+    }
+  int8_t status = 0;
+  const int err = ugo_fec_reconstruct_host(enc_->handle(), one_, &mask, 1, maxlen, pitch,
+                                           UGO_FEC_RECONSTRUCT_DATA_ONLY, &status);  // :202 -> GPU
+  lastError_ = err;
+  if (err == UGO_FEC_OK)
+    for (int k = 0; k < dataShards_; ++k)
+      if (!shards[k]) out.emplace_back(one_ + k * pitch, one_ + k * pitch + maxlen);
+  return err != UGO_FEC_ERR_HIP;  // a failing Reconstruct is logged and swallowed upstream (:208-210)
 }
 
 void FEC::flushInto(std::vector<Bytes>& out) {
@@ -455,6 +488,7 @@ std::vector<Bytes> FEC::setBatch(int groups, unsigned flags) {
 }
 
 FEC::~FEC() {
+  if (one_) ugo_fec_host_free(one_);
   for (Batch& b : batch_) {
     if (b.inflight && b.done) (void)hipEventSynchronize(b.done);
     freeBatch(b);

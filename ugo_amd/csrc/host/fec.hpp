@@ -139,6 +139,7 @@ class FEC {
   bool ensureBatch(Batch& b, size_t cap);
   void freeBatch(Batch& b);
   void recoverGroup(const std::vector<PoolBuf*>& shards, size_t maxlen, std::vector<Bytes>& out);
+  bool recoverOne(const std::vector<PoolBuf*>& shards, size_t maxlen, std::vector<Bytes>& out);
   bool stage(Batch& b, const std::vector<PoolBuf*>& shards, size_t maxlen);
   bool launch(Batch& b);
   void collect(Batch& b, std::vector<Bytes>& out);
@@ -167,8 +168,11 @@ class FEC {
   std::vector<uint32_t> slotFree_;
   std::function<uint32_t()> clock_;
   int lastError_ = 0;
-  // recovery on the GPU: one stream; per-call recovery uses batch_[0] (1 group)
+  // recovery on the GPU: one stream for the batches; per call a pinned
+  // one-group stage (recoverOne)
   hipStream_t stream_ = nullptr;
+  uint8_t* one_ = nullptr;
+  size_t oneBytes_ = 0;
   int batchCap_ = 0;
   unsigned batchFlags_ = 0;
   Batch batch_[2];

@@ -226,13 +226,26 @@ __global__ __launch_bounds__(256) void k_tx_var(TxArgs a) {
 
 }  // namespace
 
-// Residency cap for the (10,3) TX kernel: dynamic LDS it never touches (79 KiB
-// per block) limits it to 2 blocks (8 waves) per CU.  Fewer requests in flight
-// run its 10-read + 13-write stream mix faster on a cold ring: 450.7 us at 2
-// blocks/CU, 464.6 at 3, 493.3 at its natural (VGPR-limited) occupancy, 567.5
-// at 1 (tools/txvariants.hip, profiles/r2/txvariants_cold_occupancy.jsonl; that
-// file's labels read one block high: 'N blocks/CU' there ran N - 1).
-constexpr uint32_t kTxLdsCap = 79u * 1024u;
+// Residency cap for the (10,3) TX kernel: dynamic LDS it never touches limits
+// it to 2 blocks (8 waves) per CU.  Fewer requests in flight run its 10-read +
+// 13-write stream mix faster on a cold ring: 450.7 us at 2 blocks/CU, 464.6 at
+// 3, 493.3 at its natural (VGPR-limited) occupancy, 567.5 at 1
+// (tools/txvariants.hip, profiles/r2/txvariants_cold_occupancy.jsonl).  The
+// cap is sized from the device's LDS per CU (half of it, less 1 KiB: 79 KiB
+// on gfx950's 160 KiB), so it stays 2 blocks whatever the LDS size.  A
+// waves-per-EU attribute only bounds the registers the compiler may use; it
+// does not cap residency.
+static uint32_t tx_lds_cap() {
+  static const uint32_t cap = [] {
+    int dev = 0, lds = 160 * 1024;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
+        lds <= 4096)
+      lds = 160 * 1024;
+    return static_cast<uint32_t>(lds / 2 - 1024);
+  }();
+  return cap;
+}
 
 hipError_t launch_tx_assemble(int dmax, const TxArgs& a, hipStream_t s) {
   const uint64_t items = a.groups * a.chunks;
@@ -243,9 +256,9 @@ hipError_t launch_tx_assemble(int dmax, const TxArgs& a, hipStream_t s) {
       // scalar lengths need a wave to span at most 2 groups: >= 64 chunks per packet
       const bool sl = kTxSL && a.chunks >= 64;
       if (a.d == 10 && a.p == 3 && sl)
-        launch(kKTx, k_tx_c<10, 3, kTxNT, true>, grid, block, kTxLdsCap, s, a);
+        launch(kKTx, k_tx_c<10, 3, kTxNT, true>, grid, block, tx_lds_cap(), s, a);
       else if (a.d == 10 && a.p == 3)
-        launch(kKTx, k_tx_c<10, 3, kTxNT, false>, grid, block, kTxLdsCap, s, a);
+        launch(kKTx, k_tx_c<10, 3, kTxNT, false>, grid, block, tx_lds_cap(), s, a);
       else if (a.d == 32 && a.p == 8 && sl)
         launch(kKTx, k_tx_c<32, 8, kTxNT, true>, grid, block, 0, s, a);
       else if (a.d == 32 && a.p == 8)
