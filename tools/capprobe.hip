@@ -95,6 +95,14 @@ int main(int argc, char** argv) {
     vars.push_back({"dec into k_apply_p, " + std::to_string(bpc) + " blocks/CU", dec_bytes, [&, x](int r) {
       hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), x, 0, roto[r]); }, {}});
   }
+  // the bench step: encode then reconstruct_into of the same batch, each timed
+  // on its own (is a reconstruct right after an encode slower than one after
+  // another reconstruct?)
+  std::vector<float> step_enc, step_dec;
+  hipEvent_t s0, s1, s2;
+  CK(hipEventCreate(&s0));
+  CK(hipEventCreate(&s1));
+  CK(hipEventCreate(&s2));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -102,7 +110,21 @@ int main(int argc, char** argv) {
   for (int w = 0; w < 3; ++w)  // clocks up
     for (auto& v : vars) v.go(cnt++ % nb);
   CK(hipDeviceSynchronize());
-  for (int rd = 0; rd < rounds; ++rd)
+  for (int rd = 0; rd < rounds; ++rd) {
+    {
+      const int r = cnt++ % nb;
+      CK(hipEventRecord(s0));
+      hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[r]);
+      CK(hipEventRecord(s1));
+      hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, roto[r]);
+      CK(hipEventRecord(s2));
+      CK(hipEventSynchronize(s2));
+      float a1 = 0, a2 = 0;
+      CK(hipEventElapsedTime(&a1, s0, s1));
+      CK(hipEventElapsedTime(&a2, s1, s2));
+      step_enc.push_back(a1);
+      step_dec.push_back(a2);
+    }
     for (auto& v : vars) {
       const int r = cnt++ % nb;
       CK(hipEventRecord(e0));
@@ -113,6 +135,13 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       v.t.push_back(ms);
     }
+  }
+  std::sort(step_enc.begin(), step_enc.end());
+  std::sort(step_dec.begin(), step_dec.end());
+  printf("{\"G\": %llu, \"variant\": \"STEP enc (production) then dec into (production) on the same batch\", "
+         "\"enc_median_us\": %.1f, \"dec_median_us\": %.1f, \"enc_TBps\": %.3f, \"dec_TBps\": %.3f}\n",
+         (unsigned long long)G, step_enc[step_enc.size() / 2] * 1e3, step_dec[step_dec.size() / 2] * 1e3,
+         enc_bytes / (step_enc[step_enc.size() / 2] * 1e-3) / 1e12, dec_bytes / (step_dec[step_dec.size() / 2] * 1e-3) / 1e12);
   for (auto& v : vars) {
     std::sort(v.t.begin(), v.t.end());
     const double med = v.t[v.t.size() / 2];
