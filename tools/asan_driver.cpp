@@ -140,7 +140,7 @@ void host_round_trip_wide(int d, int p, size_t S, size_t G, bool pinned) {
 // the FEC object: TX by markData / calcECC / markFEC over reused buffers, RX
 // over a lossy, duplicating channel per call and batched -- same recovered
 // sequence, and every lost full-length payload comes back
-void fec_object(int batch) {
+void fec_object(int batch, unsigned flags = 0) {
   const int d = 10, p = 3, n = 13;
   const size_t L = UGO_FEC_MAX_PACKET;
   ugo_fecconn *tx = nullptr, *rx1 = nullptr, *rx2 = nullptr;
@@ -148,10 +148,10 @@ void fec_object(int batch) {
   EXPECT(ugo_fecconn_new(128, d, p, 0, &rx1) == UGO_FEC_OK);
   EXPECT(ugo_fecconn_new(128, d, p, 0, &rx2) == UGO_FEC_OK);
   if (!tx || !rx1 || !rx2) return;
-  std::vector<uint8_t> out1(size_t(batch + 1) * d * L), out2(size_t(batch + 1) * d * L);
+  std::vector<uint8_t> out1(size_t(batch + 1) * d * L), out2(size_t(2 * batch + 1) * d * L);
   int nrec = 0;
   size_t rl = 0;
-  EXPECT(ugo_fecconn_set_batch(rx2, batch, out2.data(), out2.size(), &nrec, &rl) == UGO_FEC_OK);
+  EXPECT(ugo_fecconn_set_batch_ex(rx2, batch, flags, out2.data(), out2.size(), &nrec, &rl) == UGO_FEC_OK);
   std::vector<std::vector<uint8_t>> grp(n, std::vector<uint8_t>(L));
   std::vector<std::vector<uint8_t>> wire, sent;
   for (int g = 0; g < 40; ++g) {
@@ -258,6 +258,21 @@ void tx_rx_batch() {
     same = std::memcmp(out + g * pitch, pkts + (g * d + k) * slot + 6, S) == 0;
   }
   EXPECT(same);
+  // the same recovery from a row-pointer table over the assembled batch (pinned, read in place)
+  auto* rows = reinterpret_cast<uint64_t*>(pin(G * n * 8));
+  uint8_t* out2 = pin(p * G * pitch);
+  for (size_t g = 0; g < G; ++g)
+    for (int r = 0; r < n; ++r) {
+      void* dv = nullptr;
+      EXPECT(ugo_fec_device_address(ctx, shards + r * G * pitch + g * pitch, &dv) == UGO_FEC_OK);
+      rows[g * n + r] = reinterpret_cast<uint64_t>(dv);
+    }
+  EXPECT(ugo_fec_reconstruct_rows(ctx, reinterpret_cast<const uint8_t* const*>(rows), present, G, S, out2, G * pitch,
+                                  pitch, UGO_FEC_RECONSTRUCT_DATA_ONLY, status, nullptr) == UGO_FEC_OK);
+  EXPECT(hipDeviceSynchronize() == hipSuccess);
+  for (size_t g = 0; g < G; ++g) EXPECT(status[g] == 0 && std::memcmp(out2 + g * pitch, out + g * pitch, S) == 0);
+  ugo_fec_host_free(rows);
+  ugo_fec_host_free(out2);
   for (uint8_t* q : {pkts, wire, reinterpret_cast<uint8_t*>(lens), reinterpret_cast<uint8_t*>(wlens),
                      reinterpret_cast<uint8_t*>(status), pad, ring, reinterpret_cast<uint8_t*>(rlens), shards,
                      reinterpret_cast<uint8_t*>(present), reinterpret_cast<uint8_t*>(stats), out})
@@ -281,6 +296,8 @@ int main() {
   }
   fec_object(1);
   fec_object(16);
+  fec_object(3, UGO_FECCONN_BATCH_OVERLAP);
+  fec_object(16, UGO_FECCONN_BATCH_OVERLAP);
   tx_rx_batch();
   std::printf("{\"asan_driver\": \"%s\", \"failures\": %d}\n", failures ? "FAIL" : "ok", failures);
   return failures ? 1 : 0;
