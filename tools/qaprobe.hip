@@ -115,6 +115,10 @@ int main(int argc, char** argv) {
   vars.push_back({"k_apply_qb OPT 1 (uniform desc)", [=]() { hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 1>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_apply_qb OPT 3 (+ saddr loads; 72 VGPRs, 7 waves/SIMD)", [=]() { hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 3>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_apply_qb OPT 7 (+ unrolled ring; 96 VGPRs, 5 waves/SIMD)", [=]() { hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 7>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+  vars.push_back({"k_apply_ql LDS-DMA ring 8", [=]() { hipLaunchKernelGGL((k_apply_ql<8, 2, 8>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+  vars.push_back({"k_apply_ql LDS-DMA ring 4", [=]() { hipLaunchKernelGGL((k_apply_ql<8, 2, 4>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+  vars.push_back({"MEMORY PATTERN ONLY of k_apply_qb OPT 7 (inputs XORed, no products; wrong bytes)", [=]() {
+    hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 15>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_prepare + k_apply_qa (production reconstruct)", [=]() {
     (void)launch_prepare(pr, G, 0);
     hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
