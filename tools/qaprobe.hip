@@ -7,6 +7,7 @@
 // variant (cdna_hip_programming.md §5.4 rule 24).
 // Usage: qaprobe [groups] [rounds].
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/qaprobe tools/qaprobe.hip
+// Round-3 results: profiles/r3/qaprobe_r3m.jsonl (DESIGN.md §3.4 "Jumbo floor").
 // Not product code: it includes the kernel TU to instantiate the variants.
 #include "../ugo_amd/csrc/fec_kernels.hip"
 
@@ -116,6 +117,7 @@ int main(int argc, char** argv) {
   vars.push_back({"k_apply_qb OPT 3 (+ saddr loads; 72 VGPRs, 7 waves/SIMD)", [=]() { hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 3>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_apply_qb OPT 7 (+ unrolled ring; 96 VGPRs, 5 waves/SIMD)", [=]() { hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 7>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_apply_ql LDS-DMA ring 8", [=]() { hipLaunchKernelGGL((k_apply_ql<8, 2, 8>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+  vars.push_back({"k_apply_ql LDS-DMA ring 8, one pair per iteration", [=]() { hipLaunchKernelGGL((k_apply_ql<8, 2, 8, false>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_apply_ql LDS-DMA ring 4", [=]() { hipLaunchKernelGGL((k_apply_ql<8, 2, 4>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"MEMORY PATTERN ONLY of k_apply_qb OPT 7 (inputs XORed, no products; wrong bytes)", [=]() {
     hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 15>), dim3(ga), dim3(256), 0, 0, aa); }, {}});

@@ -936,7 +936,7 @@ __device__ __forceinline__ void lds_pair(V4& x0, V4& x1, uint32_t ad0, uint32_t 
 // one pair in registers, without spending VGPRs on them.  The input loop is
 // unrolled over R/2 pairs so every slot and every vmcnt is a constant; the
 // last R/2 pairs drain the ring.  Needs d % R == 0 (the (32,8) jumbo code).
-template <int EMAX, int MODE, int R = 8>
+template <int EMAX, int MODE, int R = 8, bool UNROLL = true>
 __global__ __launch_bounds__(256) void k_apply_ql(Batch a) {
   static_assert(R % 2 == 0 && R >= 4 && R <= 12, "ring of 4..12 slots");
   __shared__ u32x4 stage[4][R][64];
@@ -963,7 +963,7 @@ __global__ __launch_bounds__(256) void k_apply_ql(Batch a) {
   const uint32_t sbase = lds_addr(&stage[w][0][0]);     // wave-uniform: M0 of a slot's DMA
   const uint32_t lbase = lds_addr(&stage[w][0][lane]);  // this lane's 16 B of slot 0
   uint32_t tok = 0;
-  auto dma = [&](uint32_t k, int slot) {  // input k into a slot
+  auto dma = [&](uint32_t k, uint32_t slot) {  // input k into a slot
     const uint32_t r = (dword(4 + (k & ~3u)) >> (8 * (k & 3u))) & 0xffu;
     uint32_t co = coff;
     asm("" : "+v"(co));
@@ -981,14 +981,16 @@ __global__ __launch_bounds__(256) void k_apply_ql(Batch a) {
     for (int i = 0; i < EMAX; ++i) {
       if (i >= static_cast<int>(e)) continue;
       const uint32_t off = cbase + i * a.dpad + (k & ~3u);
-      const uint32_t cw = dword(off);
-      const ctab_t tA = (ctab_t)(a.mult) + 8u * ((cw >> (8 * (k & 3u))) & 0xffu);
-      const ctab_t tB = (ctab_t)(a.mult) + 8u * ((cw >> (8 * ((k + 1) & 3u))) & 0xffu);
       uint32_t t[5], u[5];
+      {
+        const ctab_t tA = (ctab_t)(a.mult) + 8u * ((dword(off) >> (8 * (k & 3u))) & 0xffu);
 #pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        t[q] = tA[q];
-        u[q] = tB[q];
+        for (int q = 0; q < 5; ++q) t[q] = tA[q];
+      }
+      {
+        const ctab_t tB = (ctab_t)(a.mult) + 8u * ((dword(off) >> (8 * ((k + 1) & 3u))) & 0xffu);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) u[q] = tB[q];
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1001,19 +1003,38 @@ __global__ __launch_bounds__(256) void k_apply_ql(Batch a) {
 #pragma unroll
   for (int j = 0; j < R; ++j) dma(j, j);  // prime the ring
   uint32_t k0 = 0;
-  for (; k0 + R < a.d; k0 += R) {  // steady state: a pair read, its slots refilled R inputs ahead
+  if constexpr (UNROLL) {
+    for (; k0 + R < a.d; k0 += R) {  // steady state: a pair read, its slots refilled R inputs ahead
 #pragma unroll
-    for (int j = 0; j < R; j += 2) {
-      V4 x0, x1;
-      lds_pair<R - 2>(x0, x1, lbase + 1024u * j, lbase + 1024u * (j + 1), tok);
-      dma(k0 + R + j, j);
-      dma(k0 + R + j + 1, j + 1);
-      fold(k0 + j, x0, x1);
+      for (int j = 0; j < R; j += 2) {
+        V4 x0, x1;
+        lds_pair<R - 2>(x0, x1, lbase + 1024u * j, lbase + 1024u * (j + 1), tok);
+        dma(k0 + R + j, j);
+        dma(k0 + R + j + 1, j + 1);
+        fold(k0 + j, x0, x1);
+      }
     }
+  } else {
+    // one pair per iteration, slots at run time (R a power of two), and one
+    // copy of the fold: the drain waits for all its inputs at once
+    static_assert((R & (R - 1)) == 0, "R a power of two");
+    for (uint32_t k = 0; k < a.d; k += 2) {
+      const uint32_t sl = k & (R - 1);
+      V4 x0, x1;
+      const bool refill = k + R < a.d;  // wave-uniform
+      if (!refill) asm volatile("s_waitcnt vmcnt(0)" : "+s"(tok));
+      lds_pair<R - 2>(x0, x1, lbase + 1024u * sl, lbase + 1024u * (sl + 1), tok);
+      if (refill) {
+        dma(k + R, sl);
+        dma(k + R + 1, sl + 1);
+      }
+      fold(k, x0, x1);
+    }
+    k0 = a.d;  // nothing left for the drain below
   }
   // drain: the last R inputs, nothing refilled (VM = inputs still in flight after this pair)
 #define UGO_DRAIN(J)                                                                        \
-  if constexpr (J < R) {                                                                    \
+  if constexpr (UNROLL && J < R) {                                                          \
     V4 x0, x1;                                                                              \
     lds_pair<(R - J - 2 > 0 ? R - J - 2 : 0)>(x0, x1, lbase + 1024u * J, lbase + 1024u * (J + 1), tok); \
     fold(k0 + J, x0, x1);                                                                   \
