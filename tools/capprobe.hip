@@ -1,7 +1,8 @@
 // capprobe.hip -- residency caps of the (10,3) kernels by batch size
 // (VERDICT r2 item 1): interleaved A/B of the production encode and
 // reconstruct_into at 2/3/4/5 blocks per CU, on a batch of G groups.
-// Usage: capprobe G rounds.  G >= 1M: one batch (its 18+ GB are far past the
+// Usage: capprobe G rounds [row_pad] [nbuf]: row_pad bytes added to the planar
+// row stride (G * pitch + row_pad).  G >= 1M: one batch (its 18+ GB are far past the
 // 256-MB Infinity Cache, so every launch is cold); G < 1M: 4 rotating
 // batches, as kvariants' cold regime.  Prints one JSON line per variant
 // (median us, TB/s of algorithmic bytes).
@@ -36,6 +37,8 @@ int main(int argc, char** argv) {
   const uint64_t G = argc > 1 ? atoll(argv[1]) : 4194304;
   const int rounds = argc > 2 ? atoi(argv[2]) : 9;
   const int nb = G >= (1u << 20) ? 1 : 4;
+  const uint64_t row_pad = argc > 3 ? atoll(argv[3]) : 0;
+  const uint64_t rstride = G * pitch + row_pad;
   std::vector<Batch> rot(nb), roto(nb);
   uint64_t* masks;
   CK(hipMalloc(&masks, G * 8));
@@ -62,16 +65,16 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dmul, hmul.data(), hmul.size(), hipMemcpyHostToDevice));
   for (int r = 0; r < nb; ++r) {
     uint8_t *buf, *ob;
-    CK(hipMalloc(&buf, G * n * pitch));
-    CK(hipMalloc(&ob, G * p * pitch));
-    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, buf, G * n * pitch / 16, 77ull + r);
+    CK(hipMalloc(&buf, n * rstride));
+    CK(hipMalloc(&ob, p * rstride));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, buf, n * rstride / 16, 77ull + r);
     Batch a{};
     a.mult = dmul;
-    a.base = buf; a.gstride = pitch; a.rstride = G * pitch; a.nmask = (1ull << n) - 1; a.S = S;
+    a.base = buf; a.gstride = pitch; a.rstride = rstride; a.nmask = (1ull << n) - 1; a.S = S;
     a.chunks = 85; a.items = static_cast<uint32_t>(G * 85); a.desc = dtab; a.present = masks;
     a.desc_stride = stride; a.d = d; a.dpad = dpad; a.epad = epad;
     rot[r] = a;
-    a.out = ob; a.ogstride = pitch; a.orstride = G * pitch;
+    a.out = ob; a.ogstride = pitch; a.orstride = rstride;
     roto[r] = a;
   }
   CK(hipDeviceSynchronize());
@@ -136,17 +139,45 @@ int main(int argc, char** argv) {
       v.t.push_back(ms);
     }
   }
+  // placement: nbuf more batches (inputs + outputs in one allocation each),
+  // production encode and reconstruct_into timed on each, back to back
+  const int nbuf = argc > 4 ? atoi(argv[4]) : 0;
+  for (int b = 0; b < nbuf; ++b) {
+    uint8_t* cp;
+    if (hipMalloc(&cp, (n + p) * rstride) != hipSuccess) break;
+    CK(hipMemcpy(cp, rot[0].base, n * rstride, hipMemcpyDeviceToDevice));
+    Batch x = rot[0], y = roto[0];
+    x.base = cp; y.base = cp; y.out = cp + n * rstride;
+    std::vector<float> te, td;
+    for (int r = 0; r < rounds + 3; ++r) {
+      CK(hipEventRecord(s0));
+      hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 13>), dim3(grid), dim3(256), 0, 0, x);
+      CK(hipEventRecord(s1));
+      hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, y);
+      CK(hipEventRecord(s2));
+      CK(hipEventSynchronize(s2));
+      float a1 = 0, a2 = 0;
+      CK(hipEventElapsedTime(&a1, s0, s1));
+      CK(hipEventElapsedTime(&a2, s1, s2));
+      if (r >= 3) { te.push_back(a1); td.push_back(a2); }
+    }
+    std::sort(te.begin(), te.end());
+    std::sort(td.begin(), td.end());
+    printf("{\"G\": %llu, \"row_pad\": %llu, \"buffer\": %d, \"va\": \"%p\", \"enc_median_us\": %.1f, \"dec_median_us\": %.1f}\n",
+           (unsigned long long)G, (unsigned long long)row_pad, b + 1, (void*)cp, te[te.size() / 2] * 1e3, td[td.size() / 2] * 1e3);
+    fflush(stdout);
+  }
   std::sort(step_enc.begin(), step_enc.end());
   std::sort(step_dec.begin(), step_dec.end());
-  printf("{\"G\": %llu, \"variant\": \"STEP enc (production) then dec into (production) on the same batch\", "
+  printf("{\"G\": %llu, \"row_pad\": %llu, \"variant\": \"STEP enc (production) then dec into (production) on the same batch\", "
          "\"enc_median_us\": %.1f, \"dec_median_us\": %.1f, \"enc_TBps\": %.3f, \"dec_TBps\": %.3f}\n",
-         (unsigned long long)G, step_enc[step_enc.size() / 2] * 1e3, step_dec[step_dec.size() / 2] * 1e3,
+         (unsigned long long)G, (unsigned long long)row_pad, step_enc[step_enc.size() / 2] * 1e3, step_dec[step_dec.size() / 2] * 1e3,
          enc_bytes / (step_enc[step_enc.size() / 2] * 1e-3) / 1e12, dec_bytes / (step_dec[step_dec.size() / 2] * 1e-3) / 1e12);
   for (auto& v : vars) {
     std::sort(v.t.begin(), v.t.end());
     const double med = v.t[v.t.size() / 2];
-    printf("{\"G\": %llu, \"variant\": \"%s\", \"median_us\": %.1f, \"TBps\": %.3f, \"min_us\": %.1f, \"max_us\": %.1f}\n",
-           (unsigned long long)G, v.name.c_str(), med * 1e3, v.bytes / (med * 1e-3) / 1e12, v.t.front() * 1e3,
+    printf("{\"G\": %llu, \"row_pad\": %llu, \"variant\": \"%s\", \"median_us\": %.1f, \"TBps\": %.3f, \"min_us\": %.1f, \"max_us\": %.1f}\n",
+           (unsigned long long)G, (unsigned long long)row_pad, v.name.c_str(), med * 1e3, v.bytes / (med * 1e-3) / 1e12, v.t.front() * 1e3,
            v.t.back() * 1e3);
   }
   return 0;

@@ -5,7 +5,9 @@
 // recovers garbage-filled erased rows of an encoded batch, checked on the
 // device against the encoded batch; then interleaved rounds, median per
 // variant (cdna_hip_programming.md §5.4 rule 24).
-// Usage: qaprobe [groups] [rounds].
+// Usage: qaprobe [groups] [rounds] [row_pad] [nbuf] [planar|gm]: row_pad bytes added to the
+// planar row stride (G * pitch + row_pad), to see whether the row streams'
+// relative alignment (G * 9008 = 2^17 * 563 at 8,192 groups) matters.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/qaprobe tools/qaprobe.hip
 // Round-3 results: profiles/r3/qaprobe_r3m.jsonl (DESIGN.md §3.4 "Jumbo floor").
 // Not product code: it includes the kernel TU to instantiate the variants.
@@ -32,14 +34,14 @@ __global__ void k_fill(uint8_t* p, uint64_t n16, uint64_t seed) {
   }
 }
 
-// erased rows of every group overwritten with 0xA5 (planar batch)
+// erased rows of every group overwritten with 0xA5
 __global__ void k_garble(uint8_t* base, const uint64_t* masks, uint64_t G, uint32_t n, uint64_t rstride,
-                         uint32_t pitch, uint32_t S) {
+                         uint64_t gstride, uint32_t S) {
   const uint64_t g = blockIdx.x;
   if (g >= G) return;
   for (uint32_t r = 0; r < n; ++r)
     if (!((masks[g] >> r) & 1))
-      for (uint32_t b = threadIdx.x; b < S; b += blockDim.x) base[r * rstride + g * pitch + b] = 0xA5;
+      for (uint32_t b = threadIdx.x; b < S; b += blockDim.x) base[r * rstride + g * gstride + b] = 0xA5;
 }
 
 __global__ void k_cmp(const uint8_t* x, const uint8_t* y, uint64_t n16, unsigned long long* bad) {
@@ -57,7 +59,12 @@ int main(int argc, char** argv) {
   const uint64_t G = argc > 1 ? atoll(argv[1]) : 8192;
   const int rounds = argc > 2 ? atoi(argv[2]) : 11;
   const uint32_t dpad = 32, epad = 8, stride = ((4 + dpad + epad + p * dpad + 15) / 16 * 16);
-  const uint64_t bytes = G * n * pitch;
+  const uint64_t row_pad = argc > 3 ? atoll(argv[3]) : 0;
+  // layout: planar [row][G][pitch] (default) or group-major [G][row][pitch] ("gm")
+  const bool gm = argc > 5 && std::string(argv[5]) == "gm";
+  const uint64_t rstride = gm ? pitch : G * pitch + row_pad;
+  const uint64_t gstride = gm ? uint64_t(n) * pitch : pitch;
+  const uint64_t bytes = gm ? G * n * pitch : n * rstride;
   uint8_t *buf, *ref, *d_gf, *d_M, *d_work, *d_ed;
   uint64_t* masks;
   unsigned long long* bad;
@@ -94,7 +101,7 @@ int main(int argc, char** argv) {
   }
   CK(hipMemcpy(masks, hm.data(), G * 8, hipMemcpyHostToDevice));
   Batch a{};
-  a.base = buf; a.gstride = pitch; a.rstride = G * pitch; a.nmask = (1ull << n) - 1; a.S = S;
+  a.base = buf; a.gstride = gstride; a.rstride = rstride; a.nmask = (1ull << n) - 1; a.S = S;
   a.chunks = (S + 15) / 16; a.items = G * a.chunks; a.desc_stride = stride; a.d = d;
   a.dpad = dpad; a.epad = epad; a.mult = reinterpret_cast<const uint32_t*>(d_gf + 1024);
   CK(launch_encode_const(d, p, a, 0));  // codewords
@@ -131,7 +138,7 @@ int main(int argc, char** argv) {
     (void)launch_prepare(pr, G, 0);
     hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 7>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   for (auto& v : vars) {  // correctness: garbage in the erased rows, recovered to the codewords
-    hipLaunchKernelGGL(k_garble, dim3(static_cast<uint32_t>(G)), dim3(256), 0, 0, buf, masks, G, n, a.rstride, pitch, S);
+    hipLaunchKernelGGL(k_garble, dim3(static_cast<uint32_t>(G)), dim3(256), 0, 0, buf, masks, G, n, a.rstride, a.gstride, S);
     v.go();
     CK(hipMemset(bad, 0, 8));
     hipLaunchKernelGGL(k_cmp, dim3(4096), dim3(256), 0, 0, buf, ref, bytes / 16, bad);
@@ -156,10 +163,48 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       v.t.push_back(ms / 3);
     }
+  // placement: the same batch copied into nbuf more allocations of the same
+  // size; the memory-pattern-only variant and OPT 7 timed on each
+  // (nbuf < 0: |nbuf| copies carved from ONE allocation, 2 MiB apart)
+  const int nbuf_arg = argc > 4 ? atoi(argv[4]) : 0;
+  const int nbuf = nbuf_arg < 0 ? -nbuf_arg : nbuf_arg;
+  const uint64_t slot = (bytes + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+  uint8_t* arena = nullptr;
+  if (nbuf_arg < 0) CK(hipMalloc(&arena, slot * nbuf));
+  for (int b = 0; b < nbuf; ++b) {
+    uint8_t* cp;
+    if (arena) cp = arena + slot * b;
+    else if (hipMalloc(&cp, bytes) != hipSuccess) break;
+    CK(hipMemcpy(cp, buf, bytes, hipMemcpyDeviceToDevice));
+    Batch ab = aa;
+    ab.base = cp;
+    hipPointerAttribute_t at{};
+    (void)hipPointerGetAttributes(&at, cp);
+    for (int opt : {15, 7}) {
+      std::vector<float> t;
+      for (int r = 0; r < rounds + 3; ++r) {
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < 3; ++i) {
+          if (opt == 15) hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 15>), dim3(ga), dim3(256), 0, 0, ab);
+          else hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 7>), dim3(ga), dim3(256), 0, 0, ab);
+        }
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 3) t.push_back(ms / 3);
+      }
+      std::sort(t.begin(), t.end());
+      printf("{\"layout\": \"%s\", \"row_pad\": %llu, \"buffer\": %d, \"va\": \"%p\", \"variant\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f}\n",
+             gm ? "group-major" : "planar", (unsigned long long)row_pad, b + 1, (void*)cp, opt == 15 ? "MEMORY PATTERN ONLY" : "k_apply_qb OPT 7",
+             t[t.size() / 2] * 1e3, t[0] * 1e3);
+    }
+    fflush(stdout);
+  }
   for (auto& v : vars) {
     std::sort(v.t.begin(), v.t.end());
     const float med = v.t[v.t.size() / 2];
-    printf("{\"variant\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f, \"TBps\": %.3f}\n", v.name.c_str(), med * 1e3,
+    printf("{\"layout\": \"%s\", \"row_pad\": %llu, \"variant\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f, \"TBps\": %.3f}\n", gm ? "group-major" : "planar", (unsigned long long)row_pad, v.name.c_str(), med * 1e3,
            v.t[0] * 1e3, dec_bytes / (med * 1e-3) / 1e12);
   }
   return 0;
