@@ -73,10 +73,12 @@ int ugo_fecconn_calc_ecc(ugo_fecconn* f, uint8_t* const* bufs, const size_t* len
  *     the next batch, and its shards come back from the input call that fills
  *     the NEXT batch (or from ugo_fecconn_flush): one batch later, the GPU time
  *     off the packet path.
- * Output capacity (checked before anything is consumed): ugo_fecconn_input
- * needs out_cap >= groups * d * UGO_FEC_MAX_PACKET (per-call mode: d packets),
- * ugo_fecconn_flush and ugo_fecconn_set_batch[_ex] that much for the current
- * mode's pending groups (OVERLAP: twice that).  groups = 0 restores per-call
+ * Output capacity (checked before anything is consumed): ugo_fecconn_input,
+ * ugo_fecconn_flush and ugo_fecconn_set_batch[_ex] need out_cap >= groups * d
+ * * UGO_FEC_MAX_PACKET for the current mode's batch (per-call mode: input
+ * d packets, flush nothing), and twice that with OVERLAP (the previous and the
+ * current batch: flush, or an input whose group finds no GPU-visible pool
+ * buffer when pinned memory has run out).  groups = 0 restores per-call
  * recovery (the default).  Both calls first flush what is pending into out.
  * UGO_FEC_ERR_INVALID_ARG for groups < 0, unknown flags or d+p > 64. */
 #define UGO_FECCONN_BATCH_OVERLAP 1u

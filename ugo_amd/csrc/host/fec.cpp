@@ -290,8 +290,11 @@ bool FEC::stage(Batch& b, const std::vector<PoolBuf*>& shards, size_t maxlen) {
   uint64_t* row = b.rows + b.groups * n;
   uint64_t mask = 0;
   int kept = 0;
-  for (size_t k = 0; k < n && kept < dataShards_; ++k)
-    if (shards[k] && !slotDev_[shards[k]->slot]) return false;
+  for (size_t k = 0, seen = 0; k < n && seen < static_cast<size_t>(dataShards_); ++k)
+    if (shards[k]) {
+      if (!slotDev_[shards[k]->slot]) return false;
+      ++seen;
+    }
   for (size_t k = 0; k < n; ++k) {
     row[k] = 0;
     if (shards[k] && kept < dataShards_) {
@@ -461,8 +464,11 @@ size_t FEC::pending() const {
 size_t FEC::maxReturnGroups(bool isFlush) const {
   const size_t cap = static_cast<size_t>(batchCap_);
   if (cap == 0) return isFlush ? 0 : 1;
-  // overlap: the previous batch (input), or the previous and the current (flush)
-  if (batchFlags_ & kBatchOverlap) return isFlush ? 2 * cap : cap;
+  // overlap: the previous batch and the current one -- flush, and input when a
+  // group cannot be staged (no GPU-visible pool slot: recoverGroup flushes
+  // both, then recovers that group by copy); without overlap the current
+  // batch, or the current batch's cap - 1 groups plus that group
+  if (batchFlags_ & kBatchOverlap) return 2 * cap;
   return cap;
 }
 
