@@ -5,7 +5,7 @@
 // recovers garbage-filled erased rows of an encoded batch, checked on the
 // device against the encoded batch; then interleaved rounds, median per
 // variant (cdna_hip_programming.md §5.4 rule 24).
-// Usage: qaprobe [groups] [rounds] [row_pad] [nbuf] [planar|gm]: row_pad bytes added to the
+// Usage: qaprobe [groups] [rounds] [row_pad] [nbuf] [planar|gm] [contig]: row_pad bytes added to the
 // planar row stride (G * pitch + row_pad), to see whether the row streams'
 // relative alignment (G * 9008 = 2^17 * 563 at 8,192 groups) matters.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/qaprobe tools/qaprobe.hip
@@ -168,13 +168,19 @@ int main(int argc, char** argv) {
   // (nbuf < 0: |nbuf| copies carved from ONE allocation, 2 MiB apart)
   const int nbuf_arg = argc > 4 ? atoi(argv[4]) : 0;
   const int nbuf = nbuf_arg < 0 ? -nbuf_arg : nbuf_arg;
+  // argv[6] == "contig": the copies from hipExtMallocWithFlags(hipDeviceMallocContiguous)
+  const bool contig = argc > 6 && std::string(argv[6]) == "contig";
   const uint64_t slot = (bytes + (2u << 20) - 1) / (2u << 20) * (2u << 20);
   uint8_t* arena = nullptr;
   if (nbuf_arg < 0) CK(hipMalloc(&arena, slot * nbuf));
   for (int b = 0; b < nbuf; ++b) {
     uint8_t* cp;
     if (arena) cp = arena + slot * b;
-    else if (hipMalloc(&cp, bytes) != hipSuccess) break;
+    else if (contig ? hipExtMallocWithFlags(reinterpret_cast<void**>(&cp), bytes, hipDeviceMallocContiguous) != hipSuccess
+                    : hipMalloc(&cp, bytes) != hipSuccess) {
+      printf("{\"buffer\": %d, \"alloc\": \"failed\"}\n", b + 1);
+      break;
+    }
     CK(hipMemcpy(cp, buf, bytes, hipMemcpyDeviceToDevice));
     Batch ab = aa;
     ab.base = cp;
@@ -195,8 +201,8 @@ int main(int argc, char** argv) {
         if (r >= 3) t.push_back(ms / 3);
       }
       std::sort(t.begin(), t.end());
-      printf("{\"layout\": \"%s\", \"row_pad\": %llu, \"buffer\": %d, \"va\": \"%p\", \"variant\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f}\n",
-             gm ? "group-major" : "planar", (unsigned long long)row_pad, b + 1, (void*)cp, opt == 15 ? "MEMORY PATTERN ONLY" : "k_apply_qb OPT 7",
+      printf("{\"layout\": \"%s\", \"contig\": %d, \"row_pad\": %llu, \"buffer\": %d, \"va\": \"%p\", \"variant\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f}\n",
+             gm ? "group-major" : "planar", contig ? 1 : 0, (unsigned long long)row_pad, b + 1, (void*)cp, opt == 15 ? "MEMORY PATTERN ONLY" : "k_apply_qb OPT 7",
              t[t.size() / 2] * 1e3, t[0] * 1e3);
     }
     fflush(stdout);
