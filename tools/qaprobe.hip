@@ -44,6 +44,15 @@ __global__ void k_garble(uint8_t* base, const uint64_t* masks, uint64_t G, uint3
       for (uint32_t b = threadIdx.x; b < S; b += blockDim.x) base[r * rstride + g * gstride + b] = 0xA5;
 }
 
+// rows [r0, r1) of every group overwritten with 0xA5 over their S bytes
+__global__ void k_garble_rows(uint8_t* base, uint32_t r0, uint32_t r1, uint64_t G, uint64_t rstride, uint64_t gstride,
+                              uint32_t S) {
+  const uint64_t g = blockIdx.x;
+  if (g >= G) return;
+  for (uint32_t r = r0; r < r1; ++r)
+    for (uint32_t b = threadIdx.x; b < S; b += blockDim.x) base[r * rstride + g * gstride + b] = 0xA5;
+}
+
 __global__ void k_cmp(const uint8_t* x, const uint8_t* y, uint64_t n16, unsigned long long* bad) {
   unsigned long long nb = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += gridDim.x * 256ull) {
@@ -114,11 +123,12 @@ int main(int argc, char** argv) {
   aa.desc = d_work; aa.present = masks; aa.g_desc0 = 0;
   aa.items = G * ((a.chunks + 63) / 64 * 64);
   const uint32_t ga = (aa.items + 255) / 256;
+  const uint32_t ga8 = (ga + 7) / 8 * 8;  // OPT & 32 grids: a multiple of 8
   CK(hipDeviceSynchronize());
   const double dec_bytes = dec_rows * S;
   struct Var { std::string name; std::function<void()> go; std::vector<float> t; };
   std::vector<Var> vars;
-  vars.push_back({"k_apply_qa ring2 (production)", [=]() {
+  vars.push_back({"k_apply_qa ring2 (round 2)", [=]() {
     hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_apply_qb OPT 1 (uniform desc)", [=]() { hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 1>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_apply_qb OPT 3 (+ saddr loads; 72 VGPRs, 7 waves/SIMD)", [=]() { hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 3>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
@@ -128,24 +138,45 @@ int main(int argc, char** argv) {
   vars.push_back({"k_apply_ql LDS-DMA ring 4", [=]() { hipLaunchKernelGGL((k_apply_ql<8, 2, 4>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"MEMORY PATTERN ONLY of k_apply_qb OPT 7 (inputs XORed, no products; wrong bytes)", [=]() {
     hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 15>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
-  vars.push_back({"k_prepare + k_apply_qa (production reconstruct)", [=]() {
+  vars.push_back({"k_apply_qb OPT 39 (7 + XCD-contiguous blocks)", [=]() {
+    hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 39>), dim3(ga8), dim3(256), 0, 0, aa); }, {}});
+  {
+    const uint32_t ge = (a.items + 255) / 256, ge8 = (ge + 7) / 8 * 8;
+    vars.push_back({"ENCODE k_encode_frs (production)", [=]() {
+      hipLaunchKernelGGL((k_encode_frs<32, 8, kEncJumboNT & 2, kEncJumboLdsRows, 256, kEncJumboLdsRows, 3, kEncJumboFrBlock>),
+                         dim3(ge), dim3(256), 0, 0, a); }, {}});
+    vars.push_back({"ENCODE k_encode_frs XCD-contiguous blocks", [=]() {
+      hipLaunchKernelGGL((k_encode_frs<32, 8, kEncJumboNT & 2, kEncJumboLdsRows, 256, kEncJumboLdsRows, 3, kEncJumboFrBlock, true>),
+                         dim3(ge8), dim3(256), 0, 0, a); }, {}});
+  }
+  vars.push_back({"k_prepare + k_apply_qa (round 2)", [=]() {
     (void)launch_prepare(pr, G, 0);
     hipLaunchKernelGGL((k_apply_qa<8, 2, 3, 2>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_prepare + k_apply_qb OPT 3", [=]() {
     (void)launch_prepare(pr, G, 0);
     hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 3>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
+  vars.push_back({"k_prepare + k_apply_qb OPT 39 (production)", [=]() {
+    (void)launch_prepare(pr, G, 0);
+    hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 39>), dim3(ga8), dim3(256), 0, 0, aa); }, {}});
   vars.push_back({"k_prepare + k_apply_qb OPT 7", [=]() {
     (void)launch_prepare(pr, G, 0);
     hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 7>), dim3(ga), dim3(256), 0, 0, aa); }, {}});
   for (auto& v : vars) {  // correctness: garbage in the erased rows, recovered to the codewords
-    hipLaunchKernelGGL(k_garble, dim3(static_cast<uint32_t>(G)), dim3(256), 0, 0, buf, masks, G, n, a.rstride, a.gstride, S);
+    CK(hipMemcpy(buf, ref, bytes, hipMemcpyDeviceToDevice));
+    const bool enc = v.name.rfind("ENCODE", 0) == 0;
+    if (enc)  // encode: garbage in every parity row, rebuilt from the data rows
+      hipLaunchKernelGGL(k_garble_rows, dim3(static_cast<uint32_t>(G)), dim3(256), 0, 0, buf, uint32_t(d), uint32_t(n), G,
+                         a.rstride, a.gstride, S);
+    else
+      hipLaunchKernelGGL(k_garble, dim3(static_cast<uint32_t>(G)), dim3(256), 0, 0, buf, masks, G, n, a.rstride, a.gstride, S);
     v.go();
     CK(hipMemset(bad, 0, 8));
     hipLaunchKernelGGL(k_cmp, dim3(4096), dim3(256), 0, 0, buf, ref, bytes / 16, bad);
     unsigned long long nbad = 0;
     CK(hipMemcpy(&nbad, bad, 8, hipMemcpyDeviceToHost));
-    printf("{\"check\": \"%s recovers garbage-filled erased rows\", \"mismatched_dwords\": %llu}\n", v.name.c_str(), nbad);
+    printf("{\"check\": \"%s recovers garbage-filled erased (encode: parity) rows\", \"mismatched_dwords\": %llu}\n", v.name.c_str(), nbad);
   }
+  CK(hipMemcpy(buf, ref, bytes, hipMemcpyDeviceToDevice));
   fflush(stdout);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -186,12 +217,14 @@ int main(int argc, char** argv) {
     ab.base = cp;
     hipPointerAttribute_t at{};
     (void)hipPointerGetAttributes(&at, cp);
-    for (int opt : {15, 7}) {
+    for (int opt : {15, 47, 7, 39}) {
       std::vector<float> t;
       for (int r = 0; r < rounds + 3; ++r) {
         CK(hipEventRecord(e0));
         for (int i = 0; i < 3; ++i) {
           if (opt == 15) hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 15>), dim3(ga), dim3(256), 0, 0, ab);
+          else if (opt == 47) hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 47>), dim3(ga8), dim3(256), 0, 0, ab);
+          else if (opt == 39) hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 39>), dim3(ga8), dim3(256), 0, 0, ab);
           else hipLaunchKernelGGL((k_apply_qb<8, 2, 3, 7>), dim3(ga), dim3(256), 0, 0, ab);
         }
         CK(hipEventRecord(e1));
@@ -202,7 +235,8 @@ int main(int argc, char** argv) {
       }
       std::sort(t.begin(), t.end());
       printf("{\"layout\": \"%s\", \"contig\": %d, \"row_pad\": %llu, \"buffer\": %d, \"va\": \"%p\", \"variant\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f}\n",
-             gm ? "group-major" : "planar", contig ? 1 : 0, (unsigned long long)row_pad, b + 1, (void*)cp, opt == 15 ? "MEMORY PATTERN ONLY" : "k_apply_qb OPT 7",
+             gm ? "group-major" : "planar", contig ? 1 : 0, (unsigned long long)row_pad, b + 1, (void*)cp, opt == 15 ? "MEMORY PATTERN ONLY" : opt == 47 ? "MEMORY PATTERN ONLY, XCD-contiguous blocks"
+             : opt == 39 ? "k_apply_qb OPT 39 (7 + XCD-contiguous blocks)" : "k_apply_qb OPT 7",
              t[t.size() / 2] * 1e3, t[0] * 1e3);
     }
     fflush(stdout);

@@ -162,11 +162,16 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 
 // k_encode_fr with the dwords forced in sequence (cparity_fr_seq): staged rows
 // read from LDS per dword, so the live set is one dword's tables.
-template <int D, int P, int NTS = 0, int GR = D, int BS = 256, int LR = GR, int WPE = 1, int BK = kFrBlock>
+// XCD (grid a multiple of 8): block b works on tile (b % 8) * (grid / 8) + b / 8,
+// each XCD on one contiguous eighth of the batch (k_apply_qb OPT & 32).
+template <int D, int P, int NTS = 0, int GR = D, int BS = 256, int LR = GR, int WPE = 1, int BK = kFrBlock,
+          bool XCD = false>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void k_encode_frs(Batch a) {
   static_assert(LR >= GR, "the stage holds at least the staged rows");
   __shared__ u32x4 stage[BS / 64][LR][64];
-  const uint32_t item = blockIdx.x * BS + threadIdx.x;
+  uint32_t bid = blockIdx.x;
+  if constexpr (XCD) bid = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  const uint32_t item = bid * BS + threadIdx.x;
   if (item >= a.items) return;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const Loc l = locate(a, item);
@@ -783,7 +788,13 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
 template <int EMAX, int MODE, int NT, int OPT = 7, int WPE = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_qb(Batch a) {
   const uint32_t cpad = (a.chunks + 63u) & ~63u;
-  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  // OPT & 32 (grid a multiple of 8): XCD-contiguous blocks -- the hardware
+  // deals blocks to the 8 XCDs round robin; block b works on tile
+  // (b % 8) * (grid / 8) + b / 8, so each XCD sweeps one contiguous eighth
+  // and the 2-3 blocks of one group read its descriptor through one L2
+  uint32_t bid = blockIdx.x;
+  if constexpr (OPT & 32) bid = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  const uint32_t wfirst = bid * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
   if (wfirst >= a.items) return;  // a.items = groups * cpad here
   const uint32_t gl = (OPT & 1) ? __builtin_amdgcn_readfirstlane(wfirst / cpad) : wfirst / cpad;
   const uint64_t g = a.g0 + gl;
@@ -801,7 +812,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const uint32_t hA = dword(0);
   const uint32_t st = (hA >> 16) & 0xffu;
   const uint32_t e = st ? 0u : (a.data_only ? ((hA >> 8) & 0xffu) : (hA & 0xffu));
-  const uint32_t c = blockIdx.x * 256u + threadIdx.x - gl * cpad;
+  const uint32_t c = bid * 256u + threadIdx.x - gl * cpad;
   const bool live = c < a.chunks;
   const bool wst = MODE != 0 && a.status != nullptr && c == 0;
   if (e == 0) {  // wave-uniform
@@ -1519,14 +1530,17 @@ static bool launch_apply_stream(const Batch& a, hipStream_t s) {
   if (MODE != 0 && (cpad - a.chunks) * 16u <= cpad) {  // groups wave-aligned at <= 1/16 idle lanes
     Batch b = a;
     b.items = (a.items / a.chunks) * cpad;
-    const dim3 ga(blocks_for(b.items, 256));
+    const dim3 ga((blocks_for(b.items, 256) + 7u) & ~7u);  // OPT & 32: a multiple of 8
     // k_apply_qb: k_apply_qa with its per-product overhead cut (uniform
     // descriptor in SGPRs, saddr loads, unrolled ring): jumbo reconstruct
-    // 524.0 vs 535.5 us (profiles/r3/qaprobe_r3e.jsonl)
+    // 524.0 vs 535.5 us (profiles/r3/qaprobe_r3e.jsonl); and each XCD on one
+    // contiguous eighth of the groups, so a group's blocks share one L2 for
+    // its descriptor: 482-523 vs 505-533 us over 8 allocations
+    // (profiles/r3/qaprobe_xcd.jsonl)
     if (a.epad == 4)
-      launch(apply_kid<MODE>(), k_apply_qb<4, MODE, kApplyQNT, 7>, ga, block, 0, s, b);
+      launch(apply_kid<MODE>(), k_apply_qb<4, MODE, kApplyQNT, 39>, ga, block, 0, s, b);
     else
-      launch(apply_kid<MODE>(), k_apply_qb<8, MODE, kApplyQNT, 7>, ga, block, 0, s, b);
+      launch(apply_kid<MODE>(), k_apply_qb<8, MODE, kApplyQNT, 39>, ga, block, 0, s, b);
     return true;
   }
   const dim3 grid(blocks_for(a.items, 256));
