@@ -236,6 +236,16 @@ def test_input_refuses_a_short_output_buffer_before_consuming(gpu):
     assert st == fec.ErrInvalidArg.code and rx.rx_len() == 0
     rx.input(pk[0])  # the binding's own buffer holds d shards
     assert rx.rx_len() == 1
+    # overlapped batches of 4: input must hold two batches (the pinned-exhaustion
+    # fallback returns both); one batch's worth is refused, nothing consumed
+    rx.set_batch(4, overlap=True)
+    one_batch = (ctypes.c_uint8 * (4 * D * fec.UGO_FEC_MAX_PACKET))()
+    w1 = (ctypes.c_uint8 * len(pk[1])).from_buffer_copy(pk[1])
+    st = rx._lib.ugo_fecconn_input(rx._h, ctypes.addressof(w1), len(pk[1]), None, None, ctypes.addressof(one_batch),
+                                   len(one_batch), ctypes.byref(nrec), ctypes.byref(rlen))
+    assert st == fec.ErrInvalidArg.code and rx.rx_len() == 1
+    rx.input(pk[1])
+    assert rx.rx_len() == 2
 
 
 def _tx_stream_any(tx, d, p, groups, rng, max_len):
