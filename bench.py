@@ -68,6 +68,8 @@ def parse(argv=None):
     ap.add_argument("--parity-shards", type=int, default=3)
     ap.add_argument("--shard-size", type=int, default=1350)
     ap.add_argument("--pitch", type=int, default=0, help="row pitch in HBM (default: shard size rounded to 16)")
+    ap.add_argument("--out-pitch", type=int, default=0,
+                    help="row pitch of the reconstruct_into output batch (default: the batch pitch)")
     ap.add_argument("--erasures", type=int, default=2)
     ap.add_argument("--batches", type=int, default=2,
                     help="rotate the steps over this many independent batches per GPU (step k works on batch "
@@ -685,7 +687,8 @@ def run_rank(args):
     masks, erased = make_masks(G, n, e, args.seed + 1000 + rank, dev)
     into = args.decode == "into"
     # one output batch per input batch, so every step's outputs are cold too
-    outs = [torch.zeros((p, G, pitch), dtype=torch.uint8, device=dev) for _ in range(nb)] if into else None
+    opitch = args.out_pitch or pitch
+    outs = [torch.zeros((p, G, opitch), dtype=torch.uint8, device=dev) for _ in range(nb)] if into else None
     stream = torch.cuda.current_stream()
     cur = [0]
 
@@ -731,7 +734,7 @@ def run_rank(args):
         for j in range(e):
             view[gi, erased[:, j].to(dev)] = 0
         if into:
-            o = torch.full((p, G, pitch), 0xA5, dtype=torch.uint8, device=dev)
+            o = torch.full((p, G, opitch), 0xA5, dtype=torch.uint8, device=dev)
             enc.reconstruct_into(shards, masks, o, shard_size=S, stream=stream, shard_major=planar)
             es = erased.sort(dim=1).values.to(dev)  # output j = j-th erased row, ascending
             ok_rt = all(bool(torch.equal(o[j, :, :S], ref[gi, es[:, j], :S])) for j in range(e))

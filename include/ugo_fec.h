@@ -101,7 +101,12 @@ int ugo_fec_encode(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_si
  * the larger one must clear a whole run of the smaller ((count - 1) * smaller
  * + shard_size), else UGO_FEC_ERR_INVALID_ARG before any launch (the same rule
  * holds for every strided batch below).
- * Fast path: shards, row_stride and group_stride all multiples of 16. */
+ * Fast path: shards, row_stride and group_stride all multiples of 16.
+ * Dense planar rows (group_stride == shard_size, no padding; shards and
+ * row_stride multiples of 16) take the vector kernels too: encode folds
+ * 16/gcd(shard_size, 16) groups into one 16-B-whole pseudo-group; reconstruct
+ * (d <= 16, p <= 4, shard_size >= 1009) runs on the rows' aligned chunks.
+ * Padded 16-B pitches stay the faster reconstruct layout. */
 int ugo_fec_encode_strided(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_size,
                            size_t row_stride, size_t group_stride, void* stream);
 

@@ -380,7 +380,8 @@ def test_host_reconstruct_pinned_zero_copy(gpu, offset, pitch, data_only):
         assert np.array_equal(got[ok][:, :, :S], want[ok][:, :, :S])
 
 
-@pytest.mark.parametrize("d,p,S,pitch", [(10, 3, 1350, 1360), (32, 8, 9000, 9008), (6, 2, 77, 80)])
+@pytest.mark.parametrize("d,p,S,pitch", [(10, 3, 1350, 1360), (32, 8, 9000, 9008), (6, 2, 77, 80),
+                                         (10, 3, 1350, 1350), (10, 3, 1476, 1476), (5, 2, 333, 333)])
 def test_shard_major_layout(gpu, d, p, S, pitch):
     """Planar [d+p][G][pitch] batches (ugo_fec_*_strided) give the same bytes."""
     n, G = d + p, 513
@@ -568,6 +569,73 @@ def test_reconstruct_into_vs_oracle(gpu, d, p, S, pitch, opitch, shard_major, ta
         if shard_major:
             got = got.transpose(1, 0, 2)
         assert np.array_equal(got, exp), (d, p, S, data_only)
+
+
+@pytest.mark.parametrize("d,p,S,G,table_max", [
+    (10, 3, 1350, 777, "16"),   # the bench's dense rows: 8 groups per pseudo-group, k_apply_p on 2-B aligned groups
+    (10, 3, 1350, 777, "0"),    # same with per-group descriptors (k_prepare)
+    (10, 3, 1476, 64, "16"),    # ugo's full packet size: 4 groups per pseudo-group
+    (12, 4, 1031, 333, "16"),   # odd S: 16 groups per pseudo-group, 1-B aligned groups
+    (4, 2, 1009, 100, "16"),    # exactly 64 chunks per row
+    (10, 3, 1350, 7, "16"),     # fewer groups than one pseudo-group: the tail alone
+    (10, 3, 1350, 1, "16"),     # one group
+    (20, 4, 1350, 99, "16"),    # d > 16: dense encode, byte-kernel reconstruct
+    (10, 3, 100, 50, "16"),     # rows < 64 chunks: dense encode, byte-kernel reconstruct
+])
+def test_dense_planar_rows_vs_oracle(gpu, d, p, S, G, table_max, monkeypatch):
+    """Dense shard-major batches (group stride == S, rows 16-B aligned: no
+    padding bytes at all): encode folds 16/gcd(S,16) groups into one
+    pseudo-group, reconstruct runs the vector kernel on unaligned group
+    offsets.  Bit-exact vs the oracle in place and into a dense output batch;
+    the bytes between rows are never written."""
+    monkeypatch.setenv("UGO_FEC_TABLE_MAX_SHARDS", table_max)
+    n = d + p
+    rs = (G * S + 15) // 16 * 16 + 32
+    rng = np.random.default_rng(S * 31 + G)
+    packed = rng.integers(0, 256, (G, n, S), dtype=np.uint8)
+    want = packed.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    flat = torch.full((n * rs,), 0x5A, dtype=torch.uint8, device="cuda")
+    view = flat.as_strided((n, G, S), (rs, S, 1))
+    view.copy_(torch.as_tensor(packed).cuda().transpose(0, 1))
+    outside = torch.ones(n * rs, dtype=torch.bool, device="cuda")
+    outside.as_strided((n, G, S), (rs, S, 1)).fill_(False)
+    untouched = flat.clone()
+    enc = fec.New(d, p)
+    enc.encode_batch(view, shard_size=S, shard_major=True)
+    assert np.array_equal(view.transpose(0, 1).cpu().numpy(), want)
+    assert torch.equal(flat[outside], untouched[outside]), "bytes between rows were written"
+    masks = np.zeros(G, np.uint64)
+    for g in range(G):
+        m = (1 << n) - 1
+        for r in rng.choice(n, size=int(rng.integers(0, p + 2)), replace=False):
+            m &= ~(1 << int(r))
+        masks[g] = m
+    inp = _erase(want, masks, n)
+    exp = inp.copy()
+    rc, exp_st = rs_ref.c_reconstruct(d, p, exp, masks, S=S)
+    # into a dense, contiguous [p][G][S] output batch (its rows need no alignment)
+    out = torch.full((p, G, S), 0xA5, dtype=torch.uint8, device="cuda")
+    view.copy_(torch.as_tensor(inp).cuda().transpose(0, 1))
+    st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    enc.reconstruct_into(view, _masks_to_dev(masks), out, shard_size=S, status=st, shard_major=True,
+                         out_shard_major=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), exp_st)
+    o = out.transpose(0, 1).cpu().numpy()
+    want_o = np.full((G, p, S), 0xA5, dtype=np.uint8)
+    for g in range(G):
+        if exp_st[g] != 0:
+            continue
+        for i, r in enumerate([r for r in range(n) if not (int(masks[g]) >> r) & 1]):
+            want_o[g, i] = exp[g, r]
+    assert np.array_equal(o, want_o)
+    # in place
+    st.fill_(-1)
+    enc.reconstruct_batch(view, _masks_to_dev(masks), shard_size=S, status=st, shard_major=True)
+    assert np.array_equal(st.cpu().numpy(), exp_st)
+    assert np.array_equal(view.transpose(0, 1).cpu().numpy(), exp)
+    assert torch.equal(flat[outside], untouched[outside])
 
 
 def test_reconstruct_into_rejects_bad_outputs(gpu):

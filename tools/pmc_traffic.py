@@ -23,7 +23,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-KERNELS = {"k_encode_c": "encode", "k_encode_g": "encode", "k_encode_frs": "encode", "k_apply_p<": "reconstruct", "k_apply_w<": "reconstruct", "k_apply<": "reconstruct", "k_apply_bytes": "reconstruct_bytes",
+KERNELS = {"k_encode_c": "encode", "k_encode_g": "encode", "k_encode_frs": "encode", "k_apply_p<": "reconstruct", "k_apply_pd<": "reconstruct", "k_apply_w<": "reconstruct", "k_apply<": "reconstruct", "k_apply_bytes": "reconstruct_bytes",
            "k_prepare": "prepare"}
 
 

@@ -563,6 +563,126 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (wst) a.status[g] = 0;
 }
 
+// k_apply_p for DENSE rows (group stride == S, no padding: row r of group g at
+// base + r*rstride + g*S, rows 16-B aligned, S >= 1009).  Lanes take the rows'
+// aligned 16-B chunks, not per-group ones, so every load and store is aligned.
+// Before this kernel dense rows ran the byte kernel.  On the (10,3) bench step
+// it takes 186-189 us against 172-178 for k_apply_p on the 16-B pitch (the two
+// partial stores of each straddling chunk ~9 us, the idle 64th lane ~3 us;
+// k_apply_p on 2-B aligned groups: 186-189 too; profiles/r3/dense/), so the
+// bench keeps padded rows.  A wave covers 63 chunks (1008 B < S: at most one group
+// boundary EB, groups A and B as in k_apply_p); a chunk's group is the group
+// of its first byte.  When EB is not 16-B aligned its chunk holds the end of
+// A and the start of B: that lane stores A's bytes [0, EB % 16), and lane 63
+// -- a B lane on the same chunk, B's rows and B's tables, in the same
+// instructions as every other lane -- stores B's bytes [EB % 16, 16).  The
+// group's status goes with the lane that holds its first byte.
+__device__ __forceinline__ void store16_from(uint8_t* p, const V4& y, uint32_t lo) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t b0 = 4u * j, w = y.v[j];
+    if (lo <= b0) {
+      *reinterpret_cast<uint32_t*>(p + b0) = w;
+    } else if (lo < b0 + 4) {
+      if (lo <= b0 + 1) p[b0 + 1] = static_cast<uint8_t>(w >> 8);
+      if (lo <= b0 + 2) p[b0 + 2] = static_cast<uint8_t>(w >> 16);
+      p[b0 + 3] = static_cast<uint8_t>(w >> 24);
+    }
+  }
+}
+
+template <int DMAX, int MODE, int NT, int EMAX = 4>
+__global__ __launch_bounds__(256) void k_apply_pd(Batch a) {
+  // a.base: row 0 of group a.g0 (16-B aligned); a.items: the slice's aligned
+  // chunks per row, ceil(groups * S / 16); a.n: groups in the slice
+  const uint32_t w = blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t c0 = w * 63u;  // the wave's first chunk
+  if (c0 >= a.items) return;
+  const uint32_t S = a.S;
+  const uint64_t fw = static_cast<uint64_t>(c0) * 16u;
+  const uint32_t gA = static_cast<uint32_t>(fw / S);
+  const uint64_t eb = static_cast<uint64_t>(gA + 1u) * S;  // end of group A
+  const uint32_t cend = min(c0 + 63u, a.items);
+  const bool has_b = gA + 1u < a.n && eb < static_cast<uint64_t>(cend) * 16u;
+  const uint32_t gB = has_b ? gA + 1u : gA;
+  const uint8_t* dA = desc_for<MODE>(a, a.g0 + gA);
+  const uint8_t* dB = desc_for<MODE>(a, a.g0 + gB);
+  constexpr int NW = (DMAX + 3) / 4;
+  const uint32_t hA = ld32(dA), hB = ld32(dB);
+  uint32_t rA[NW], rB[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    rA[q] = ld32(dA + 4 + 4 * q);
+    rB[q] = ld32(dB + 4 + 4 * q);
+  }
+  const uint32_t oA = ld32(dA + 4 + a.dpad), oB = ld32(dB + 4 + a.dpad);
+  const uint32_t eA = ((hA >> 16) & 0xffu) ? 0u : (a.data_only ? ((hA >> 8) & 0xffu) : (hA & 0xffu));
+  const uint32_t eB = ((hB >> 16) & 0xffu) ? 0u : (a.data_only ? ((hB >> 8) & 0xffu) : (hB & 0xffu));
+  const uint32_t emax = max(eA, eB);
+  // this lane's chunk, group and byte range [lo, hi) of the chunk it stores
+  uint64_t f;
+  bool inB;
+  uint32_t lo = 0, hi;
+  if (lane < 63u) {
+    const uint32_t ci = c0 + lane;
+    if (ci >= a.items) return;
+    f = static_cast<uint64_t>(ci) * 16u;
+    inB = has_b && f >= eb;
+    const uint64_t gend = inB ? eb + S : eb;  // end of this lane's group
+    hi = static_cast<uint32_t>(min(gend - f, static_cast<uint64_t>(16)));
+  } else {  // lane 63: B's bytes of a straddling chunk, if any
+    if (!has_b || (eb & 15u) == 0) return;
+    f = eb & ~static_cast<uint64_t>(15);
+    inB = true;
+    lo = static_cast<uint32_t>(eb & 15u);
+    hi = 16u;
+  }
+  const uint64_t gstart = inB ? eb : eb - S;
+  const uint64_t g = a.g0 + (inB ? gB : gA);
+  const uint32_t hdr = inB ? hB : hA;
+  const uint32_t st = (hdr >> 16) & 0xffu;
+  const bool wst = a.status != nullptr && f <= gstart && gstart < f + 16u;  // holds the group's first byte
+  const uint32_t e = inB ? eB : eA;
+  if (e == 0) {
+    if (wst) a.status[g] = static_cast<int8_t>(st);
+    return;
+  }
+  uint32_t mB;
+  asm("v_mov_b32 %0, %1" : "=v"(mB) : "v"(inB ? ~0u : 0u));
+  uint8_t* gp = a.base + f;
+  V4 x[DMAX];
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    if (k < static_cast<int>(a.d)) {
+      const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
+      const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
+      x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
+    } else {
+      x[k] = V4{{0u, 0u, 0u, 0u}};
+    }
+  }
+  V4 acc[EMAX];
+  if (dA == dB)
+    p_accum<DMAX, 0, EMAX, true>(acc, x, a, dA, dA, 0u, emax);
+  else
+    p_accum<DMAX, 1, EMAX, true>(acc, x, a, dA, dB, mB, emax);
+  const uint32_t orows = inB ? oB : oA;
+  const int64_t off = static_cast<int64_t>(f) - static_cast<int64_t>(gstart);  // chunk start within the group
+#pragma unroll
+  for (int i = 0; i < EMAX; ++i) {
+    if (i >= static_cast<int>(e)) continue;
+    const uint32_t r = (orows >> (8 * i)) & 0xffu;
+    uint8_t* p = a.out ? a.out + static_cast<int64_t>(g * a.ogstride + static_cast<uint64_t>(i) * a.orstride) + off
+                       : gp + static_cast<uint64_t>(r) * a.rstride;
+    if (lo)
+      store16_from(p, acc[i], lo);
+    else
+      store16<NT>(p, acc[i], hi);
+  }
+  if (wst) a.status[g] = 0;
+}
+
 // Streaming form of k_apply_p for wide codes ((32,8) jumbo: d up to 255,
 // e <= EMAX outputs): inputs are not held -- a 4-deep ring of survivor
 // chunks is loaded ahead while the current pair is folded into EMAX live
@@ -1603,6 +1723,30 @@ hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s) {
     case 0: return launch_apply_mode<0>(dmax, a, s);
     case 1: return launch_apply_mode<1>(dmax, a, s);
     case 2: return launch_apply_mode<2>(dmax, a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int MODE>
+static hipError_t launch_apply_dense_mode(int dmax, const Batch& a, hipStream_t s) {
+  const uint32_t waves = (a.items + 62u) / 63u;
+  const dim3 grid((waves + 3u) / 4u), block(256);
+  switch (dmax) {
+    case 4: launch(kKReconstruct, k_apply_pd<4, MODE, kApplyPNT>, grid, block, 0, s, a); break;
+    case 8: launch(kKReconstruct, k_apply_pd<8, MODE, kApplyPNT>, grid, block, 0, s, a); break;
+    case 10: launch(kKReconstruct, k_apply_pd<10, MODE, kApplyPNT>, grid, block, 0, s, a); break;
+    case 12: launch(kKReconstruct, k_apply_pd<12, MODE, kApplyPNT>, grid, block, 0, s, a); break;
+    case 16: launch(kKReconstruct, k_apply_pd<16, MODE, kApplyPNT>, grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_apply_dense(int mode, int dmax, const Batch& a, hipStream_t s) {
+  if (a.S < kDenseMinS || a.epad != 4) return hipErrorInvalidValue;
+  switch (mode) {
+    case 1: return launch_apply_dense_mode<1>(dmax, a, s);
+    case 2: return launch_apply_dense_mode<2>(dmax, a, s);
     default: return hipErrorInvalidValue;
   }
 }

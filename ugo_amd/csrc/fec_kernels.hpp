@@ -33,7 +33,7 @@ struct Batch {
   uint64_t ogstride;        //   (i-th erased row, ascending) of group g at out + g*ogstride + i*orstride
   uint64_t orstride;
   const uint64_t* rows;     // k_apply_rows: row r of group g at rows[g*n + r] (device addresses)
-  uint32_t n;               // k_apply_rows: d + p
+  uint32_t n;               // k_apply_rows: d + p; k_apply_pd: groups in the launch
 };
 
 struct Prep {
@@ -59,6 +59,12 @@ hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s);
 hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s);
 hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s);
 hipError_t launch_apply_rows(int mode, const Batch& a, hipStream_t s);  // MODE 1 / 2, output batch required
+// Dense rows (group stride == S, no padding; k_apply_pd): MODE 1 / 2, d <= 16
+// (dmax 4..16), p <= 4, S >= kDenseMinS (a wave's 63 chunks span at most one
+// group boundary).  a.base = row 0 of group a.g0, 16-B aligned; a.items =
+// ceil(groups * S / 16); a.n = groups in the launch.
+constexpr uint32_t kDenseMinS = 63 * 16 + 1;
+hipError_t launch_apply_dense(int mode, int dmax, const Batch& a, hipStream_t s);
 
 
 

@@ -266,8 +266,28 @@ int check_batch(const ugo_fec* c, const void* shards, size_t groups, size_t S, c
   return UGO_FEC_OK;
 }
 
+// Dense planar batch: groups packed back to back in each row (group stride ==
+// S, no padding), rows 16-B aligned.  Encode is column-wise and every group
+// uses the same matrix, so k = 16 / gcd(S, 16) consecutive groups form one
+// pseudo-group of k*S bytes, a whole number of 16-B chunks: the vector kernels
+// then read and write exactly the batch's bytes, with no padding and no
+// partial chunk except at the batch's end.
+bool dense_rows(const uint8_t* shards, size_t S, const Layout& L) {
+  return L.gstride == S && S % 16 != 0 && reinterpret_cast<uintptr_t>(shards) % 16 == 0 && L.rstride % 16 == 0 &&
+         S <= 0xffffffffu / 16;
+}
+
 int encode_dev(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, const Layout& L, hipStream_t s) {
   if (c->p == 0 || groups == 0) return UGO_FEC_OK;
+  if (groups > 1 && dense_rows(shards, S, L)) {
+    size_t k = 16;
+    while (S % (16 / k * 2) == 0) k /= 2;  // k = 16 / gcd(S, 16)
+    const size_t full = groups / k, tail = groups % k;
+    int st = full ? encode_dev(c, shards, full, k * S, Layout{L.rstride, k * S}, s) : UGO_FEC_OK;
+    if (st == UGO_FEC_OK && tail)  // one pseudo-group (its group stride is never used)
+      st = encode_dev(c, shards + full * k * S, 1, tail * S, Layout{L.rstride, round_up(tail * S, 16)}, s);
+    return st;
+  }
   const bool fast = fast_layout(c, shards, L, S);
   ugo::kern::Batch a = base_batch(c, shards, S, L);
   a.desc = c->d_encdesc;
@@ -405,7 +425,12 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
   if (groups == 0) return UGO_FEC_OK;
   if (!present) return UGO_FEC_ERR_INVALID_ARG;
   if (c->n > 64) return reconstruct_wide(c, shards, present, groups, S, L, flags, status, s, O, host_present);
-  const bool fast = fast_layout(c, shards, L, S) && fast_out(O);
+  // A dense planar batch (group stride == S) runs k_apply_pd: lanes on the
+  // rows' aligned 16-B chunks, the bytes of a chunk that straddles two groups
+  // split between two lanes.  That kernel's shape: d <= 16, p <= 4, S >= 1009.
+  const bool dense = dense_rows(shards, S, L) && ugo::kern::apply_dmax(c->d) > 0 &&
+                     ugo::kern::apply_dmax(c->d) <= 16 && c->epad == 4 && S >= ugo::kern::kDenseMinS;
+  const bool fast = (fast_layout(c, shards, L, S) && fast_out(O)) || dense;
   const int mode = c->d_table ? 1 : 2;
   ugo::kern::Batch a = base_batch(c, shards, S, L);
   a.out = O.base;
@@ -416,6 +441,9 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
   a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
   a.chunks = static_cast<uint32_t>(fast ? (S + 15) / 16 : (S + 3) / 4);
   size_t per = slice_groups(a.chunks, fast);
+  if (dense) {  // slices start on 16-B aligned bytes: a multiple of 16 / gcd(S, 16) groups
+    per = std::max<size_t>(16, per / 16 * 16);
+  }
   uint8_t* work = nullptr;
   if (mode == 2) {
     // per-group descriptors, bounded workspace (<= 64 Ki groups per slice)
@@ -454,8 +482,17 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
       a.desc = work;
       a.g_desc0 = g0;
     }
-    hipError_t e = fast ? ugo::kern::launch_apply(mode, ugo::kern::apply_dmax(c->d), a, s)
-                        : ugo::kern::launch_apply_bytes(mode, a, s);
+    hipError_t e;
+    if (dense) {
+      ugo::kern::Batch b = a;
+      b.base = shards + g0 * S;
+      b.n = static_cast<uint32_t>(gn);
+      b.items = static_cast<uint32_t>((gn * S + 15) / 16);
+      e = ugo::kern::launch_apply_dense(mode, ugo::kern::apply_dmax(c->d), b, s);
+    } else {
+      e = fast ? ugo::kern::launch_apply(mode, ugo::kern::apply_dmax(c->d), a, s)
+               : ugo::kern::launch_apply_bytes(mode, a, s);
+    }
     if (e != hipSuccess) return UGO_FEC_ERR_HIP;
   }
   return UGO_FEC_OK;
