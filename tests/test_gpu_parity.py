@@ -638,6 +638,51 @@ def test_dense_planar_rows_vs_oracle(gpu, d, p, S, G, table_max, monkeypatch):
     assert torch.equal(flat[outside], untouched[outside])
 
 
+@settings(max_examples=int(os.environ.get("UGO_HYP_EXAMPLES", "150")) // 5, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(d=st.integers(1, 16), p=st.integers(1, 4), S=st.integers(900, 2100), G=st.integers(1, 160),
+       table=st.sampled_from(["16", "0"]), seed=st.integers(0, 2**31 - 1))
+def test_random_dense_rows_vs_oracle(gpu, d, p, S, G, table, seed, monkeypatch):
+    """Random dense shard-major batches around the k_apply_pd threshold
+    (S >= 1009) and every pseudo-group fold (any S mod 16): encode, reconstruct
+    in place and into a dense output batch, bit-exact vs the oracle."""
+    monkeypatch.setenv("UGO_FEC_TABLE_MAX_SHARDS", table)
+    n = d + p
+    rs = (G * S + 15) // 16 * 16
+    rng = np.random.default_rng(seed)
+    packed = rng.integers(0, 256, (G, n, S), dtype=np.uint8)
+    want = packed.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    flat = torch.zeros((n * rs,), dtype=torch.uint8, device="cuda")
+    view = flat.as_strided((n, G, S), (rs, S, 1))
+    view.copy_(torch.as_tensor(packed).cuda().transpose(0, 1))
+    enc = fec.New(d, p)
+    enc.encode_batch(view, shard_size=S, shard_major=True)
+    assert np.array_equal(view.transpose(0, 1).cpu().numpy(), want)
+    masks = np.zeros(G, np.uint64)
+    for g in range(G):
+        m = (1 << n) - 1
+        for r in rng.choice(n, size=int(rng.integers(0, p + 2)), replace=False):
+            m &= ~(1 << int(r))
+        masks[g] = m
+    inp = _erase(want, masks, n)
+    exp = inp.copy()
+    rc, exp_st = rs_ref.c_reconstruct(d, p, exp, masks, S=S)
+    view.copy_(torch.as_tensor(inp).cuda().transpose(0, 1))
+    out = torch.full((p, G, S), 0xA5, dtype=torch.uint8, device="cuda")
+    st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    enc.reconstruct_into(view, _masks_to_dev(masks), out, shard_size=S, status=st, shard_major=True,
+                         out_shard_major=True)
+    assert np.array_equal(st.cpu().numpy(), exp_st)
+    o = out.transpose(0, 1).cpu().numpy()
+    for g in range(G):
+        er = [r for r in range(n) if not (int(masks[g]) >> r) & 1] if exp_st[g] == 0 else []
+        for i in range(p):
+            assert np.array_equal(o[g, i], exp[g, er[i]] if i < len(er) else np.full(S, 0xA5, np.uint8)), (g, i)
+    enc.reconstruct_batch(view, _masks_to_dev(masks), shard_size=S, shard_major=True)
+    assert np.array_equal(view.transpose(0, 1).cpu().numpy(), exp)
+
+
 def test_reconstruct_into_rejects_bad_outputs(gpu):
     d, p, S = 10, 3, 1350
     enc = fec.New(d, p)
