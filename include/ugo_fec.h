@@ -50,7 +50,7 @@ extern "C" {
 /* 4: ugo_fec_rx_assemble keeps the first copy of a seqid across calls into one
  *    batch too (a (group, row) already present at call entry is not written). */
 /* 5: ugo_fec_reconstruct_rows (row-pointer batches) and ugo_fec_device_address. */
-#define UGO_FEC_ABI_VERSION 5
+#define UGO_FEC_ABI_VERSION 6
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
  * that ugo/fec.go logs and swallows (ugo/fec.go:60-63, 208-210, 239-241). */
@@ -180,6 +180,21 @@ int ugo_fec_encode_host(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t sha
 int ugo_fec_reconstruct_host(ugo_fec* ctx, uint8_t* shards, const uint64_t* present,
                              size_t groups, size_t shard_size, size_t pitch, unsigned flags,
                              int8_t* status);
+
+/* ---- per-call latency service --------------------------------------------
+ * The drop-in route calls Encode once per group (calcECC, ugo/fec.go:238) and
+ * Reconstruct once per lossy group (input, ugo/fec.go:202).  Launched one by
+ * one, each call pays a kernel launch and a stream synchronize.  After
+ * ugo_fec_service_start, ugo_fec_encode_host / ugo_fec_reconstruct_host calls
+ * on PINNED group-major batches of <= 16 groups (shards and pitch multiples of
+ * 16; codes with d <= 16, p <= 4, and d + p <= 16 for reconstruct) are served
+ * by one resident workgroup polling a mailbox in pinned memory instead: no
+ * launch, no synchronize, same bytes and statuses.  The workgroup occupies one
+ * CU while it waits; it leaves after `idle_us` (0 = 2000) without a request
+ * and is relaunched by the next call.  Every other call takes the usual path.
+ * ugo_fec_service_stop (and ugo_fec_destroy) waits for it to leave. */
+int ugo_fec_service_start(ugo_fec* ctx, unsigned idle_us);
+int ugo_fec_service_stop(ugo_fec* ctx);
 
 /* ---- per-call validation shared with the Go shim ------------------------
  * checkShards(shards, nilok) [klauspost] over a list of n shard lengths:

@@ -1,0 +1,162 @@
+"""Per-call latency service (ugo_fec_service_start): small pinned host batches
+served by the resident k_service workgroup give the same bytes and statuses as
+the launch path and the oracle, across idle exits and relaunches, stops, and
+batches the service does not take.  Oracle = checker only.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import rs_ref
+from ugo_amd import fec
+
+pytestmark = pytest.mark.gpu
+
+
+def _pinned(G, n, pitch, rng):
+    buf = fec.host_alloc(G * n * pitch).reshape(G, n, pitch)
+    buf[:] = rng.integers(0, 256, (G, n, pitch), dtype=np.uint8)
+    return buf
+
+
+def _masks(G, n, p, rng):
+    m = np.zeros(G, np.uint64)
+    for g in range(G):
+        v = (1 << n) - 1
+        for r in rng.choice(n, size=int(rng.integers(0, p + 2)), replace=False):  # includes too-few-shards
+            v &= ~(1 << int(r))
+        m[g] = v
+    return m
+
+
+def _timed_launches(enc, fn):
+    enc.timing_begin(64)
+    fn()
+    times, untimed = enc.timing_end()
+    return len(times) + untimed
+
+
+@pytest.mark.parametrize("d,p,S,G", [(10, 3, 1470, 1), (10, 3, 1476, 1), (10, 3, 1350, 16), (4, 2, 17, 5),
+                                     (12, 4, 1000, 3), (16, 4, 64, 2), (10, 3, 1, 7), (1, 1, 1476, 2)])
+def test_service_encode_and_reconstruct_vs_oracle(gpu, d, p, S, G):
+    n = d + p
+    pitch = (S + 15) // 16 * 16
+    rng = np.random.default_rng(S * 7 + G + d)
+    enc = fec.New(d, p)
+    enc.service_start()
+    buf = _pinned(G, n, pitch, rng)
+    try:
+        want = buf.copy()
+        rs_ref.c_encode(d, p, want, S=S)
+        assert _timed_launches(enc, lambda: enc.encode_host(buf, S)) == 0  # served by the resident block
+        assert np.array_equal(buf[:, :, :S], want[:, :, :S])
+        assert np.array_equal(buf[:, :, S:], want[:, :, S:]), "padding written"
+        masks = _masks(G, n, p, rng)
+        for data_only in (False, True):
+            inp = want.copy()
+            for g in range(G):
+                for r in range(n):
+                    if not (int(masks[g]) >> r) & 1:
+                        inp[g, r, :S] = 0xEE
+            exp = inp.copy()
+            rc_want, st_want = rs_ref.c_reconstruct(d, p, exp, masks, S=S, data_only=data_only)
+            buf[:] = inp
+            st = np.full(G, -1, np.int8)
+            rc = None
+
+            def run():
+                nonlocal rc
+                rc = enc.reconstruct_host(buf, masks, S, data_only, st)
+            if n <= 16:
+                assert _timed_launches(enc, run) == 0
+            else:
+                run()
+            assert np.array_equal(st, st_want)
+            assert rc == (next((int(v) for v in st_want if v), 0))
+            assert np.array_equal(buf, exp)
+    finally:
+        enc.service_stop()
+        fec.host_free(buf.reshape(-1))
+        enc.close()
+
+
+def test_service_idle_exit_relaunch_and_stop(gpu):
+    """A short idle window: the block leaves between calls and the next call
+    relaunches it; many back-to-back calls keep one block; after stop, calls
+    take the launch path; batches over 16 groups never use the service."""
+    d, p, S = 10, 3, 1470
+    n, pitch = d + p, 1472
+    rng = np.random.default_rng(5)
+    enc = fec.New(d, p)
+    enc.service_start(idle_us=200)
+    bufs = [_pinned(1, n, pitch, rng), _pinned(40, n, pitch, rng)]
+    try:
+        for i in range(300):
+            b = bufs[0]
+            b[:] = rng.integers(0, 256, b.shape, dtype=np.uint8)
+            want = b.copy()
+            rs_ref.c_encode(d, p, want, S=S)
+            enc.encode_host(b, S)
+            assert np.array_equal(b[:, :, :S], want[:, :, :S]), i
+            if i % 50 == 7:
+                time.sleep(0.003)  # > idle: the block has left; the next call relaunches it
+        big = bufs[1]
+        want = big.copy()
+        rs_ref.c_encode(d, p, want, S=S)
+        assert _timed_launches(enc, lambda: enc.encode_host(big, S)) > 0  # 40 groups: launch path
+        assert np.array_equal(big[:, :, :S], want[:, :, :S])
+        enc.service_stop()
+        b = bufs[0]
+        want = b.copy()
+        rs_ref.c_encode(d, p, want, S=S)
+        assert _timed_launches(enc, lambda: enc.encode_host(b, S)) > 0  # stopped: launch path
+        assert np.array_equal(b[:, :, :S], want[:, :, :S])
+        enc.service_start()
+        enc.encode_host(b, S)  # restarted
+        assert np.array_equal(b[:, :, :S], want[:, :, :S])
+    finally:
+        enc.service_stop()
+        for b in bufs:
+            fec.host_free(b.reshape(-1))
+        enc.close()
+
+
+def test_service_serves_the_cgo_shim_sequence(gpu):
+    """The cgo shim's own call sequence (replayed by
+    test_cgo_shim_replay.GoShim: one pinned stage at the 16-B pitch, groups = 1)
+    with the service on: every Encode / Reconstruct / ReconstructData is served
+    without a launch, and the shards equal the oracle's and a launch-path
+    shim's call for call."""
+    from test_cgo_shim_replay import GoShim
+    d, p = 10, 3
+    rng = np.random.default_rng(9)
+    a, b = GoShim(d, p), GoShim(d, p)
+    assert a.lib.ugo_fec_service_start(a.ctx, 0) == 0
+    try:
+        for i in range(60):
+            S = (1470, 1476)[i % 2]
+            data = [bytearray(rng.integers(0, 256, S, dtype=np.uint8).tobytes()) for _ in range(d)]
+            sa = [bytearray(x) for x in data] + [bytearray(S) for _ in range(p)]
+            sb = [bytearray(x) for x in data] + [bytearray(S) for _ in range(p)]
+            a.timing_begin()
+            a.Encode(sa)
+            lost = rng.choice(d + p, size=int(rng.integers(1, p + 1)), replace=False)
+            ra = [None if r in lost else bytearray(x) for r, x in enumerate(sa)]
+            (a.ReconstructData if i % 3 == 1 else a.Reconstruct)(ra)
+            assert len(a.timing_end()) == 0, "a per-group call launched a kernel"
+            b.Encode(sb)
+            rb = [None if r in lost else bytearray(x) for r, x in enumerate(sb)]
+            (b.ReconstructData if i % 3 == 1 else b.Reconstruct)(rb)
+            assert sa == sb and ra == rb
+            g = np.zeros((1, d + p, S), np.uint8)
+            for k in range(d):
+                g[0, k] = np.frombuffer(bytes(data[k]), np.uint8)
+            rs_ref.c_encode(d, p, g)
+            assert [bytes(x) for x in sa] == [bytes(g[0, k]) for k in range(d + p)]
+            for r in range(d):
+                assert ra[r] == sa[r]
+    finally:
+        assert a.lib.ugo_fec_service_stop(a.ctx) == 0
+        a.close()
+        b.close()

@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "../include/ugo_fec.h"
@@ -204,17 +205,24 @@ int main(int argc, char** argv) {
       }
       report(name, t, "us per call (one group)");
     };
-    time_case("shim_encode_1470", PKT - 6, [&](auto& g) { check(shim.Encode(g), "shim encode"); });
-    time_case("shim_reconstruct_1476_1loss", PKT, [&](auto& g) {
-      auto w = g;
-      w[3].clear();
-      check(shim.reconstruct(w, 0), "shim reconstruct");
-    });
-    time_case("shim_reconstruct_data_1476_1loss", PKT, [&](auto& g) {
-      auto w = g;
-      w[3].clear();
-      check(shim.reconstruct(w, UGO_FEC_RECONSTRUCT_DATA_ONLY), "shim reconstruct data");
-    });
+    // then the same calls with the per-call service on (ugo_fec_service_start:
+    // a resident workgroup serves them, no launch and no synchronize per call)
+    for (int svc = 0; svc < 2; ++svc) {
+      if (svc) check(ugo_fec_service_start(shim.ctx, 0), "service_start");
+      const std::string pre = svc ? "svc_shim_" : "shim_";
+      time_case((pre + "encode_1470").c_str(), PKT - 6, [&](auto& g) { check(shim.Encode(g), "shim encode"); });
+      time_case((pre + "reconstruct_1476_1loss").c_str(), PKT, [&](auto& g) {
+        auto w = g;
+        w[3].clear();
+        check(shim.reconstruct(w, 0), "shim reconstruct");
+      });
+      time_case((pre + "reconstruct_data_1476_1loss").c_str(), PKT, [&](auto& g) {
+        auto w = g;
+        w[3].clear();
+        check(shim.reconstruct(w, UGO_FEC_RECONSTRUCT_DATA_ONLY), "shim reconstruct data");
+      });
+    }
+    check(ugo_fec_service_stop(shim.ctx), "service_stop");
     if (shim.stage) ugo_fec_host_free(shim.stage);
     ugo_fec_destroy(shim.ctx);
   }

@@ -683,6 +683,218 @@ __global__ __launch_bounds__(256) void k_apply_pd(Batch a) {
   if (wst) a.status[g] = 0;
 }
 
+// ---------------------------------------------------------------- per-call service
+// k_service: ONE block of 16 waves stays resident and serves the per-group
+// calls of the drop-in path (one Encode from calcECC, one Reconstruct per lossy
+// group from input: ugo/fec.go:202,238) from a mailbox in pinned host memory
+// (SvcBox, fec_kernels.hpp).  Thread 0 polls the request word with relaxed
+// system-scope loads and s_sleep, then ONE system-scope acquire; the block
+// reads the batch's rows over PCIe, applies the descriptor (the encode
+// descriptor, or the MODE-1 table entry of each group's presence mask) with
+// the same split-table products as k_apply_p, one group per wave at a time,
+// and writes the outputs back through the mapping.  Every wave drains its
+// stores, the block meets, and thread 0 releases at system scope and stores
+// done = seq.  Exit: idle_ticks without a request, or a stop request; `alive`
+// is cleared last.  All stores are vector stores.
+// Global-address-space 16-B access for the service: a flat access would also
+// count in lgkmcnt, so every scalar descriptor wait would wait for the PCIe
+// round trips of the loads before it.
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+
+__device__ __forceinline__ V4 gload16(const uint8_t* p) {
+  const u32x4 v = *(const g_u32x4*)(p);
+  return V4{{v.x, v.y, v.z, v.w}};
+}
+
+__device__ __forceinline__ void gstore16(uint8_t* p, const V4& y, uint32_t nb) {
+  if (nb >= 16) {
+    *(g_u32x4*)(p) = u32x4{y.v[0], y.v[1], y.v[2], y.v[3]};
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t lo = 4u * j;
+    if (nb >= lo + 4) {
+      *(g_u32*)(p + lo) = y.v[j];
+    } else if (nb > lo) {
+      const uint32_t w = y.v[j], rem = nb - lo;
+      *(g_u8*)(p + lo) = static_cast<uint8_t>(w);
+      if (rem >= 2) *(g_u8*)(p + lo + 1) = static_cast<uint8_t>(w >> 8);
+      if (rem >= 3) *(g_u8*)(p + lo + 2) = static_cast<uint8_t>(w >> 16);
+    }
+  }
+}
+
+// The service keeps its tables in LDS: the split-table words of all 256
+// coefficients (copied once at start) and, per slot (a group of the request,
+// or the encode slot copied at start), the descriptor itself.  A request's
+// descriptors are ONE round of parallel loads; every table lookup after that
+// is an LDS read, where reading them through the scalar cache would be a
+// chain of dependent loads per product.
+constexpr uint32_t kSvcDescWords = 32;  // descriptor bytes <= 128 (host: svc_eligible)
+template <int DMAX>
+struct SvcLds {
+  uint32_t mult[256][5];                         // split tables of every coefficient
+  uint32_t desc[kSvcMaxGroups + 1][kSvcDescWords];
+  uint32_t t[kSvcMaxGroups + 1][4][DMAX][5];     // per slot: tables of every (output, input) product
+};
+
+template <int DMAX>
+__device__ __forceinline__ void svc_copy_desc(SvcLds<DMAX>& L, uint32_t slot, const uint8_t* desc, uint32_t words,
+                                              uint32_t tid, uint32_t nthreads) {
+  for (uint32_t w = tid; w < words; w += nthreads) L.desc[slot][w] = *(const g_u32*)(desc + 4u * w);
+}
+
+// the slot's product tables from its descriptor copy and the LDS mult table
+template <int DMAX>
+__device__ __forceinline__ void svc_expand(SvcLds<DMAX>& L, uint32_t slot, const Batch& a, uint32_t tid,
+                                           uint32_t nthreads) {
+  for (uint32_t it = tid; it < 4u * DMAX * 5u; it += nthreads) {
+    const uint32_t q = it % 5u, k = (it / 5u) % DMAX, i = it / (5u * DMAX);
+    const uint32_t off = 4u + a.dpad + a.epad + i * a.dpad + k;
+    const uint32_t c = (L.desc[slot][off / 4u] >> (8u * (off & 3u))) & 0xffu;
+    L.t[slot][i][k][q] = L.mult[c][q];
+  }
+}
+
+constexpr uint32_t kSvcThreads = 512;  // 8 waves: 2 per SIMD, so DMAX 16 fits its registers
+
+template <int DMAX>
+__global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
+  static_assert(DMAX % 2 == 0, "inputs are taken in pairs");
+  __shared__ u32x4 line[4];                     // the request line
+  __shared__ uint64_t msk[kSvcMaxGroups];       // presence masks of a reconstruct
+  __shared__ SvcLds<DMAX> L;
+  constexpr uint32_t ENC = kSvcMaxGroups;  // the encode slot
+  SvcBox* box = sa.box;
+  const Batch& a = sa.a;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t dwords = a.desc_stride / 4u;
+  for (uint32_t w = threadIdx.x; w < 256u * 5u; w += kSvcThreads) L.mult[w / 5u][w % 5u] = a.mult[8u * (w / 5u) + w % 5u];
+  svc_copy_desc(L, ENC, sa.encdesc, dwords, threadIdx.x, kSvcThreads);
+  __syncthreads();
+  svc_expand(L, ENC, a, threadIdx.x, kSvcThreads);
+  uint32_t last = sa.start_seq;
+  uint64_t t0 = wall_clock64();
+  for (;;) {
+    if (wv == 0) {
+      // wave 0 polls the whole request line: lanes 0-3 one 16-B piece each
+      const volatile g_u32x4* src = (const volatile g_u32x4*)(box->line) + (lane & 3u);
+      u32x4 v;
+      bool stop = false;
+      for (;;) {
+        v = *src;
+        const uint32_t tq = __builtin_amdgcn_readlane(v.x, 0);
+        const bool ok = tq != last && tq == __builtin_amdgcn_readlane(v.x, 1) &&
+                        tq == __builtin_amdgcn_readlane(v.x, 2) && tq == __builtin_amdgcn_readlane(v.x, 3);
+        if (ok) break;
+        if (static_cast<uint64_t>(wall_clock64()) - t0 > sa.idle_ticks) {
+          stop = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (lane < 4u) {
+        if (lane == 0 && stop) v.y = kSvcStop;
+        line[lane] = v;
+      }
+      const uint32_t op = __builtin_amdgcn_readlane(v.y, 0), G = __builtin_amdgcn_readlane(v.z, 0);
+      if (!stop && op == kSvcReconstruct) {
+        if (lane == 0) {
+          msk[0] = static_cast<uint64_t>(__builtin_amdgcn_readlane(v.y, 3)) << 32 | __builtin_amdgcn_readlane(v.w, 2);
+          msk[1] = static_cast<uint64_t>(__builtin_amdgcn_readlane(v.w, 3)) << 32 | __builtin_amdgcn_readlane(v.z, 3);
+        }
+        if (lane >= 2u && lane < min(G, static_cast<uint32_t>(kSvcMaxGroups)))  // groups 2+: one more load
+          msk[lane] = *(const volatile __attribute__((address_space(1))) uint64_t*)(&box->present[lane]);
+      }
+    }
+    __syncthreads();
+    const uint32_t* rq = reinterpret_cast<const uint32_t*>(line);
+    const uint32_t sq = rq[0], op = rq[1];
+    if (op != kSvcEncode && op != kSvcReconstruct) break;
+    const uint32_t G = min(rq[2], static_cast<uint32_t>(kSvcMaxGroups)), S = rq[3];
+    uint8_t* base = reinterpret_cast<uint8_t*>(static_cast<uint64_t>(rq[6]) << 32 | rq[5]);
+    const uint64_t pitch = static_cast<uint64_t>(rq[10]) << 32 | rq[9];
+    const bool recon = op == kSvcReconstruct;
+    const uint32_t data_only = recon && (rq[7] & 1u);
+    if (recon) {  // this request's descriptors: one slot per group, a wave each
+      for (uint32_t g = wv; g < G; g += kSvcThreads / 64u) {
+        svc_copy_desc(L, g, a.desc + (msk[g] & a.nmask) * a.desc_stride, dwords, lane, 64u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        svc_expand(L, g, a, lane, 64u);
+      }
+      __syncthreads();
+    }
+    const uint32_t chunks = (S + 15u) / 16u, cpad = (chunks + 63u) & ~63u;
+    // groups wave-aligned: wave w takes 64 chunks of one group at a time
+    for (uint32_t w0 = wv * 64u; w0 < G * cpad; w0 += kSvcThreads) {
+      const uint32_t g = w0 / cpad;
+      const uint32_t c = w0 - g * cpad + lane;
+      const uint32_t slot = recon ? g : ENC;
+      const uint32_t* dw = L.desc[slot];
+      const uint32_t hdr = __builtin_amdgcn_readfirstlane(dw[0]);
+      const uint32_t st = (hdr >> 16) & 0xffu;
+      const uint32_t e = st ? 0u : (data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu));
+      if (recon && c == 0) *(g_u8*)(&box->status[g]) = static_cast<uint8_t>(st);
+      if (e == 0) continue;
+      uint8_t* gp = base + static_cast<uint64_t>(g) * a.n * pitch + static_cast<uint64_t>(c) * 16u;
+      V4 x[DMAX];
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) {
+        x[k] = V4{{0u, 0u, 0u, 0u}};
+        const uint32_t r = (__builtin_amdgcn_readfirstlane(dw[1 + (k >> 2)]) >> (8 * (k & 3))) & 0xffu;
+        if (k < static_cast<int>(a.d) && c < chunks) x[k] = gload16(gp + static_cast<uint64_t>(r) * pitch);
+      }
+      V4 acc[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
+#pragma unroll
+      for (int k = 0; k < DMAX; k += 2) {
+        if (k >= static_cast<int>(a.d)) continue;
+        uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
+        p_sel(x[k], s0, s1, s2);
+        p_sel(x[k + 1], r0, r1, r2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (i >= static_cast<int>(e)) continue;
+          const uint32_t* t = L.t[slot][i][k];
+          const uint32_t* u = L.t[slot][i][k + 1];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            uint32_t y = xor3(acc[i].v[j], perm(t[1], t[0], s0[j]), perm(t[3], t[2], s1[j]));
+            y = xor3(y, perm(0u, t[4], s2[j]), perm(u[1], u[0], r0[j]));
+            acc[i].v[j] = xor3(y, perm(u[3], u[2], r1[j]), perm(0u, u[4], r2[j]));
+          }
+        }
+      }
+      if (c < chunks) {
+        const uint32_t orows = __builtin_amdgcn_readfirstlane(dw[(4u + a.dpad) / 4u]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (i >= static_cast<int>(e)) continue;
+          const uint32_t r = (orows >> (8 * i)) & 0xffu;
+          gstore16(gp + static_cast<uint64_t>(r) * pitch, acc[i], S - c * 16u);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(&box->done, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    last = sq;
+    t0 = wall_clock64();
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&box->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Streaming form of k_apply_p for wide codes ((32,8) jumbo: d up to 255,
 // e <= EMAX outputs): inputs are not held -- a 4-deep ring of survivor
 // chunks is loaded ahead while the current pair is folded into EMAX live
@@ -1749,6 +1961,20 @@ hipError_t launch_apply_dense(int mode, int dmax, const Batch& a, hipStream_t s)
     case 2: return launch_apply_dense_mode<2>(dmax, a, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_service(int dmax, const SvcArgs& sa, hipStream_t s) {
+  if (sa.a.epad != 4) return hipErrorInvalidValue;
+  const dim3 grid(1), block(kSvcThreads);
+  switch (dmax) {  // never timed: it stays resident across calls
+    case 4: hipLaunchKernelGGL(k_service<4>, grid, block, 0, s, sa); break;
+    case 8: hipLaunchKernelGGL(k_service<8>, grid, block, 0, s, sa); break;
+    case 10: hipLaunchKernelGGL(k_service<10>, grid, block, 0, s, sa); break;
+    case 12: hipLaunchKernelGGL(k_service<12>, grid, block, 0, s, sa); break;
+    case 16: hipLaunchKernelGGL(k_service<16>, grid, block, 0, s, sa); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s) {

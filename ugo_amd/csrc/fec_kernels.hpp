@@ -67,6 +67,39 @@ constexpr uint32_t kDenseMinS = 63 * 16 + 1;
 hipError_t launch_apply_dense(int mode, int dmax, const Batch& a, hipStream_t s);
 
 
+// Per-call service (ugo_fec_service_*): one resident block polls a mailbox in
+// pinned host memory and runs each small group-major host batch it is handed
+// (zero-copy, through the descriptor path), so a per-group call costs neither
+// a launch nor a stream synchronize.  Protocol: the host fills the request,
+// then bumps seq; the block serves it, then stores done = seq.  The block
+// leaves after idle_ticks (100 MHz) without a request or on kSvcStop, and
+// clears `alive` as its last store; the host relaunches on its next request.
+constexpr int kSvcMaxGroups = 16;
+struct SvcBox {
+  // request line (host -> device): four 16-B pieces, each {tag, 3 words};
+  // the host writes every field, then the tags, then piece 0's tag (seq).
+  // The poll reads the whole line in one load and takes it when all four tags
+  // equal a new seq (a 16-B piece is read whole):
+  //   [0] seq  [1] op        [2] groups     [3] S
+  //   [4] tag  [5] shards lo [6] shards hi  [7] flags
+  //   [8] tag  [9] pitch lo  [10] pitch hi  [11] present[0] lo
+  //   [12] tag [13] present[0] hi [14] present[1] lo [15] present[1] hi
+  alignas(64) uint32_t line[16];
+  alignas(64) uint64_t present[kSvcMaxGroups];  // reconstruct: masks of groups 2 and up
+  alignas(64) uint32_t done;                     // device -> host
+  uint32_t alive;
+  int8_t status[kSvcMaxGroups];
+};
+enum : uint32_t { kSvcEncode = 1, kSvcReconstruct = 2, kSvcStop = 3 };
+struct SvcArgs {
+  Batch a;                  // d, dpad, epad, desc_stride, nmask, mult; a.desc = MODE-1 table
+  const uint8_t* encdesc;   // encode descriptor (MODE 0)
+  SvcBox* box;              // device view of the mailbox
+  uint64_t idle_ticks;
+  uint32_t start_seq;       // the last request already served
+};
+// dmax 4..16 (d <= 16) and p <= 4 (epad 4) only
+hipError_t launch_service(int dmax, const SvcArgs& sa, hipStream_t s);
 
 }  // namespace kern
 }  // namespace ugo

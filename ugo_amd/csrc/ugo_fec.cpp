@@ -11,6 +11,9 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -91,6 +94,13 @@ struct ugo_fec {
   // launch timing (ugo_fec_timing_begin/end)
   bool timing = false;
   ugo::kern::LaunchTimer timer;
+  // per-call service (ugo_fec_service_start): mailbox in coherent pinned memory
+  bool svc_on = false;
+  uint64_t svc_idle_ticks = 0;
+  ugo::kern::SvcBox* svc_box = nullptr;   // host address
+  ugo::kern::SvcBox* svc_dbox = nullptr;  // device view
+  hipStream_t svc_stream = nullptr;
+  uint32_t svc_seq = 0;
 };
 
 namespace {
@@ -175,9 +185,14 @@ int build_desc(const ugo_fec* c, uint64_t mask, uint8_t* out) { return build_des
 
 int hip_status(hipError_t e) { return e == hipSuccess ? UGO_FEC_OK : UGO_FEC_ERR_HIP; }
 
+int svc_stop(ugo_fec* c);
+
 void free_ctx(ugo_fec* c) {
   if (!c) return;
   DeviceGuard g(c->device);
+  (void)svc_stop(c);  // the resident block leaves before its mailbox goes
+  if (c->svc_stream) (void)hipStreamDestroy(c->svc_stream);
+  if (c->svc_box) (void)hipHostFree(c->svc_box);
   timer_release(c);
   (void)hipFree(c->d_M);
   (void)hipFree(c->d_gf);
@@ -586,6 +601,112 @@ int host_reconstruct_mapped(ugo_fec* c, uint8_t* mapped, const uint64_t* present
   return first;
 }
 
+// ---------------------------------------------------------------- per-call service
+// The resident k_service block (fec_kernels.hip) serves small pinned batches
+// from the context's mailbox: the host fills the request, bumps seq and spins
+// on done; a block that has left (idle, alive == 0) is relaunched on the
+// service stream, which also orders it after its predecessor.
+constexpr auto kSvcTimeout = std::chrono::seconds(5);
+
+template <typename T>
+T svc_ld(const T& v) { return __atomic_load_n(&v, __ATOMIC_ACQUIRE); }
+template <typename T>
+void svc_st(T& v, T x) { __atomic_store_n(&v, x, __ATOMIC_RELEASE); }
+
+int svc_launch(ugo_fec* c) {
+  ugo::kern::SvcArgs sa{};
+  sa.a = base_batch(c, nullptr, 0, Layout{0, 0});
+  sa.a.desc = c->d_table;
+  sa.a.n = static_cast<uint32_t>(c->n);
+  sa.encdesc = c->d_encdesc;
+  sa.box = c->svc_dbox;
+  sa.idle_ticks = c->svc_idle_ticks;
+  sa.start_seq = svc_ld(c->svc_box->done);
+  svc_st(c->svc_box->alive, 1u);
+  return hip_status(ugo::kern::launch_service(ugo::kern::apply_dmax(c->d), sa, c->svc_stream));
+}
+
+bool svc_eligible(const ugo_fec* c, const uint8_t* mapped, size_t groups, size_t pitch, bool recon) {
+  const int dm = ugo::kern::apply_dmax(c->d);
+  return c->svc_on && mapped && groups <= size_t(ugo::kern::kSvcMaxGroups) && pitch % 16 == 0 &&
+         reinterpret_cast<uintptr_t>(mapped) % 16 == 0 && dm > 0 && dm <= 16 && c->epad == 4 && c->p > 0 &&
+         c->desc_stride <= 128 &&
+         (!recon || c->d_table);
+}
+
+// Writes one request (layout: SvcBox::line): every field, then the pieces'
+// tags, then seq; returns seq.
+uint32_t svc_post(ugo_fec* c, uint32_t op, const uint8_t* mapped, size_t groups, size_t S, size_t pitch,
+                  unsigned flags, const uint64_t* present) {
+  ugo::kern::SvcBox* b = c->svc_box;
+  uint32_t* l = b->line;
+  const uint64_t sh = reinterpret_cast<uint64_t>(mapped);
+  const uint64_t m0 = present && groups > 0 ? present[0] : 0, m1 = present && groups > 1 ? present[1] : 0;
+  if (present && groups > 2) std::memcpy(b->present + 2, present + 2, (groups - 2) * sizeof(uint64_t));
+  l[1] = op;
+  l[2] = static_cast<uint32_t>(groups);
+  l[3] = static_cast<uint32_t>(S);
+  l[5] = static_cast<uint32_t>(sh);
+  l[6] = static_cast<uint32_t>(sh >> 32);
+  l[7] = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
+  l[9] = static_cast<uint32_t>(pitch);
+  l[10] = static_cast<uint32_t>(uint64_t(pitch) >> 32);
+  l[11] = static_cast<uint32_t>(m0);
+  l[13] = static_cast<uint32_t>(m0 >> 32);
+  l[14] = static_cast<uint32_t>(m1);
+  l[15] = static_cast<uint32_t>(m1 >> 32);
+  const uint32_t sq = ++c->svc_seq;
+  svc_st(l[4], sq);
+  svc_st(l[8], sq);
+  svc_st(l[12], sq);
+  svc_st(l[0], sq);  // release: everything above is visible first
+  return sq;
+}
+
+// One request: op on `groups` (<= kSvcMaxGroups) groups of the pinned
+// group-major batch at `mapped` (device view).  Statuses as the launch path.
+int svc_call(ugo_fec* c, uint32_t op, uint8_t* mapped, size_t groups, size_t S, size_t pitch, unsigned flags,
+             const uint64_t* present, int8_t* status) {
+  ugo::kern::SvcBox* b = c->svc_box;
+  if (!svc_ld(b->alive) && svc_launch(c) != UGO_FEC_OK) return UGO_FEC_ERR_HIP;
+  const uint32_t sq = svc_post(c, op, mapped, groups, S, pitch, flags, present);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0; svc_ld(b->done) != sq; ++spin) {
+    if (!svc_ld(b->alive)) {  // it left before it saw this request
+      if (svc_ld(b->done) == sq) break;
+      if (svc_launch(c) != UGO_FEC_OK) return UGO_FEC_ERR_HIP;
+    }
+    if ((spin & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > kSvcTimeout) {
+      (void)hipStreamQuery(c->svc_stream);
+      return UGO_FEC_ERR_HIP;
+    }
+    __builtin_ia32_pause();
+  }
+  if (op != ugo::kern::kSvcReconstruct) return UGO_FEC_OK;
+  int first = UGO_FEC_OK;
+  for (size_t g = 0; g < groups; ++g) {
+    const int8_t v = b->status[g];
+    if (status) status[g] = v;
+    if (v && !first) first = v;
+  }
+  return first;
+}
+
+int svc_stop(ugo_fec* c) {
+  if (!c->svc_box) return UGO_FEC_OK;
+  c->svc_on = false;
+  ugo::kern::SvcBox* b = c->svc_box;
+  if (svc_ld(b->alive)) {
+    (void)svc_post(c, ugo::kern::kSvcStop, nullptr, 0, 0, 0, 0, nullptr);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (svc_ld(b->alive)) {
+      if (std::chrono::steady_clock::now() - t0 > kSvcTimeout) return UGO_FEC_ERR_HIP;
+      __builtin_ia32_pause();
+    }
+  }
+  return hip_status(hipStreamSynchronize(c->svc_stream));
+}
+
 // Host path: chunks of stage_groups groups round-robin over kStreams streams:
 // H2D(chunk) -> kernel -> D2H(chunk) on one stream, chunks on different
 // streams overlap (copy engines in both directions + compute).
@@ -619,6 +740,9 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
       (void)hipGetLastError();  // pageable: clear the sticky lookup error
     }
   }
+  if (svc_eligible(c, mapped, groups, pitch, recon))
+    return svc_call(c, recon ? ugo::kern::kSvcReconstruct : ugo::kern::kSvcEncode, mapped, groups, S, pitch, flags,
+                    recon ? present : nullptr, status);
   if (recon && mapped) return host_reconstruct_mapped(c, mapped, present, groups, S, pitch, flags, status);
   // Encode of a small pinned batch (the per-group calls of the drop-in
   // reedsolomon::Encoder, calcECC): zero-copy too -- one launch reading the data
@@ -957,6 +1081,33 @@ int ugo_fec_device_address(const ugo_fec* c, const void* p, void** dev) {
   if (!q || !device_view(q)) return UGO_FEC_ERR_INVALID_ARG;
   *dev = const_cast<uint8_t*>(q);
   return UGO_FEC_OK;
+}
+
+int ugo_fec_service_start(ugo_fec* c, unsigned idle_us) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!c->svc_box) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, sizeof(ugo::kern::SvcBox), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
+    std::memset(p, 0, sizeof(ugo::kern::SvcBox));
+    c->svc_box = static_cast<ugo::kern::SvcBox*>(p);
+    c->svc_dbox = c->svc_box;
+    if (!device_view(c->svc_dbox)) return UGO_FEC_ERR_HIP;
+  }
+  if (!c->svc_stream && hipStreamCreateWithFlags(&c->svc_stream, hipStreamNonBlocking) != hipSuccess)
+    return UGO_FEC_ERR_HIP;
+  c->svc_idle_ticks = uint64_t(idle_us ? idle_us : 2000u) * 100u;  // wall_clock64: 100 MHz
+  c->svc_on = true;
+  return UGO_FEC_OK;
+}
+
+int ugo_fec_service_stop(ugo_fec* c) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  return svc_stop(c);
 }
 
 int ugo_fec_encode_host(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch) {

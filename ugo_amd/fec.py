@@ -125,6 +125,8 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_reconstruct_into.argtypes = [vp, vp, vp, sz, sz, sz, sz, vp, sz, sz, u, vp, vp]
     lib.ugo_fec_encode_host.argtypes = [vp, vp, sz, sz, sz]
     lib.ugo_fec_reconstruct_host.argtypes = [vp, vp, vp, sz, sz, sz, u, vp]
+    lib.ugo_fec_service_start.argtypes = [vp, u]
+    lib.ugo_fec_service_stop.argtypes = [vp]
     lib.ugo_fec_check_shards.argtypes = [i, vp, i, ctypes.POINTER(sz)]
     lib.ugo_fec_host_alloc.argtypes = [sz, ctypes.POINTER(vp)]
     lib.ugo_fec_host_free.argtypes = [vp]
@@ -396,6 +398,14 @@ class Encoder:
         return out[:n.value], untimed.value
 
     # ------------------------------------------------------ host-buffer batch
+    def service_start(self, idle_us: int = 0):
+        """Per-call latency service (ugo_fec_service_start): small pinned host
+        batches are served by a resident workgroup, no launch per call."""
+        _raise(load_library().ugo_fec_service_start(self._h, idle_us))
+
+    def service_stop(self):
+        _raise(load_library().ugo_fec_service_stop(self._h))
+
     def encode_host(self, shards: np.ndarray, shard_size: Optional[int] = None):
         _require(shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"] and shards.ndim == 3)
         G, n, pitch = shards.shape
