@@ -90,6 +90,13 @@ int ugo_fecconn_flush(ugo_fecconn* f, uint8_t* out, size_t out_cap, int* nrec, s
 /* Lossy groups staged and not yet recovered. */
 int ugo_fecconn_pending(const ugo_fecconn* f, size_t* groups);
 
+/* Per-call latency service on this object's encoder (ugo_fec_service_start,
+ * include/ugo_fec.h): calcECC's Encode and per-call recovery's Reconstruct are
+ * served by a resident workgroup instead of one launch + synchronize each.
+ * idle_us: how long it waits for the next call before leaving (0 = 2000);
+ * idle_us < 0 stops it (ugo_fecconn_free does too). */
+int ugo_fecconn_service(ugo_fecconn* f, int idle_us);
+
 /* len(fec.rx): packets held in the ordered receive queue. */
 int ugo_fecconn_rx_len(const ugo_fecconn* f, size_t* len);
 

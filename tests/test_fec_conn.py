@@ -84,14 +84,20 @@ def _channel(packets, rng, drop, dup, junk, reorder=4):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("full_len,drop,seed", [(True, 0.12, 1), (False, 0.12, 2), (False, 0.3, 3)])
-def test_fec_object_lockstep_with_reference_restatement(gpu, full_len, drop, seed):
+@pytest.mark.parametrize("full_len,drop,seed,service", [(True, 0.12, 1, False), (False, 0.12, 2, False),
+                                                         (False, 0.3, 3, False), (True, 0.12, 1, True),
+                                                         (False, 0.3, 3, True)])
+def test_fec_object_lockstep_with_reference_restatement(gpu, full_len, drop, seed, service):
+    """service: calcECC's Encode and the per-call Reconstruct served by the
+    resident workgroup (ugo_fecconn_service) -- the same bytes."""
     rng = np.random.default_rng(seed)
     now = [1_000_000]
     clock = lambda: now[0]  # noqa: E731
 
     # TX: C++ mirror (GPU parity) vs oracle restatement, byte for byte
     tx_c = fec.FecConn(RXLIMIT, D, P)
+    if service:
+        tx_c.service()
     tx_o = fec_ref.FEC.new(RXLIMIT, D, P, clock)
     pk_c, orig = _tx_stream(tx_c, 40, np.random.default_rng(seed), full_len)
     pk_o, _ = _tx_stream(tx_o, 40, np.random.default_rng(seed), full_len)
@@ -101,6 +107,8 @@ def test_fec_object_lockstep_with_reference_restatement(gpu, full_len, drop, see
     # RX over a lossy channel
     rx_c = fec.FecConn(RXLIMIT, D, P)
     rx_c.set_clock(clock)
+    if service:
+        rx_c.service(500)
     rx_o = fec_ref.FEC.new(RXLIMIT, D, P, clock)
     wire = _channel(pk_c, rng, drop=drop, dup=0.05, junk=0.02)
     recovered_total = 0

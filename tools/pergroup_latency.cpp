@@ -157,6 +157,15 @@ int main(int argc, char** argv) {
       t.push_back(us_since(t0));
     }
     report("calc_ecc", t, "us per call (one group)");
+    check(ugo_fecconn_service(f, 0), "service");
+    for (int i = 0; i < 200; ++i) check(ugo_fecconn_calc_ecc(f, ptrs.data(), lens.data(), N, 6, PKT), "calc_ecc");
+    t.clear();
+    for (int i = 0; i < reps; ++i) {
+      const auto t0 = clk::now();
+      check(ugo_fecconn_calc_ecc(f, ptrs.data(), lens.data(), N, 6, PKT), "calc_ecc");
+      t.push_back(us_since(t0));
+    }
+    report("svc_calc_ecc", t, "us per call (one group)");
     ugo_fecconn_free(f);
   }
 
@@ -229,11 +238,12 @@ int main(int argc, char** argv) {
 
   // input: lossless / lossy per call / lossy batched
   std::vector<uint8_t> out(size_t(4096) * D * PKT);
-  auto run = [&](const char* name, int drop, int batch, unsigned flags = 0) {
+  auto run = [&](const char* name, int drop, int batch, unsigned flags = 0, bool svc = false) {
     const int gpr = std::max(64, batch);  // groups per repetition
     const int nrep = std::max(10, reps / gpr);
     ugo_fecconn* f = nullptr;
     check(ugo_fecconn_new(RXLIMIT, D, P, 0, &f), "new");
+    if (svc) check(ugo_fecconn_service(f, 0), "service");
     int nrec = 0;
     size_t rl = 0;
     check(ugo_fecconn_set_batch_ex(f, batch, flags, out.data(), out.size(), &nrec, &rl), "set_batch");
@@ -280,6 +290,7 @@ int main(int argc, char** argv) {
   };
   run("input_lossless", -1, 0);
   run("input_lossy", 3, 0);
+  run("svc_input_lossy", 3, 0, 0, true);
   run("input_batch_16", 3, 16);
   run("input_batch_64", 3, 64);
   run("input_batch_256", 3, 256);

@@ -146,6 +146,11 @@ int ugo_fecconn_flush(ugo_fecconn* f, uint8_t* out, size_t out_cap, int* nrec, s
   return f->fec->lastError() == UGO_FEC_ERR_HIP ? UGO_FEC_ERR_HIP : UGO_FEC_OK;
 }
 
+int ugo_fecconn_service(ugo_fecconn* f, int idle_us) {
+  if (!f) return UGO_FEC_ERR_INVALID_ARG;
+  return f->fec->service(idle_us);
+}
+
 int ugo_fecconn_pending(const ugo_fecconn* f, size_t* groups) {
   if (!f || !groups) return UGO_FEC_ERR_INVALID_ARG;
   *groups = f->fec->pending();

@@ -93,6 +93,10 @@ class FEC {
   // most groups one input() / flush() can return in the current mode
   size_t maxReturnGroups(bool isFlush) const;
   size_t pending() const;
+  // Per-call latency service on this object's encoder (ugo_fec_service_start):
+  // calcECC's Encode and per-call recovery's Reconstruct are then served by a
+  // resident workgroup instead of a launch each.  idle_us < 0 stops it.
+  int service(int idle_us);
   ~FEC();
 
   // test / inspection hooks

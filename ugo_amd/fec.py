@@ -524,6 +524,7 @@ def _bind_conn(lib):
     lib.ugo_fecconn_set_batch_ex.argtypes = [vp, i, ctypes.c_uint, vp, sz, ctypes.POINTER(i), ctypes.POINTER(sz)]
     lib.ugo_fecconn_flush.argtypes = [vp, vp, sz, ctypes.POINTER(i), ctypes.POINTER(sz)]
     lib.ugo_fecconn_pending.argtypes = [vp, ctypes.POINTER(sz)]
+    lib.ugo_fecconn_service.argtypes = [vp, ctypes.c_int]
     lib._conn_bound = True
     return lib
 
@@ -619,6 +620,11 @@ class FecConn:
         _raise(self._lib.ugo_fecconn_flush(self._h, ctypes.addressof(self._out), len(self._out),
                                            ctypes.byref(nrec), ctypes.byref(rlen)))
         return self._recovered(nrec, rlen)
+
+    def service(self, idle_us: int = 0):
+        """Per-call latency service on this object's encoder (ugo_fecconn_service);
+        idle_us < 0 stops it."""
+        _raise(self._lib.ugo_fecconn_service(self._h, idle_us))
 
     def pending(self) -> int:
         v = ctypes.c_size_t()
