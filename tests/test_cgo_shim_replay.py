@@ -59,6 +59,9 @@ class GoShim:
             self.lib.ugo_fec_host_free(self.stage)
         self.lib.ugo_fec_destroy(self.ctx)
 
+    def ServiceStart(self, idle_us):  # func (e *Encoder) ServiceStart(idleUs uint) error
+        status_err(self.lib.ugo_fec_service_start(self.ctx, idle_us))
+
     def staging(self, n):  # func (e *Encoder) staging(n int) []byte
         if n > self.stageN:
             if self.stage:

@@ -132,7 +132,7 @@ def test_service_serves_the_cgo_shim_sequence(gpu):
     d, p = 10, 3
     rng = np.random.default_rng(9)
     a, b = GoShim(d, p), GoShim(d, p)
-    assert a.lib.ugo_fec_service_start(a.ctx, 0) == 0
+    a.ServiceStart(0)
     try:
         for i in range(60):
             S = (1470, 1476)[i % 2]
