@@ -192,7 +192,11 @@ int ugo_fec_reconstruct_host(ugo_fec* ctx, uint8_t* shards, const uint64_t* pres
  * launch, no synchronize, same bytes and statuses.  The workgroup occupies one
  * CU while it waits; it leaves after `idle_us` (0 = 2000) without a request
  * and is relaunched by the next call.  Every other call takes the usual path.
- * ugo_fec_service_stop (and ugo_fec_destroy) waits for it to leave. */
+ * While it is resident, a device-wide synchronize (hipDeviceSynchronize) waits
+ * for it to leave, i.e. up to idle_us after the last call.  A call the service
+ * cannot complete (a fault, or no answer within 5 s) returns UGO_FEC_ERR_HIP
+ * and turns the service off.  ugo_fec_service_stop (and ugo_fec_destroy)
+ * waits for it to leave. */
 int ugo_fec_service_start(ugo_fec* ctx, unsigned idle_us);
 int ugo_fec_service_stop(ugo_fec* ctx);
 

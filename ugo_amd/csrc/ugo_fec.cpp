@@ -623,7 +623,12 @@ int svc_launch(ugo_fec* c) {
   sa.idle_ticks = c->svc_idle_ticks;
   sa.start_seq = svc_ld(c->svc_box->done);
   svc_st(c->svc_box->alive, 1u);
-  return hip_status(ugo::kern::launch_service(ugo::kern::apply_dmax(c->d), sa, c->svc_stream));
+  if (ugo::kern::launch_service(ugo::kern::apply_dmax(c->d), sa, c->svc_stream) != hipSuccess) {
+    svc_st(c->svc_box->alive, 0u);
+    c->svc_on = false;  // later calls take the launch path
+    return UGO_FEC_ERR_HIP;
+  }
+  return UGO_FEC_OK;
 }
 
 bool svc_eligible(const ugo_fec* c, const uint8_t* mapped, size_t groups, size_t pitch, bool recon) {
@@ -676,8 +681,9 @@ int svc_call(ugo_fec* c, uint32_t op, uint8_t* mapped, size_t groups, size_t S, 
       if (svc_ld(b->done) == sq) break;
       if (svc_launch(c) != UGO_FEC_OK) return UGO_FEC_ERR_HIP;
     }
-    if ((spin & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > kSvcTimeout) {
-      (void)hipStreamQuery(c->svc_stream);
+    if ((spin & 1023u) == 0 &&
+        (hipStreamQuery(c->svc_stream) == hipErrorLaunchFailure || std::chrono::steady_clock::now() - t0 > kSvcTimeout)) {
+      c->svc_on = false;  // a faulted or silent block: later calls take the launch path
       return UGO_FEC_ERR_HIP;
     }
     __builtin_ia32_pause();
