@@ -160,3 +160,43 @@ def test_service_serves_the_cgo_shim_sequence(gpu):
         assert a.lib.ugo_fec_service_stop(a.ctx) == 0
         a.close()
         b.close()
+
+
+def test_service_two_contexts_from_two_threads(gpu):
+    """Two contexts (two connections), each with its own resident service
+    block, driven concurrently from two host threads: every call's parity is
+    the oracle's."""
+    import threading
+    d, p, S = 10, 3, 1470
+    n, pitch = d + p, 1472
+    errors = []
+
+    def worker(seed):
+        try:
+            rng = np.random.default_rng(seed)
+            enc = fec.New(d, p)
+            enc.service_start(300)
+            b = _pinned(2, n, pitch, rng)
+            try:
+                for i in range(150):
+                    b[:] = rng.integers(0, 256, b.shape, dtype=np.uint8)
+                    want = b.copy()
+                    rs_ref.c_encode(d, p, want, S=S)
+                    enc.encode_host(b, S)
+                    if not np.array_equal(b[:, :, :S], want[:, :, :S]):
+                        errors.append((seed, i))
+                        return
+            finally:
+                enc.service_stop()
+                fec.host_free(b.reshape(-1))
+                enc.close()
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append((seed, repr(ex)))
+
+    ts = [threading.Thread(target=worker, args=(s,)) for s in (11, 12)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors
