@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void k_apply_pd(Batch a) {
                        : gp + static_cast<uint64_t>(r) * a.rstride;
     if (lo)
       store16_from(p, acc[i], lo);
-    else
+    else  // (a partial chunk's stores take any byte address: an output batch of any layout)
       store16<NT>(p, acc[i], hi);
   }
   if (wst) a.status[g] = 0;

@@ -36,7 +36,8 @@ except Exception:  # pragma: no cover - torch is optional for the host-only path
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libugofec.so")
+# UGO_FEC_LIB: another build of the same library (interleaved A/B runs in tools/)
+LIB_PATH = os.environ.get("UGO_FEC_LIB") or os.path.join(_HERE, "libugofec.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ugo_fec.h")
 CONN_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ugo_fec_conn.h")
 PKT_HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "ugo_pkt.h")
