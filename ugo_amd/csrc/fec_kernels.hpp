@@ -72,7 +72,7 @@ hipError_t launch_apply_dense(int mode, int dmax, const Batch& a, hipStream_t s)
 // (zero-copy, through the descriptor path), so a per-group call costs neither
 // a launch nor a stream synchronize.  Protocol: the host fills the request,
 // then bumps seq; the block serves it, then stores done = seq.  The block
-// leaves after idle_ticks (100 MHz) without a request or on kSvcStop, and
+// leaves after idle_ticks (wall clock) without a request or on kSvcStop, and
 // clears `alive` as its last store; the host relaunches on its next request.
 constexpr int kSvcMaxGroups = 16;
 struct SvcBox {

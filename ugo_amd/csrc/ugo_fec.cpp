@@ -1104,7 +1104,9 @@ int ugo_fec_service_start(ugo_fec* c, unsigned idle_us) {
   }
   if (!c->svc_stream && hipStreamCreateWithFlags(&c->svc_stream, hipStreamNonBlocking) != hipSuccess)
     return UGO_FEC_ERR_HIP;
-  c->svc_idle_ticks = uint64_t(idle_us ? idle_us : 2000u) * 100u;  // wall_clock64: 100 MHz
+  int khz = 0;  // wall_clock64's rate (100 MHz on gfx950)
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
+  c->svc_idle_ticks = uint64_t(idle_us ? idle_us : 2000u) * uint64_t(khz) / 1000u;
   c->svc_on = true;
   return UGO_FEC_OK;
 }
