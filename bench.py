@@ -647,6 +647,85 @@ def host_path_leg(args, dev_index):
     return res
 
 
+def per_call_leg(args, dev_index):
+    """The drop-in route's latency (north_star: unchanged Encode / Reconstruct
+    signatures, ugo/fec.go:202,238): one (10+3) group per call, as the cgo shim
+    of INTEGRATION.md §2 makes it -- a pinned stage at the 16-B pitch, groups =
+    1 -- with the 1470-B calcECC window for Encode and ugo's 1476-B buffers and
+    one lost data shard for Reconstruct.  Each call is made through the C-ABI
+    (ctypes: ~1 us of Python call overhead included) 2,000 times after 200
+    untimed, median per call; first on the launch path, then with the per-call
+    service on (ugo_fec_service_start).  Verified: the service's parity and
+    rebuilt shard equal the launch path's."""
+    import ctypes
+
+    import numpy as np
+
+    from ugo_amd import fec
+
+    d, p = 10, 3
+    n = d + p
+    lib = fec.load_library()
+    enc = fec.New(d, p, device=dev_index)
+    res = {}
+    raw = fec.host_alloc(2 * n * 1488)
+    try:
+        rng = np.random.default_rng(args.seed + 5)
+
+        def median_us(call, reps=2000):
+            for _ in range(200):
+                assert call() == 0
+            ts = np.empty(reps)
+            for i in range(reps):
+                t0 = time.perf_counter_ns()
+                call()
+                ts[i] = time.perf_counter_ns() - t0
+            return round(float(np.median(ts)) / 1e3, 2)
+
+        mask = np.array([((1 << n) - 1) & ~(1 << 3)], np.uint64)
+        status = np.zeros(1, np.int8)
+        mp = ctypes.c_void_p(mask.ctypes.data)
+        sp = ctypes.c_void_p(status.ctypes.data)
+        src = {S: rng.integers(0, 256, (1, n, (S + 15) // 16 * 16), dtype=np.uint8) for S in (1470, 1476)}
+        outs = {}
+        for mode in ("launch", "service"):
+            if mode == "service":
+                enc.service_start()
+            row = {}
+            # Encode: the 1470-B calcECC window, parity rows zeroed first
+            S, P = 1470, 1472
+            g = raw[: n * P].reshape(1, n, P)
+            g[:] = src[S]
+            g[0, d:, :S] = 0
+            ptr = ctypes.c_void_p(g.ctypes.data)
+            row["encode_1470_us"] = median_us(lambda: lib.ugo_fec_encode_host(enc._h, ptr, 1, S, P))
+            enc_out = g.copy()
+            # Reconstruct: a 1476-B codeword with data shard 3 lost
+            S2, P2 = 1476, 1488
+            g2 = raw[n * 1488: n * 1488 + n * P2].reshape(1, n, P2)
+            g2[:] = src[S2]
+            ptr2 = ctypes.c_void_p(g2.ctypes.data)
+            assert lib.ugo_fec_encode_host(enc._h, ptr2, 1, S2, P2) == 0
+            want = g2[0, 3, :S2].copy()
+            g2[0, 3, :S2] = 0xEE
+            row["reconstruct_1476_1loss_us"] = median_us(
+                lambda: lib.ugo_fec_reconstruct_host(enc._h, ptr2, mp, 1, S2, P2, 0, sp))
+            row["rebuilt_ok"] = bool(np.array_equal(g2[0, 3, :S2], want))
+            outs[mode] = (enc_out, g2.copy())
+            res[mode] = row
+        enc.service_stop()
+        res["service"]["same_bytes_as_launch"] = all(
+            bool(np.array_equal(x, y)) for x, y in zip(outs["launch"], outs["service"]))
+    finally:
+        fec.host_free(raw)
+        enc.close()
+    res["note"] = ("one (10+3) group per call through the C-ABI from Python (ctypes), the cgo shim's staging: "
+                   "launch = one kernel launch + stream synchronize per call; service = ugo_fec_service_start "
+                   "(a resident workgroup polls a pinned mailbox); one GFNI CPU core: ~0.67 us Encode, ~0.48 us "
+                   "1-loss Reconstruct (DESIGN.md §4)")
+    return res
+
+
 def run_rank(args):
     import numpy as np
     import torch
@@ -762,6 +841,7 @@ def run_rank(args):
     torch.cuda.empty_cache()
     strong = strong_leg(args, enc, rank, world, dev, stream) if args.c4_total_groups > 0 else None
     host = host_path_leg(args, dev_index) if (world == 1 and not args.no_host_path) else None
+    per_call = per_call_leg(args, dev_index) if (world == 1 and not args.no_host_path) else None
 
     if rank == 0:
         payload = G * d * S  # klauspost's convention: data bytes per call (BASELINE.md secondary column)
@@ -816,6 +896,8 @@ def run_rank(args):
             out["strong_c4"] = strong
         if host is not None:
             out["host_path"] = host
+        if per_call is not None:
+            out["per_call"] = per_call
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, d, p, S, n)
         print(json.dumps(out), flush=True)
