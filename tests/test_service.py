@@ -200,3 +200,41 @@ def test_service_two_contexts_from_two_threads(gpu):
         t.join(timeout=60)
     assert not any(t.is_alive() for t in ts)
     assert not errors, errors
+
+
+@pytest.mark.parametrize("d,p,pinned", [(5, 5, True), (20, 4, True), (10, 3, False)])
+def test_service_declines_what_it_does_not_serve(gpu, d, p, pinned):
+    """p > 4, d > 16 (and d + p > 16: no host-built table to reconstruct
+    from), or a pageable batch: with the service on, the calls take the launch
+    path and return the oracle's bytes."""
+    n, S = d + p, 700
+    pitch = 704
+    rng = np.random.default_rng(d * 10 + p)
+    enc = fec.New(d, p)
+    enc.service_start()
+    buf = _pinned(3, n, pitch, rng) if pinned else rng.integers(0, 256, (3, n, pitch), dtype=np.uint8)
+    try:
+        want = buf.copy()
+        rs_ref.c_encode(d, p, want, S=S)
+        launches = _timed_launches(enc, lambda: enc.encode_host(buf, S))
+        assert launches > 0
+        assert np.array_equal(buf[:, :, :S], want[:, :, :S])
+        masks = _masks(3, n, p, rng)
+        inp = want.copy()
+        for g in range(3):
+            for r in range(n):
+                if not (int(masks[g]) >> r) & 1:
+                    inp[g, r, :S] = 0
+        buf[:] = inp
+        exp = inp.copy()
+        rc, st_want = rs_ref.c_reconstruct(d, p, exp, masks, S=S)
+        st = np.full(3, -1, np.int8)
+        launches = _timed_launches(enc, lambda: enc.reconstruct_host(buf, masks, S, False, st))
+        assert launches > 0
+        assert np.array_equal(st, st_want)
+        assert np.array_equal(buf, exp)
+    finally:
+        enc.service_stop()
+        if pinned:
+            fec.host_free(buf.reshape(-1))
+        enc.close()
