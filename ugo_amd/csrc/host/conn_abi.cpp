@@ -159,12 +159,7 @@ int ugo_fecconn_pending(const ugo_fecconn* f, size_t* groups) {
 
 int ugo_fecconn_calc_ecc(ugo_fecconn* f, uint8_t* const* bufs, const size_t* lens, int n, int offset, int maxlen) {
   if (!f || !bufs || !lens || n < 0) return UGO_FEC_ERR_INVALID_ARG;
-  std::vector<ugo::Bytes> data(n);
-  for (int k = 0; k < n; ++k) data[k].assign(bufs[k], bufs[k] + lens[k]);
-  auto ecc = f->fec->calcECC(data, offset, maxlen);
-  if (ecc.empty()) return f->fec->lastError() ? f->fec->lastError() : UGO_FEC_ERR_INVALID_ARG;
-  for (int k = f->fec->dataShards(); k < n; ++k) std::memcpy(bufs[k], data[k].data(), lens[k]);
-  return UGO_FEC_OK;
+  return f->fec->calcECC(bufs, lens, n, offset, maxlen);  // in place on the caller's packets
 }
 
 int ugo_fecconn_rx_len(const ugo_fecconn* f, size_t* len) {

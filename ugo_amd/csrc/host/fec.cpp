@@ -511,27 +511,26 @@ FEC::~FEC() {
   }
 }
 
+int FEC::calcECC(uint8_t* const* bufs, const size_t* lens, int n, int offset, int maxlen) {  // :228-243
+  if (n != shardSize_) return lastError_ = UGO_FEC_ERR_INVALID_ARG;  // "mismatch" logged upstream
+  if (offset < 0 || maxlen < offset) return lastError_ = UGO_FEC_ERR_INVALID_ARG;  // Go: slice bounds panic
+  uint8_t* rows[256];
+  for (int k = 0; k < n; ++k) {
+    if (lens[k] < static_cast<size_t>(maxlen)) return lastError_ = UGO_FEC_ERR_INVALID_ARG;  // slice bounds
+    rows[k] = bufs[k] + offset;
+  }
+  return lastError_ = enc_->EncodeWindows(rows, size_t(maxlen - offset));  // :238 -> GPU
+}
+
 std::vector<Bytes*> FEC::calcECC(std::vector<Bytes>& data, int offset, int maxlen) {  // :228-243
   std::vector<Bytes*> ecc;
-  if (static_cast<int>(data.size()) != shardSize_) {
-    lastError_ = UGO_FEC_ERR_INVALID_ARG;  // "mismatch" logged upstream
-    return ecc;
+  std::vector<uint8_t*> bufs(data.size());
+  std::vector<size_t> lens(data.size());
+  for (size_t k = 0; k < data.size(); ++k) {
+    bufs[k] = data[k].data();
+    lens[k] = data[k].size();
   }
-  if (offset < 0 || maxlen < offset) {  // Go: slice bounds panic
-    lastError_ = UGO_FEC_ERR_INVALID_ARG;
-    return ecc;
-  }
-  std::vector<uint8_t*> rows(shardSize_);
-  for (int k = 0; k < shardSize_; ++k) {
-    if (static_cast<int>(data[k].size()) < maxlen) {  // Go: slice bounds panic
-      lastError_ = UGO_FEC_ERR_INVALID_ARG;
-      return ecc;
-    }
-    rows[k] = data[k].data() + offset;
-  }
-  const int err = enc_->EncodeWindows(rows.data(), size_t(maxlen - offset));  // :238 -> GPU
-  lastError_ = err;
-  if (err != UGO_FEC_OK) return ecc;
+  if (calcECC(bufs.data(), lens.data(), static_cast<int>(data.size()), offset, maxlen) != UGO_FEC_OK) return ecc;
   for (int k = dataShards_; k < shardSize_; ++k) ecc.push_back(&data[k]);
   return ecc;
 }

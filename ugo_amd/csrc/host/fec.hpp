@@ -71,6 +71,9 @@ class FEC {
   // Parity over data[k][offset:maxlen]; returns pointers to data[d:], or empty
   // on error (length mismatch, window outside a buffer, Encode error).
   std::vector<Bytes*> calcECC(std::vector<Bytes>& data, int offset, int maxlen);
+  // The same over n caller buffers of lengths lens[] (the C-ABI's form: no
+  // copies of the packets), parity into bufs[d..n)[offset:maxlen); a status.
+  int calcECC(uint8_t* const* bufs, const size_t* lens, int n, int offset, int maxlen);
 
   // Batched recovery (a GPU extension; ugo has none).  With setBatch(n), n > 0,
   // input() does not Reconstruct a recoverable lossy group itself
