@@ -56,12 +56,13 @@ void null_args() {
 }
 
 // encode -> erase up to p rows -> reconstruct == original, host buffers
-void host_round_trip(int d, int p, size_t S, size_t G, bool pinned) {
+void host_round_trip(int d, int p, size_t S, size_t G, bool pinned, bool svc = false) {
   const int n = d + p;
   const size_t pitch = (S + 15) / 16 * 16 + (pinned ? 0 : 16);
   ugo_fec* ctx = nullptr;
   EXPECT(ugo_fec_create(0, d, p, &ctx) == UGO_FEC_OK);
   if (!ctx) return;
+  if (svc) EXPECT(ugo_fec_service_start(ctx, 300) == UGO_FEC_OK);  // the per-call service's host side
   const size_t bytes = G * n * pitch;
   uint8_t* buf = nullptr;
   std::vector<uint8_t> pageable;
@@ -93,6 +94,7 @@ void host_round_trip(int d, int p, size_t S, size_t G, bool pinned) {
     for (int r = 0; r < n && same; ++r)
       same = std::memcmp(buf + (g * n + r) * pitch, ref.data() + (g * n + r) * pitch, S) == 0;
   EXPECT(same);
+  if (svc) EXPECT(ugo_fec_service_stop(ctx) == UGO_FEC_OK);
   if (pinned) ugo_fec_host_free(buf);
   ugo_fec_destroy(ctx);
 }
@@ -140,7 +142,7 @@ void host_round_trip_wide(int d, int p, size_t S, size_t G, bool pinned) {
 // the FEC object: TX by markData / calcECC / markFEC over reused buffers, RX
 // over a lossy, duplicating channel per call and batched -- same recovered
 // sequence, and every lost full-length payload comes back
-void fec_object(int batch, unsigned flags = 0) {
+void fec_object(int batch, unsigned flags = 0, bool svc = false) {
   const int d = 10, p = 3, n = 13;
   const size_t L = UGO_FEC_MAX_PACKET;
   ugo_fecconn *tx = nullptr, *rx1 = nullptr, *rx2 = nullptr;
@@ -148,6 +150,10 @@ void fec_object(int batch, unsigned flags = 0) {
   EXPECT(ugo_fecconn_new(128, d, p, 0, &rx1) == UGO_FEC_OK);
   EXPECT(ugo_fecconn_new(128, d, p, 0, &rx2) == UGO_FEC_OK);
   if (!tx || !rx1 || !rx2) return;
+  if (svc) {  // calcECC and rx1's per-call recovery through the per-call service
+    EXPECT(ugo_fecconn_service(tx, 0) == UGO_FEC_OK);
+    EXPECT(ugo_fecconn_service(rx1, 300) == UGO_FEC_OK);
+  }
   std::vector<uint8_t> out1(size_t(batch + 1) * d * L), out2(size_t(2 * batch + 1) * d * L);
   int nrec = 0;
   size_t rl = 0;
@@ -294,10 +300,14 @@ int main() {
     host_round_trip_wide(70, 10, 64, 5, pinned);
     host_round_trip_wide(8, 120, 48, 3, pinned);
   }
+  host_round_trip(10, 3, 1470, 1, true, true);
+  host_round_trip(10, 3, 1476, 16, true, true);
+  host_round_trip(4, 2, 77, 7, true, true);
   fec_object(1);
   fec_object(16);
   fec_object(3, UGO_FECCONN_BATCH_OVERLAP);
   fec_object(16, UGO_FECCONN_BATCH_OVERLAP);
+  fec_object(4, 0, true);
   tx_rx_batch();
   std::printf("{\"asan_driver\": \"%s\", \"failures\": %d}\n", failures ? "FAIL" : "ok", failures);
   return failures ? 1 : 0;
