@@ -536,8 +536,7 @@ std::vector<Bytes*> FEC::calcECC(std::vector<Bytes>& data, int offset, int maxle
 }
 
 int FEC::service(int idle_us) {
-  return idle_us < 0 ? ugo_fec_service_stop(enc_->handle())
-                     : ugo_fec_service_start(enc_->handle(), static_cast<unsigned>(idle_us));
+  return idle_us < 0 ? enc_->ServiceStop() : enc_->ServiceStart(static_cast<unsigned>(idle_us));
 }
 
 }  // namespace ugo

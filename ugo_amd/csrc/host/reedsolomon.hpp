@@ -38,6 +38,12 @@ class Encoder {
   int ReconstructBatch(uint8_t* batch, const uint64_t* present, size_t groups, size_t shard_size,
                        size_t pitch, unsigned flags, int8_t* status);
 
+  // Per-call latency service (ugo_fec_service_start): the one-group Encode /
+  // Reconstruct calls above are served by a resident workgroup, no launch
+  // each (the cgo shim's ServiceStart).
+  int ServiceStart(unsigned idle_us = 0) { return ugo_fec_service_start(ctx_, idle_us); }
+  int ServiceStop() { return ugo_fec_service_stop(ctx_); }
+
   int DataShards() const { return d_; }
   int ParityShards() const { return p_; }
   int Shards() const { return d_ + p_; }

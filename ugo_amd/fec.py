@@ -208,6 +208,9 @@ class Encoder:
         if getattr(self, "_h", None):
             load_library().ugo_fec_destroy(self._h)
             self._h = None
+        if getattr(self, "_stage_buf", None) is not None:
+            host_free(self._stage_buf)
+            self._stage_buf = None
 
     def __del__(self):  # pragma: no cover
         try:
@@ -435,17 +438,30 @@ class Encoder:
         return rc
 
     # ------------------------------------------- Go-shaped, one group per call
+    def _stage(self, S: int) -> np.ndarray:
+        """One pinned group [d+p][P] at the 16-B pitch P, reused across calls
+        (the cgo shim's staging): the vector kernels, and the
+        per-call service when it is on, serve it."""
+        P = (S + 15) // 16 * 16
+        need = self.Shards * P
+        st = getattr(self, "_stage_buf", None)
+        if st is None or st.size < need:
+            if st is not None:
+                host_free(st)
+            st = self._stage_buf = host_alloc(max(need, self.Shards * 1488))
+        return st[:need].reshape(1, self.Shards, P)
+
     def Encode(self, shards: List[bytearray]) -> None:
         """reedsolomon Encode: parity shards written in place (ugo/fec.go:238)."""
         if len(shards) != self.Shards:
             raise ErrTooFewShards(strerror(ErrTooFewShards.code))
         S = check_shards([len(s) for s in shards], nil_ok=False)
-        buf = np.zeros((1, self.Shards, S), np.uint8)
+        buf = self._stage(S)
         for k in range(self.DataShards):
-            buf[0, k] = np.frombuffer(bytes(shards[k]), np.uint8)
+            buf[0, k, :S] = np.frombuffer(bytes(shards[k]), np.uint8)
         self.encode_host(buf, S)
         for k in range(self.DataShards, self.Shards):
-            shards[k][:] = buf[0, k].tobytes()
+            shards[k][:] = buf[0, k, :S].tobytes()
 
     def _reconstruct(self, shards: list, data_only: bool) -> None:
         if len(shards) != self.Shards:
@@ -453,18 +469,18 @@ class Encoder:
         lens = [0 if s is None else len(s) for s in shards]
         S = check_shards(lens, nil_ok=True)
         mask = np.zeros(self.mask_words, np.uint64)
-        buf = np.zeros((1, self.Shards, S), np.uint8)
+        buf = self._stage(S)
         for r, s in enumerate(shards):
             if lens[r]:
                 mask[r >> 6] |= np.uint64(1 << (r & 63))
-                buf[0, r] = np.frombuffer(bytes(s), np.uint8)
+                buf[0, r, :S] = np.frombuffer(bytes(s), np.uint8)
         status = np.zeros(1, np.int8)
         rc = self.reconstruct_host(buf, mask, S, data_only, status)
         _raise(rc)
         limit = self.DataShards if data_only else self.Shards
         for r in range(limit):
             if not lens[r]:
-                shards[r] = bytearray(buf[0, r].tobytes())
+                shards[r] = bytearray(buf[0, r, :S].tobytes())
 
     def Reconstruct(self, shards: list) -> None:
         """reedsolomon Reconstruct (ugo/fec.go:202): fills every missing shard."""
