@@ -190,8 +190,8 @@ int ugo_fec_reconstruct_host(ugo_fec* ctx, uint8_t* shards, const uint64_t* pres
  * 16; codes with d <= 16, p <= 4, and d + p <= 16 for reconstruct) are served
  * by one resident workgroup polling a mailbox in pinned memory instead: no
  * launch, no synchronize, same bytes and statuses.  The workgroup occupies one
- * CU while it waits; it leaves after `idle_us` (0 = 2000) without a request
- * and is relaunched by the next call.  Every other call takes the usual path.
+ * CU while it waits; it leaves after `idle_us` (0 = 2000, at most 1000000)
+ * without a request and is relaunched by the next call.  Every other call takes the usual path.
  * While it is resident, a device-wide synchronize (hipDeviceSynchronize) waits
  * for it to leave, i.e. up to idle_us after the last call.  A call the service
  * cannot complete (a fault, or no answer within 5 s) returns UGO_FEC_ERR_HIP

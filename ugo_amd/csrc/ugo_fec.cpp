@@ -1106,7 +1106,10 @@ int ugo_fec_service_start(ugo_fec* c, unsigned idle_us) {
     return UGO_FEC_ERR_HIP;
   int khz = 0;  // wall_clock64's rate (100 MHz on gfx950)
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
-  c->svc_idle_ticks = uint64_t(idle_us ? idle_us : 2000u) * uint64_t(khz) / 1000u;
+  // at most 1 s resident after the last call: a process that exits without
+  // ugo_fec_destroy leaves no long-running wave behind
+  const uint64_t us = std::min<uint64_t>(idle_us ? idle_us : 2000u, 1000000u);
+  c->svc_idle_ticks = us * uint64_t(khz) / 1000u;
   c->svc_on = true;
   return UGO_FEC_OK;
 }
