@@ -610,6 +610,14 @@ constexpr auto kSvcTimeout = std::chrono::seconds(5);
 
 template <typename T>
 T svc_ld(const T& v) { return __atomic_load_n(&v, __ATOMIC_ACQUIRE); }
+
+inline void svc_relax() {  // one spin of the host's wait on the mailbox
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#else
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#endif
+}
 template <typename T>
 void svc_st(T& v, T x) { __atomic_store_n(&v, x, __ATOMIC_RELEASE); }
 
@@ -686,7 +694,7 @@ int svc_call(ugo_fec* c, uint32_t op, uint8_t* mapped, size_t groups, size_t S, 
       c->svc_on = false;  // a faulted or silent block: later calls take the launch path
       return UGO_FEC_ERR_HIP;
     }
-    __builtin_ia32_pause();
+    svc_relax();
   }
   if (op != ugo::kern::kSvcReconstruct) return UGO_FEC_OK;
   int first = UGO_FEC_OK;
@@ -707,7 +715,7 @@ int svc_stop(ugo_fec* c) {
     const auto t0 = std::chrono::steady_clock::now();
     while (svc_ld(b->alive)) {
       if (std::chrono::steady_clock::now() - t0 > kSvcTimeout) return UGO_FEC_ERR_HIP;
-      __builtin_ia32_pause();
+      svc_relax();
     }
   }
   return hip_status(hipStreamSynchronize(c->svc_stream));
