@@ -70,6 +70,8 @@ def parse(argv=None):
     ap.add_argument("--pitch", type=int, default=0, help="row pitch in HBM (default: shard size rounded to 16)")
     ap.add_argument("--out-pitch", type=int, default=0,
                     help="row pitch of the reconstruct_into output batch (default: the batch pitch)")
+    ap.add_argument("--out-layout", choices=["planar", "grouped"], default="planar",
+                    help="reconstruct_into output batch: planar [p][G][pitch] or grouped [G][p][pitch]")
     ap.add_argument("--erasures", type=int, default=2)
     ap.add_argument("--batches", type=int, default=2,
                     help="rotate the steps over this many independent batches per GPU (step k works on batch "
@@ -767,7 +769,9 @@ def run_rank(args):
     into = args.decode == "into"
     # one output batch per input batch, so every step's outputs are cold too
     opitch = args.out_pitch or pitch
-    outs = [torch.zeros((p, G, opitch), dtype=torch.uint8, device=dev) for _ in range(nb)] if into else None
+    oplanar = args.out_layout == "planar"
+    oshape = (p, G, opitch) if oplanar else (G, p, opitch)
+    outs = [torch.zeros(oshape, dtype=torch.uint8, device=dev) for _ in range(nb)] if into else None
     stream = torch.cuda.current_stream()
     cur = [0]
 
@@ -777,7 +781,8 @@ def run_rank(args):
         cur[0] += 1
         enc.encode_batch(b, shard_size=S, stream=stream, shard_major=planar)
         if into:
-            enc.reconstruct_into(b, masks, outs[i], shard_size=S, stream=stream, shard_major=planar)
+            enc.reconstruct_into(b, masks, outs[i], shard_size=S, stream=stream, shard_major=planar,
+                                 out_shard_major=oplanar)
         else:
             enc.reconstruct_batch(b, masks, shard_size=S, stream=stream, shard_major=planar)
 
