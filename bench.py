@@ -846,7 +846,12 @@ def run_rank(args):
     torch.cuda.empty_cache()
     strong = strong_leg(args, enc, rank, world, dev, stream) if args.c4_total_groups > 0 else None
     host = host_path_leg(args, dev_index) if (world == 1 and not args.no_host_path) else None
-    per_call = per_call_leg(args, dev_index) if (world == 1 and not args.no_host_path) else None
+    per_call = None
+    if world == 1 and not args.no_host_path:
+        try:  # a secondary leg: a failure here is reported in the line, never loses it
+            per_call = per_call_leg(args, dev_index)
+        except Exception as ex:  # noqa: BLE001
+            per_call = {"error": repr(ex)[:300]}
 
     if rank == 0:
         payload = G * d * S  # klauspost's convention: data bytes per call (BASELINE.md secondary column)
