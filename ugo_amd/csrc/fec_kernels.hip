@@ -1804,8 +1804,14 @@ static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
 // ONE batch back to back instead (a warm loop) favours plain stores by 3-5%,
 // because the Infinity Cache then absorbs the rewritten parity lines.
 constexpr int kEncNT = 3;    // nontemporal loads and stores
-constexpr int kEncLdsRows = 8;  // (10,3): rows 0-7 by LDS-DMA nt, 8-9 to registers
-constexpr int kEncStageRows = 13;  // (10,3): 52-KiB stage, 3 blocks per CU (see k_encode_g)
+#ifndef UGO_ENC_LDS_ROWS  // A/B builds only (tools/bench_ab.sh with UGO_FEC_LIB)
+#define UGO_ENC_LDS_ROWS 8
+#endif
+#ifndef UGO_ENC_STAGE_ROWS
+#define UGO_ENC_STAGE_ROWS 13
+#endif
+constexpr int kEncLdsRows = UGO_ENC_LDS_ROWS;  // (10,3): rows 0-7 by LDS-DMA nt, 8-9 to registers
+constexpr int kEncStageRows = UGO_ENC_STAGE_ROWS;  // (10,3): 52-KiB stage, 3 blocks per CU (see k_encode_g)
 constexpr int kEncJumboNT = 3;  // (32,8): NT loads and stores (578 vs 615 us, tools/jvariants.hip)
 // (32,8): the network in Four-Russians form with the dwords in sequence
 // (k_encode_frs), rows 0-15 by LDS-DMA nt and read from LDS one dword at a
