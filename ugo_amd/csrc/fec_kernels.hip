@@ -759,6 +759,9 @@ __device__ __forceinline__ void svc_expand(SvcLds<DMAX>& L, uint32_t slot, const
   }
 }
 
+#ifndef UGO_SVC_SLEEP  // the poll's s_sleep between reads of the request line (A/B builds only)
+#define UGO_SVC_SLEEP 1
+#endif
 constexpr uint32_t kSvcThreads = 512;  // 8 waves: 2 per SIMD, so DMAX 16 fits its registers
 
 template <int DMAX>
@@ -795,7 +798,7 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
           stop = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(UGO_SVC_SLEEP);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       if (lane < 4u) {
