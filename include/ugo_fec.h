@@ -50,7 +50,10 @@ extern "C" {
 /* 4: ugo_fec_rx_assemble keeps the first copy of a seqid across calls into one
  *    batch too (a (group, row) already present at call entry is not written). */
 /* 5: ugo_fec_reconstruct_rows (row-pointer batches) and ugo_fec_device_address. */
-#define UGO_FEC_ABI_VERSION 6
+/* 6: the per-call service (ugo_fec_service_start / _stop). */
+/* 7: ugo_fec_service_config, ugo_fec_poisoned; rx_assemble places packets in
+ *    destination order (index + gather) -- same results. */
+#define UGO_FEC_ABI_VERSION 7
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
  * that ugo/fec.go logs and swallows (ugo/fec.go:60-63, 208-210, 239-241). */
@@ -193,12 +196,27 @@ int ugo_fec_reconstruct_host(ugo_fec* ctx, uint8_t* shards, const uint64_t* pres
  * CU while it waits; it leaves after `idle_us` (0 = 2000, at most 1000000)
  * without a request and is relaunched by the next call.  Every other call takes the usual path.
  * While it is resident, a device-wide synchronize (hipDeviceSynchronize) waits
- * for it to leave, i.e. up to idle_us after the last call.  A call the service
- * cannot complete (a fault, or no answer within 5 s) returns UGO_FEC_ERR_HIP
- * and turns the service off.  ugo_fec_service_stop (and ugo_fec_destroy)
- * waits for it to leave. */
+ * for it to leave, i.e. up to idle_us after the last call.
+ * Failure: a call the service cannot complete (a GPU fault, or no answer
+ * within the watchdog timeout, 5 s by default) turns the service off, asks the
+ * workgroup to leave and waits up to the grace period (5 s by default) for it
+ * to be gone, so it can no longer write into the caller's batch; then the call
+ * returns UGO_FEC_ERR_HIP and later calls take the launch path.  If the
+ * workgroup is still resident after the grace period, the context is
+ * POISONED: every later call on it returns UGO_FEC_ERR_HIP, and
+ * ugo_fec_destroy frees nothing the workgroup reads (its mailbox and tables
+ * are leaked); the caller must then keep the timed-out call's batch alive.
+ * ugo_fec_service_stop (and ugo_fec_destroy) waits the same way. */
 int ugo_fec_service_start(ugo_fec* ctx, unsigned idle_us);
 int ugo_fec_service_stop(ugo_fec* ctx);
+/* Watchdog of the service: timeout_ms a call waits for an answer (0 = 5000),
+ * grace_ms it then waits for the workgroup to leave (0 = 5000).
+ * test_stall_us (tests only; normally 0): the workgroup waits that long before
+ * serving each request, from its next launch on, so a test can drive the
+ * timeout and poison paths. */
+int ugo_fec_service_config(ugo_fec* ctx, unsigned timeout_ms, unsigned grace_ms, unsigned test_stall_us);
+/* 1 if the context is poisoned (see above), 0 if not. */
+int ugo_fec_poisoned(const ugo_fec* ctx);
 
 /* ---- per-call validation shared with the Go shim ------------------------
  * checkShards(shards, nilok) [klauspost] over a list of n shard lengths:
@@ -306,7 +324,9 @@ int ugo_fec_timing_end(ugo_fec* ctx, ugo_fec_launch_time* out, size_t cap, size_
                        size_t* n_untimed);
 
 /* ---- helpers ------------------------------------------------------------- */
-int ugo_fec_host_alloc(size_t bytes, void** out);  /* pinned host memory */
+/* pinned host memory; tests may set UGO_FEC_HOST_ALLOC_LIMIT=<bytes> in the
+ * environment to make larger requests fail (fault injection) */
+int ugo_fec_host_alloc(size_t bytes, void** out);
 int ugo_fec_host_free(void* p);
 const char* ugo_fec_strerror(int status);
 int ugo_fec_abi_version(void);

@@ -351,3 +351,48 @@ def test_calc_ecc_random_windows(gpu, d, p, offset, width, buflen, seed):
     else:
         f.calcECC(bufs, offset, maxlen)
     assert bufs == ref
+
+
+@pytest.mark.gpu
+def test_set_batch_allocation_failure_falls_back_to_per_call(gpu, monkeypatch):
+    """a set_batch whose pinned batch cannot be allocated (fault
+    injected: UGO_FEC_HOST_ALLOC_LIMIT) fails with ErrHip and leaves the object
+    in per-call mode -- it never keeps pointing at a freed batch.  Before and
+    after, input recovers exactly what the reference restatement recovers
+    (pending groups of the old batch come back first)."""
+    rng = np.random.default_rng(41)
+    tx = fec_ref.FEC.new(RXLIMIT, D, P, clock=lambda: 0)
+    pk, _ = _tx_stream(tx, 12, np.random.default_rng(41), False)
+    rx_o = fec_ref.FEC.new(RXLIMIT, D, P, clock=lambda: 0)
+    rx_b = fec.FecConn(RXLIMIT, D, P)
+    rx_b.set_clock(lambda: 0)
+    rx_b.set_batch(4)
+    got, want = [], []
+
+    def feed(groups):
+        for g in groups:
+            for k, pkt in enumerate(pk[g * N:(g + 1) * N]):
+                if k == g % D:
+                    continue
+                _, _, rb = rx_b.input(pkt)
+                got.extend(bytes(x) for x in rb or [])
+                want.extend(bytes(x) for x in fec_ref.handle(rx_o, pkt)[2] or [])
+
+    feed(range(0, 6))  # one full batch of 4 came back, 2 pending
+    assert rx_b.pending() == 2
+    monkeypatch.setenv("UGO_FEC_HOST_ALLOC_LIMIT", "4096")
+    import ctypes
+    lib = fec._bind_conn(fec.load_library())
+    nrec, rlen = ctypes.c_int(), ctypes.c_size_t()
+    st = lib.ugo_fecconn_set_batch_ex(rx_b._h, 8, 0, ctypes.addressof(rx_b._out), len(rx_b._out),
+                                      ctypes.byref(nrec), ctypes.byref(rlen))
+    assert st == fec.ErrHip.code
+    got.extend(bytes(x) for x in rx_b._recovered(nrec, rlen) or [])  # the 2 pending groups, flushed first
+    monkeypatch.delenv("UGO_FEC_HOST_ALLOC_LIMIT")
+    assert rx_b.pending() == 0
+    n_before = len(got)
+    feed(range(6, 12))  # per-call mode now: every lossy group comes back at once
+    assert rx_b.pending() == 0
+    assert len(got) == n_before + 6
+    assert got == want and len(want) == 12
+    del rng

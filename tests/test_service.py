@@ -238,3 +238,102 @@ def test_service_declines_what_it_does_not_serve(gpu, d, p, pinned):
         if pinned:
             fec.host_free(buf.reshape(-1))
         enc.close()
+
+
+def test_service_restart_while_alive(gpu):
+    """stop and restart the service while its block is resident
+    (long idle window), many times: a relaunched block must never take the
+    stop request still on the mailbox line, nor an older request, for a new
+    one -- every call after a restart is served (no launch) with the right
+    bytes."""
+    d, p, S = 10, 3, 1470
+    n, pitch = d + p, 1472
+    rng = np.random.default_rng(17)
+    enc = fec.New(d, p)
+    b = _pinned(1, n, pitch, rng)
+    try:
+        for i in range(60):
+            enc.service_start(idle_us=1_000_000)
+            for _ in range(2):
+                b[:] = rng.integers(0, 256, b.shape, dtype=np.uint8)
+                want = b.copy()
+                rs_ref.c_encode(d, p, want, S=S)
+                assert _timed_launches(enc, lambda: enc.encode_host(b, S)) == 0, i
+                assert np.array_equal(b[:, :, :S], want[:, :, :S]), i
+            enc.service_stop()
+    finally:
+        enc.service_stop()
+        fec.host_free(b.reshape(-1))
+        enc.close()
+
+
+def test_service_timeout_waits_for_the_block_to_leave(gpu):
+    """a call the service does not answer within the
+    watchdog timeout (forced: the block stalls 300 ms per request, timeout 50
+    ms) returns ErrHip only after the block has left -- so nothing writes the
+    caller's batch after the call returns -- and later calls take the launch
+    path with the right bytes; the service can be started again."""
+    d, p, S = 10, 3, 1470
+    n, pitch = d + p, 1472
+    rng = np.random.default_rng(23)
+    enc = fec.New(d, p)
+    b = _pinned(1, n, pitch, rng)
+    try:
+        enc.service_config(timeout_ms=50, grace_ms=5000, test_stall_us=300_000)
+        enc.service_start(idle_us=1_000_000)
+        want = b.copy()
+        rs_ref.c_encode(d, p, want, S=S)
+        t0 = time.perf_counter()
+        with pytest.raises(fec.ErrHip):
+            enc.encode_host(b, S)
+        el = time.perf_counter() - t0
+        assert 0.25 < el < 4.0, el  # the stall ran out and the block left before the call returned
+        assert not enc.poisoned
+        snap = b.copy()
+        time.sleep(0.4)
+        assert np.array_equal(b, snap), "the batch changed after the call returned"
+        # the block served the request on its way out: its bytes are the right ones
+        assert np.array_equal(b[:, :, :S], want[:, :, :S])
+        b[:, d:, :] = 0
+        assert _timed_launches(enc, lambda: enc.encode_host(b, S)) > 0  # service off: launch path
+        assert np.array_equal(b[:, :, :S], want[:, :, :S])
+        enc.service_config()  # no stall
+        enc.service_start()
+        b[:, d:, :] = 0
+        assert _timed_launches(enc, lambda: enc.encode_host(b, S)) == 0
+        assert np.array_equal(b[:, :, :S], want[:, :, :S])
+    finally:
+        enc.service_stop()
+        fec.host_free(b.reshape(-1))
+        enc.close()
+
+
+def test_service_block_that_never_leaves_poisons_the_context(gpu):
+    """A block still resident after the grace period (stall 1.2 s, timeout 50
+    ms, grace 100 ms): the call fails, the context is poisoned, every later
+    call on it fails without touching the GPU, and destroy frees nothing the
+    block reads (it finishes later, serving into the batch this test keeps
+    alive, and leaves on the stop request)."""
+    import torch
+
+    d, p, S = 10, 3, 1470
+    n, pitch = d + p, 1472
+    rng = np.random.default_rng(29)
+    enc = fec.New(d, p)
+    b = _pinned(1, n, pitch, rng)
+    try:
+        enc.service_config(timeout_ms=50, grace_ms=100, test_stall_us=1_200_000)
+        enc.service_start(idle_us=1_000_000)
+        with pytest.raises(fec.ErrHip):
+            enc.encode_host(b, S)
+        assert enc.poisoned
+        for call in (lambda: enc.encode_host(b, S), lambda: enc.service_start(),
+                     lambda: enc.encode_batch(torch.zeros((2, n, pitch), dtype=torch.uint8, device="cuda"), S),
+                     lambda: enc.reconstruct_host(b, np.full(1, (1 << n) - 1, np.uint64), S)):
+            with pytest.raises(fec.ErrHip):
+                call()
+        enc.close()  # leaks the mailbox and tables: the block still reads them
+        time.sleep(1.6)  # the stalled block serves, sees the stop line and leaves
+        torch.cuda.synchronize()
+    finally:
+        fec.host_free(b.reshape(-1))

@@ -684,7 +684,7 @@ __global__ __launch_bounds__(256) void k_apply_pd(Batch a) {
 }
 
 // ---------------------------------------------------------------- per-call service
-// k_service: ONE block of 16 waves stays resident and serves the per-group
+// k_service: ONE block of 8 waves stays resident and serves the per-group
 // calls of the drop-in path (one Encode from calcECC, one Reconstruct per lossy
 // group from input: ugo/fec.go:202,238) from a mailbox in pinned host memory
 // (SvcBox, fec_kernels.hpp).  Thread 0 polls the request word with relaxed
@@ -824,6 +824,10 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
     const uint64_t pitch = static_cast<uint64_t>(rq[10]) << 32 | rq[9];
     const bool recon = op == kSvcReconstruct;
     const uint32_t data_only = recon && (rq[7] & 1u);
+    if (sa.stall_ticks) {  // tests only: a slow block, to drive the host's watchdog
+      const uint64_t ts = wall_clock64();
+      while (static_cast<uint64_t>(wall_clock64()) - ts < sa.stall_ticks) __builtin_amdgcn_s_sleep(127);
+    }
     if (recon) {  // this request's descriptors: one slot per group, a wave each
       for (uint32_t g = wv; g < G; g += kSvcThreads / 64u) {
         svc_copy_desc(L, g, a.desc + (msk[g] & a.nmask) * a.desc_stride, dwords, lane, 64u);
@@ -1850,7 +1854,7 @@ hipError_t launch_encode_const(int d, int p, const Batch& a, hipStream_t s) {
   if (d == 10 && p == 3)
     launch(kKEncode, k_encode_g<10, 3, kEncNT & 2, kEncLdsRows, 256, kEncStageRows>, grid, block, 0, s, a);
   else if (d == 32 && p == 8)
-    launch(kKEncode, k_encode_frs<32, 8, kEncJumboNT & 2, kEncJumboLdsRows, 256, kEncJumboLdsRows, 3, kEncJumboFrBlock>,
+    launch(kKEncode, k_encode_frs<32, 8, kEncJumboNT & 2, kEncJumboLdsRows, 256, kEncJumboLdsRows, 2, kEncJumboFrBlock>,
            grid, block, 0, s, a);
   else
     return hipErrorInvalidValue;

@@ -96,7 +96,8 @@ struct SvcArgs {
   const uint8_t* encdesc;   // encode descriptor (MODE 0)
   SvcBox* box;              // device view of the mailbox
   uint64_t idle_ticks;
-  uint32_t start_seq;       // the last request already served
+  uint32_t start_seq;       // the last seq on the line that must not be served (served, or abandoned)
+  uint64_t stall_ticks;     // tests only (ugo_fec_service_config): wait this long before serving each request
 };
 // dmax 4..16 (d <= 16) and p <= 4 (epad 4) only
 hipError_t launch_service(int dmax, const SvcArgs& sa, hipStream_t s);

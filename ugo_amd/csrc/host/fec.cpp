@@ -253,15 +253,13 @@ void FEC::freeBatch(Batch& b) {
 }
 
 // Pinned [rows | masks | status | out] for `cap` groups (empty batch only).
+// The new memory is allocated before the old is freed: on failure the batch
+// keeps what it had (setBatch then drops back to per-call recovery).
 bool FEC::ensureBatch(Batch& b, size_t cap) {
   if (b.mem && b.cap >= cap) return true;
   const size_t n = static_cast<size_t>(shardSize_), slots = outSlots();
   const size_t o_rows = 0, o_masks = o_rows + cap * n * 8, o_status = o_masks + cap * 8;
   const size_t o_out = (o_status + cap + 15) / 16 * 16, bytes = o_out + cap * slots * kSlotStride;
-  hipEvent_t ev = b.done;
-  b.done = nullptr;
-  freeBatch(b);
-  b.done = ev;
   void* p = nullptr;
   if (ugo_fec_host_alloc(bytes, &p) != UGO_FEC_OK) return false;
   if (!b.done) {
@@ -272,6 +270,7 @@ bool FEC::ensureBatch(Batch& b, size_t cap) {
       return false;
     }
   }
+  if (b.mem) ugo_fec_host_free(b.mem);
   b.mem = static_cast<uint8_t*>(p);
   b.cap = cap;
   b.rows = reinterpret_cast<uint64_t*>(b.mem + o_rows);
@@ -483,6 +482,11 @@ std::vector<Bytes> FEC::setBatch(int groups, unsigned flags) {
   if (groups > 0) {
     if (!ensureGpu() || !ensureBatch(batch_[0], size_t(groups)) ||
         ((flags & kBatchOverlap) && !ensureBatch(batch_[1], size_t(groups)))) {
+      // no room for the batch: per-call recovery (a batch smaller than asked
+      // for is never used -- the pending batches are empty after flushInto)
+      batchCap_ = 0;
+      batchFlags_ = 0;
+      cur_ = 0;
       lastError_ = UGO_FEC_ERR_HIP;
       return out;
     }

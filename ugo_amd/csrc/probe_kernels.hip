@@ -1,0 +1,135 @@
+// probe_kernels.hip -- measurement kernels for bench.py's ceilings (not product
+// code: built into a separate library, libugoprobe.so, which nothing in the
+// product path loads).  They give the driver's line a ceiling measured on the
+// same box, in the same process, on the same cold batches as the kernels they
+// bound:
+//   * ugo_probe_encode_twin: the compute-free twin of the (10,3) encode
+//     k_encode_g<10,3,2,8,256,13> -- the same grid, the same 52-KiB stage (3
+//     blocks per CU), rows 0-7 by LDS-DMA nt and 8-9 by nt register loads, the
+//     same nt stores of 3 parity rows with the same tail handling -- with each
+//     parity row a plain XOR of the inputs instead of the GF network (wrong
+//     bytes on purpose: it is the access pattern alone);
+//   * ugo_probe_nt_copy: an nt copy, one 16-B chunk per thread over a full
+//     grid (the fastest copy form measured, tools/rxgather.hip).
+// Each launch is timed with hipExtLaunchKernel start/stop events (the same
+// timestamps ugo_fec_timing_* gives the production kernels).
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "gf_device.hpp"
+
+namespace {
+
+using ugo::kern::lds16;
+using ugo::kern::lds_dma16;
+using ugo::kern::lds_dma_wait;
+using ugo::kern::load16;
+using ugo::kern::store16;
+using ugo::kern::u32x4;
+using ugo::kern::V4;
+
+struct Twin {
+  uint8_t* base;
+  uint64_t rstride, gstride;
+  uint32_t chunks, S, items;
+};
+
+// k_encode_g<D=10, P=3, NTS=2, GR=8, BS=256, LR=13>'s loads, stage and stores
+__global__ __launch_bounds__(256) void k_encode_twin(Twin a) {
+  constexpr int D = 10, P = 3, GR = 8, LR = 13;
+  __shared__ u32x4 stage[4][LR][64];
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (item >= a.items) return;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t gl = item / a.chunks, c = item - gl * a.chunks;
+  uint8_t* gp = a.base + gl * a.gstride + static_cast<uint64_t>(c) * 16u;
+  const uint32_t nb = a.S - c * 16u;
+#pragma unroll
+  for (int k = 0; k < GR; ++k) lds_dma16(gp + static_cast<uint64_t>(k) * a.rstride, &stage[w][k][0]);
+  V4 x[D];
+#pragma unroll
+  for (int k = GR; k < D; ++k) x[k] = load16<1>(gp + static_cast<uint64_t>(k) * a.rstride);
+  lds_dma_wait();
+#pragma unroll
+  for (int k = 0; k < GR; ++k) x[k] = lds16(&stage[w][k][lane]);
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    V4 y = x[i];
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+      if (k != i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y.v[j] ^= x[k].v[j];
+    store16<2>(gp + static_cast<uint64_t>(D + i) * a.rstride, y, nb);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_nt_copy(const u32x4* src, u32x4* dst, uint64_t n16) {
+  const uint64_t c = blockIdx.x * 256ull + threadIdx.x;
+  if (c >= n16) return;
+  __builtin_nontemporal_store(__builtin_nontemporal_load(src + c), dst + c);
+}
+
+template <typename F>
+int timed(F launch_one, int reps, hipStream_t s, float* ms_out) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 1;
+  int st = 0;
+  for (int r = 0; r < reps && !st; ++r) {
+    if (launch_one(r, e0, e1) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+        hipEventElapsedTime(&ms_out[r], e0, e1) != hipSuccess)
+      st = 1;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)s;
+  return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+// reps launches of the encode twin over a planar (10+3) batch set: launch r
+// works on bases[r % nbuf] (rows at row_stride, groups at pitch), chunks =
+// ceil(S / 16) per group; ms_out[r] = that launch's duration.  0 = OK.
+int ugo_probe_encode_twin(uint8_t* const* bases, int nbuf, size_t groups, size_t S, size_t pitch,
+                          size_t row_stride, int reps, void* stream, float* ms_out) {
+  if (!bases || nbuf <= 0 || !ms_out || reps <= 0 || S == 0 || pitch < S || pitch % 16 || row_stride % 16)
+    return 2;
+  const uint64_t chunks = (S + 15) / 16, items = groups * chunks;
+  if (items == 0 || items > 0xffffffffull) return 2;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<uint32_t>((items + 255) / 256)), block(256);
+  return timed(
+      [&](int r, hipEvent_t e0, hipEvent_t e1) {
+        Twin a{bases[r % nbuf], row_stride, pitch, static_cast<uint32_t>(chunks), static_cast<uint32_t>(S),
+               static_cast<uint32_t>(items)};
+        hipExtLaunchKernelGGL(k_encode_twin, grid, block, 0, s, e0, e1, 0u, a);
+        return hipGetLastError();
+      },
+      reps, s, ms_out);
+}
+
+// reps launches of an nt copy of `bytes` (a multiple of 16) from srcs[r % nbuf]
+// to dsts[r % nbuf]; ms_out[r] = that launch's duration.  0 = OK.
+int ugo_probe_nt_copy(const uint8_t* const* srcs, uint8_t* const* dsts, int nbuf, size_t bytes, int reps,
+                      void* stream, float* ms_out) {
+  if (!srcs || !dsts || nbuf <= 0 || !ms_out || reps <= 0 || bytes == 0 || bytes % 16) return 2;
+  const uint64_t n16 = bytes / 16;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<uint32_t>((n16 + 255) / 256)), block(256);
+  return timed(
+      [&](int r, hipEvent_t e0, hipEvent_t e1) {
+        hipExtLaunchKernelGGL(k_nt_copy, grid, block, 0, s, e0, e1, 0u,
+                              reinterpret_cast<const u32x4*>(srcs[r % nbuf]), reinterpret_cast<u32x4*>(dsts[r % nbuf]),
+                              n16);
+        return hipGetLastError();
+      },
+      reps, s, ms_out);
+}
+
+}  // extern "C"

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 // MODE (A/B timing only, tools/rxvariants.hip): 0 = production, 1 = without
 // the presence atomics, 2 = the same loads and stores without the realignment.
 // NT: bit 0 nontemporal payload loads, bit 1 nontemporal stores.
-template <int NP, int MODE = 0, int NT = 0>
+template <int NP, int MODE = 0, int NT = 0, int ORD = 0>
 __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
   if (rx_gated_off(a)) return;
   __shared__ uint32_t bstats[5];
@@ -207,6 +207,9 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
   const u32x4 zero = {0u, 0u, 0u, 0u};
   const uint32_t slot = static_cast<uint32_t>(a.slot);
   const u32x4 K0 = a.pad ? ld16(a.pad) : zero;  // keystream over the header chunk
+  // a batch with no presence bit at call entry (the usual case: one call per
+  // batch) has nothing an earlier call placed: no per-packet snapshot lookup
+  const bool chk_prev = a.prev && !(a.seen && *a.seen < a.call);
   u32x4 K[NP];
   uint32_t kbx[NP], kby[NP];  // keystream of the neighbour chunk (lane 31 of a half)
 #pragma unroll
@@ -221,20 +224,31 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
     }
   }
   RxAccount acct;
-  uint64_t i = 2 * wave + half;
+  // ORD 0: grid-stride over packet pairs.  ORD 1: block b owns the contiguous
+  // packet range [b*per, b*per + per) (per a multiple of 8), its eight
+  // half-waves take packets b*per + h, + 8, ...
+  uint64_t first = 2 * wave, step = 2 * nwaves, end = a.npk;
+  if constexpr (ORD == 1) {
+    uint64_t per = (a.npk + gridDim.x - 1) / gridDim.x;
+    per = (per + 7) / 8 * 8;
+    first = blockIdx.x * per + 2 * (threadIdx.x >> 6);
+    step = 8;
+    end = min(a.npk, blockIdx.x * per + per);
+  }
+  uint64_t i = first + half;
   u32x4 hn = zero;
   uint32_t ln = 0;
-  if (i < a.npk) {
+  if (i < end) {
     hn = ld16(a.wire + i * a.slot);
     ln = a.lens[i];
   }
-  for (uint64_t base = 2 * wave; base < a.npk; base += 2 * nwaves, i += 2 * nwaves) {
-    const bool have = i < a.npk;
+  for (uint64_t base = first; base < end; base += step, i += step) {
+    const bool have = i < end;
     const uint8_t* pk = a.wire + i * a.slot;
     const u32x4 h = hn ^ K0;
     const uint32_t len = have ? min(ln, slot) : 0u;
-    const uint64_t inext = i + 2 * nwaves;
-    if (inext < a.npk) {  // prefetch the next packet's header and length
+    const uint64_t inext = i + step;
+    if (inext < end) {  // prefetch the next packet's header and length
       hn = ld16(a.wire + inext * a.slot);
       ln = a.lens[inext];
     }
@@ -253,7 +267,7 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
     uint32_t claim = static_cast<uint32_t>(i);
     if (acc && a.win) claim = a.win[(grp - a.first_group) * a.n + row];
     uint64_t before = 0;  // presence at call entry: set = an earlier call placed this seqid
-    if (acc && a.prev) before = a.prev[grp - a.first_group];
+    if (acc && chk_prev) before = a.prev[grp - a.first_group];
     const uint32_t L = acc ? min(len - 6u, a.S) : 0u;  // payload bytes kept
     const uint32_t lim = acc ? L + 6u : 0u;            // packet bytes [0, lim) are needed
     u32x4 A[NP];
@@ -328,9 +342,258 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
     }
   }
   if (hl == 0) acct.settle(a, bstats);
-  if (a.stats) {
+  if (a.parts) {
+    __syncthreads();
+    if (threadIdx.x < 5) a.parts[blockIdx.x * 5u + threadIdx.x] = bstats[threadIdx.x];
+  } else if (a.stats) {
     __syncthreads();
     if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+  }
+}
+
+// Sums per-block counters into stats (one block).
+__global__ __launch_bounds__(256) void k_rx_sum_parts(const uint32_t* parts, uint32_t nparts, uint32_t* stats) {
+  __shared__ uint32_t tot[5];
+  if (threadIdx.x < 5) tot[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t c[5] = {0u, 0u, 0u, 0u, 0u};
+  for (uint32_t b = threadIdx.x; b < nparts; b += 256u)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) c[k] += parts[b * 5u + k];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    if (c[k]) atomicAdd(&tot[k], c[k]);
+  __syncthreads();
+  if (threadIdx.x < 5 && tot[threadIdx.x]) atomicAdd(&stats[threadIdx.x], tot[threadIdx.x]);
+}
+
+// ---------------------------------------------------------------------------
+// Destination-ordered RX (index + gather).
+//
+// k_rx_place writes each packet where its seqid says, in ring order: a block's
+// stores are 1470-B pieces scattered over the 13 planar row streams, and the
+// 128-B lines where two pieces meet are written half by one block and half by
+// another, often on another XCD.  The two kernels below turn that around:
+//  1. k_rx_index reads only the 8 header bytes and the length of each packet,
+//     classifies it exactly as input does (ugo/fec.go:123-175; conn.go:395)
+//     and takes, per (row, group), the smallest packet index (atomicMin: the
+//     first copy in ring order wins, ugo/fec.go:123-129).  A (row, group) whose
+//     presence bit is already set belongs to an earlier call (duplicate).  The
+//     table is row-major -- win[row * groups + g] -- like the planar batch.
+//     The atomicMin that finds the word still empty is the one claim that
+//     counts as accepted; every other valid packet is a duplicate.  Each block
+//     writes its five counters to its own slot of `parts` (no contended
+//     device atomics: 2,048 blocks adding into one word cost ~25 us).
+//  2. k_rx_gather walks the DESTINATION in order: a full grid, block b owns a
+//     contiguous run of (row, group) pieces and writes whole runs of
+//     consecutive groups of one row (ORDER 0: the planar rows themselves;
+//     ORDER 1: tiles of GT groups, all rows of a tile), reading each piece's
+//     packet by the index.  Presence bits are OR-ed per placed piece (no
+//     return value, distinct words); block 0 also sums the index kernel's
+//     per-block counters into `stats`.
+__device__ __forceinline__ uint32_t rx_why(const RxArgs& a, uint32_t len, uint2 hw, uint32_t k0, uint32_t k1,
+                                           uint32_t& row, uint64_t& gs) {
+  row = 0;
+  gs = 0;
+  if (len < 6u) return 3;
+  const uint32_t seqid = hw.x ^ k0;
+  const uint32_t flag = (hw.y ^ k1) & 0xffffu;
+  if (flag != 0xf1u && flag != 0xf2u) return 1;  // ugo/conn.go:395
+  const uint64_t grp = seqid / a.n;
+  if (grp < a.first_group || grp >= a.first_group + a.groups) return 2;
+  row = seqid % a.n;
+  gs = grp - a.first_group;
+  return 0;
+}
+
+// PPT packets per thread, all their loads issued first: thread t of block b
+// takes packets b*256*PPT + t + 256k.  Per-block counters {accepted, bad flag,
+// out of window, too short, duplicate} go to parts[b*5 + k].
+template <int PPT>
+__global__ __launch_bounds__(256) void k_rx_index(RxArgs a, uint32_t* parts) {
+  __shared__ uint32_t bstats[5];
+  if (threadIdx.x < 5) bstats[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t k0 = 0u, k1 = 0u;
+  if (a.pad) {
+    k0 = reinterpret_cast<const uint32_t*>(a.pad)[0];
+    k1 = reinterpret_cast<const uint32_t*>(a.pad)[1];
+  }
+  const uint64_t i0 = blockIdx.x * 256ull * PPT + threadIdx.x;
+  uint32_t len[PPT];
+  uint2 hw[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const uint64_t i = i0 + 256u * k;
+    len[k] = 0u;
+    hw[k] = make_uint2(0u, 0u);
+    if (i < a.npk) {
+      len[k] = a.lens[i];
+      hw[k] = *reinterpret_cast<const uint2*>(a.wire + i * a.slot);
+    }
+  }
+  uint32_t cnt[5] = {0u, 0u, 0u, 0u, 0u};
+  uint32_t row[PPT];
+  uint64_t gs[PPT];
+  bool live[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const uint32_t why = rx_why(a, len[k], hw[k], k0, k1, row[k], gs[k]);
+    live[k] = i0 + 256u * k < a.npk && why == 0;
+    if (i0 + 256u * k < a.npk && why) ++cnt[why];
+  }
+  uint64_t pm[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) pm[k] = live[k] ? a.present[gs[k]] : 0ull;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    if (!live[k]) continue;
+    if ((pm[k] >> row[k]) & 1ull) {  // an earlier call's seqid
+      ++cnt[4];
+      continue;
+    }
+    const uint32_t old = atomicMin(&a.win[row[k] * a.groups + gs[k]], static_cast<uint32_t>(i0 + 256u * k));
+    ++cnt[old == 0xffffffffu ? 0 : 4];
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    if (cnt[k]) atomicAdd(&bstats[k], cnt[k]);
+  __syncthreads();
+  if (threadIdx.x < 5) parts[blockIdx.x * 5u + threadIdx.x] = bstats[threadIdx.x];
+}
+
+// Half a wave per piece (as k_rx_place: 32 lanes x NP passes of 16 B, the
+// keystream held in registers, DPP realignment).  The eight half-waves of a
+// block take pieces j0 + h, j0 + h + 8, ... of the block's run; the next
+// piece's packet index is prefetched one iteration ahead.  NT as k_rx_place.
+template <int NP, int ORDER, int GT, int NT = 3>
+__global__ __launch_bounds__(256) void k_rx_gather(RxArgs a, const uint32_t* parts, uint32_t nparts) {
+  const uint32_t lane = threadIdx.x & 63u, hl = lane & 31u;
+  const uint32_t hw = threadIdx.x >> 5;  // half-wave of the block, 0..7
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  if (blockIdx.x == 0 && parts && a.stats) {  // the index kernel's counters
+    __shared__ uint32_t tot[5];
+    if (threadIdx.x < 5) tot[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t c[5] = {0u, 0u, 0u, 0u, 0u};
+    for (uint32_t b = threadIdx.x; b < nparts; b += 256u)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) c[k] += parts[b * 5u + k];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (c[k]) atomicAdd(&tot[k], c[k]);
+    __syncthreads();
+    if (threadIdx.x < 5 && tot[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], tot[threadIdx.x]);
+  }
+  const uint64_t ntiles = ORDER == 0 ? a.groups : (a.groups + GT - 1) / GT;
+  const uint64_t space = ntiles * (ORDER == 0 ? 1u : GT) * a.n;  // pieces, tail tile included
+  const uint64_t unit = ORDER == 0 ? 8u : uint64_t(GT) * a.n;
+  uint64_t per = (space + gridDim.x - 1) / gridDim.x;
+  per = (per + unit - 1) / unit * unit;
+  const uint64_t j0 = blockIdx.x * per;
+  const uint64_t j1 = min(space, j0 + per);
+  u32x4 K[NP];
+  uint32_t kbx[NP], kby[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const uint32_t o = 16u * (32u * q + hl);
+    K[q] = (a.pad && o + 16u <= slot) ? ld16(a.pad + o) : zero;
+    kbx[q] = kby[q] = 0u;
+    if (a.pad && hl == 31u && o + 32u <= slot) {
+      const u32x4 B = ld16(a.pad + o + 16u);
+      kbx[q] = B.x;
+      kby[q] = B.y;
+    }
+  }
+  auto piece = [&](uint64_t j, uint32_t& row, uint64_t& gs) {
+    if constexpr (ORDER == 0) {
+      row = static_cast<uint32_t>(j / a.groups);
+      gs = j - uint64_t(row) * a.groups;
+    } else {
+      const uint64_t t = j / (uint64_t(GT) * a.n);
+      const uint32_t w = static_cast<uint32_t>(j - t * GT * a.n);
+      row = w / GT;
+      gs = t * GT + (w - row * GT);
+    }
+  };
+  constexpr uint32_t kNone = 0xffffffffu;
+  uint64_t j = j0 + hw;
+  uint32_t row_n = 0;
+  uint64_t gs_n = 0;
+  uint32_t idx_n = kNone;
+  if (j < j1) {
+    piece(j, row_n, gs_n);
+    if (gs_n < a.groups) idx_n = a.win[row_n * a.groups + gs_n];
+  }
+  for (; j < j1; j += 8) {
+    const uint32_t row = row_n, idx = idx_n;
+    const uint64_t gs = gs_n;
+    if (j + 8 < j1) {  // prefetch the next piece's packet index
+      piece(j + 8, row_n, gs_n);
+      idx_n = gs_n < a.groups ? a.win[row_n * a.groups + gs_n] : kNone;
+    }
+    if (idx == kNone) continue;  // half-wave-uniform: lost, or an earlier call's
+    const uint8_t* pk = a.wire + uint64_t(idx) * a.slot;
+    const uint32_t len = min(static_cast<uint32_t>(a.lens[idx]), slot);  // >= 6: k_rx_index accepted it
+    const uint32_t L = min(len - 6u, a.S);
+    const uint32_t lim = L + 6u;
+    u32x4 A[NP];
+    uint32_t bx[NP], by[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      A[q] = o < lim ? ((NT & 1) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + o)) : ld16(pk + o))
+                     : zero;
+      bx[q] = by[q] = 0u;
+      if (hl == 31u && o + 16u < lim) {
+        const u32x4 B = ld16(pk + o + 16u);
+        bx[q] = B.x;
+        by[q] = B.y;
+      }
+    }
+    uint8_t* dst = a.shards + row * a.rstride + gs * a.gstride;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      const u32x4 Aq = A[q] ^ K[q];
+      uint32_t nx = from_next_lane(Aq.x), ny = from_next_lane(Aq.y);
+      if (hl == 31u) {
+        nx = bx[q] ^ kbx[q];
+        ny = by[q] ^ kby[q];
+      }
+      if (o >= a.S) continue;
+      uint32_t w[4];
+      w[0] = __builtin_amdgcn_alignbyte(Aq.z, Aq.y, 2);
+      w[1] = __builtin_amdgcn_alignbyte(Aq.w, Aq.z, 2);
+      w[2] = __builtin_amdgcn_alignbyte(nx, Aq.w, 2);
+      w[3] = __builtin_amdgcn_alignbyte(ny, nx, 2);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t b0 = o + 4u * k;
+        const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
+        w[k] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+      }
+      const uint32_t nb = a.S - o;
+      if (nb >= 16u) {
+        const u32x4 v = {w[0], w[1], w[2], w[3]};
+        if constexpr (NT & 2)
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + o));
+        else
+          *reinterpret_cast<u32x4*>(dst + o) = v;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t lo = 4u * k;
+          if (nb >= lo + 4u) {
+            *reinterpret_cast<uint32_t*>(dst + o + lo) = w[k];
+          } else if (nb > lo) {
+            for (uint32_t t = 0; t < nb - lo; ++t) dst[o + lo + t] = static_cast<uint8_t>(w[k] >> (8u * t));
+          }
+        }
+      }
+    }
+    if (hl == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
   }
 }
 
@@ -366,17 +629,29 @@ __global__ __launch_bounds__(256) void k_rx_fill(uint32_t* win, uint64_t words, 
 }
 
 __global__ __launch_bounds__(256) void k_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups,
-                                                  uint32_t* dup) {
+                                                  uint32_t* dup, uint32_t* win, uint64_t words,
+                                                  unsigned long long* seen, unsigned long long call) {
   const uint64_t t = blockIdx.x * 256ull + threadIdx.x;
+  const uint64_t nt = gridDim.x * 256ull;
   if (t == 0) *dup = 0u;
-  for (uint64_t g = t; g < groups; g += gridDim.x * 256ull) prev[g] = present[g];
+  uint64_t any = 0;
+  for (uint64_t g = t; g < groups; g += nt) {
+    const uint64_t m = present[g];
+    prev[g] = m;
+    any |= m;
+  }
+  if (win)
+    for (uint64_t i = t; i < words; i += nt) win[i] = 0xffffffffu;
+  if (seen && __any(any != 0) && (threadIdx.x & 63u) == 0) atomicMax(seen, call);
 }
 
-hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, hipStream_t s) {
+hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, uint32_t* win,
+                           uint64_t words, unsigned long long* seen, unsigned long long call, hipStream_t s) {
   uint64_t blocks = (groups + 255) / 256;
   if (blocks == 0) blocks = 1;
   if (blocks > 1024u) blocks = 1024u;
-  launch(kKRx, k_rx_begin, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, present, prev, groups, dup);
+  launch(kKRx, k_rx_begin, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, present, prev, groups, dup, win,
+         words, seen, call);
   return hipGetLastError();
 }
 

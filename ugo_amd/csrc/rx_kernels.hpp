@@ -20,6 +20,12 @@ struct RxArgs {
   const uint64_t* prev;    // presence masks at call entry (launch_rx_begin's snapshot), or null: a packet
                            // whose bit was already set there is a duplicate of an earlier call's copy
   uint32_t fixup;          // re-place pass: claim winners only, no stats, presence already set
+  uint32_t* parts;         // if non-null: block b writes its five counters to parts[b*5 + k] instead of
+                           // adding them to stats (a full grid's blocks would contend on those words)
+  const unsigned long long* seen;  // if non-null: k_rx_begin's record -- *seen >= call means some group had a
+                           // presence bit set at call entry (or a concurrent later call's did); below
+                           // call, none did, and the place pass skips its per-packet `prev` lookups
+  unsigned long long call; // this call's id (per context, increasing)
   uint64_t npk;
   uint64_t slot;
   uint64_t first_group;
@@ -34,7 +40,11 @@ struct RxArgs {
 // the packet index into a.win, which launch_rx_fill sets to 0xffffffff), then
 // places the winners.  a.win == null places every accepted packet.
 // Call entry: *dup = 0 and prev[g] = present[g] for every group (one launch).
-hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, hipStream_t s);
+// Call entry, one launch: *dup = 0, prev[g] = present[g], win[0 .. words) =
+// 0xffffffff (claim words; win may be null), and atomicMax(seen, call) by
+// every block that finds a presence bit set (seen may be null).
+hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, uint32_t* win,
+                           uint64_t words, unsigned long long* seen, unsigned long long call, hipStream_t s);
 hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, hipStream_t s);
 hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s);
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s);

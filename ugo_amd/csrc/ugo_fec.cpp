@@ -85,6 +85,10 @@ struct ugo_fec {
   int8_t* d_status[kStreams] = {};
   uint64_t* d_zc_mask = nullptr;  // zero-copy host reconstruct: presence masks / status of the batch,
   int8_t* d_zc_status = nullptr;   // pinned host memory the kernels read / write through its mapping
+  // RX: k_rx_begin's record of calls that found a presence bit set (atomicMax of
+  // the call id), and this context's call counter
+  unsigned long long* d_rxseen = nullptr;
+  unsigned long long rx_calls = 0;
   size_t zc_groups = 0;
   // d+p > 64: decode descriptors built on the host, one per erasure pattern
   // (klauspost caches its inversions per pattern the same way)
@@ -100,7 +104,15 @@ struct ugo_fec {
   ugo::kern::SvcBox* svc_box = nullptr;   // host address
   ugo::kern::SvcBox* svc_dbox = nullptr;  // device view
   hipStream_t svc_stream = nullptr;
-  uint32_t svc_seq = 0;
+  uint32_t svc_seq = 0;                 // the last seq posted on the mailbox line
+  uint32_t svc_timeout_ms = 5000;       // watchdog: a call's wait for an answer
+  uint32_t svc_grace_ms = 5000;         // then: the wait for the block to leave
+  uint32_t svc_stall_us = 0;            // tests only (ugo_fec_service_config)
+  uint64_t svc_khz = 100000;            // wall_clock64's rate (100 MHz on gfx950)
+  // the service block did not leave within the grace period: it may still read
+  // the mailbox and tables and write a caller's batch, so every call fails and
+  // destroy leaks what the block reads
+  bool poisoned = false;
 };
 
 namespace {
@@ -190,14 +202,19 @@ int svc_stop(ugo_fec* c);
 void free_ctx(ugo_fec* c) {
   if (!c) return;
   DeviceGuard g(c->device);
-  (void)svc_stop(c);  // the resident block leaves before its mailbox goes
-  if (c->svc_stream) (void)hipStreamDestroy(c->svc_stream);
-  if (c->svc_box) (void)hipHostFree(c->svc_box);
+  // the resident block leaves before its mailbox and tables go; if it does not
+  // (poisoned), everything it reads is leaked rather than freed under it
+  const bool block_gone = svc_stop(c) == UGO_FEC_OK && !c->poisoned;
+  if (block_gone) {
+    if (c->svc_stream) (void)hipStreamDestroy(c->svc_stream);
+    if (c->svc_box) (void)hipHostFree(c->svc_box);
+    (void)hipFree(c->d_M);
+    (void)hipFree(c->d_gf);
+    (void)hipFree(c->d_encdesc);
+    (void)hipFree(c->d_table);
+  }
+  (void)hipFree(c->d_rxseen);
   timer_release(c);
-  (void)hipFree(c->d_M);
-  (void)hipFree(c->d_gf);
-  (void)hipFree(c->d_encdesc);
-  (void)hipFree(c->d_table);
   (void)hipHostFree(c->d_zc_mask);
   (void)hipHostFree(c->d_zc_status);
   for (int i = 0; i < kStreams; ++i) {
@@ -272,6 +289,7 @@ bool layout_disjoint(size_t S, size_t rstride, size_t rows, size_t gstride, size
 
 int check_batch(const ugo_fec* c, const void* shards, size_t groups, size_t S, const Layout& L) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;  // checkShards: all shards empty
   if (S > 0xffffffffu) return UGO_FEC_ERR_INVALID_ARG;
   if (groups == 0) return UGO_FEC_OK;  // an empty batch has no layout to check
@@ -606,8 +624,11 @@ int host_reconstruct_mapped(ugo_fec* c, uint8_t* mapped, const uint64_t* present
 // from the context's mailbox: the host fills the request, bumps seq and spins
 // on done; a block that has left (idle, alive == 0) is relaunched on the
 // service stream, which also orders it after its predecessor.
-constexpr auto kSvcTimeout = std::chrono::seconds(5);
-
+//
+// The line always holds the LAST request posted (c->svc_seq); a block is
+// launched with start_seq = the one seq it must not serve: c->svc_seq when no
+// request is waiting (that line was served, or abandoned by a stop or a
+// timeout), sq - 1 when request sq is posted and waiting.
 template <typename T>
 T svc_ld(const T& v) { return __atomic_load_n(&v, __ATOMIC_ACQUIRE); }
 
@@ -621,7 +642,7 @@ inline void svc_relax() {  // one spin of the host's wait on the mailbox
 template <typename T>
 void svc_st(T& v, T x) { __atomic_store_n(&v, x, __ATOMIC_RELEASE); }
 
-int svc_launch(ugo_fec* c) {
+int svc_launch(ugo_fec* c, uint32_t skip_seq) {
   ugo::kern::SvcArgs sa{};
   sa.a = base_batch(c, nullptr, 0, Layout{0, 0});
   sa.a.desc = c->d_table;
@@ -629,7 +650,8 @@ int svc_launch(ugo_fec* c) {
   sa.encdesc = c->d_encdesc;
   sa.box = c->svc_dbox;
   sa.idle_ticks = c->svc_idle_ticks;
-  sa.start_seq = svc_ld(c->svc_box->done);
+  sa.start_seq = skip_seq;
+  sa.stall_ticks = uint64_t(c->svc_stall_us) * c->svc_khz / 1000u;
   svc_st(c->svc_box->alive, 1u);
   if (ugo::kern::launch_service(ugo::kern::apply_dmax(c->d), sa, c->svc_stream) != hipSuccess) {
     svc_st(c->svc_box->alive, 0u);
@@ -676,22 +698,60 @@ uint32_t svc_post(ugo_fec* c, uint32_t op, const uint8_t* mapped, size_t groups,
   return sq;
 }
 
+// A HIP status of the service stream that means the block died (any error:
+// a fault, an illegal address, a launch timeout -- not "still running").
+bool svc_faulted(ugo_fec* c) {
+  const hipError_t q = hipStreamQuery(c->svc_stream);
+  if (q == hipSuccess || q == hipErrorNotReady) return false;
+  return true;
+}
+
+// Makes sure no service block is left: posts a stop if one is alive, then
+// waits up to the grace period for it to clear `alive` and for its stream to
+// drain.  OK: gone (or dead), nothing it could still write.  Otherwise the
+// context is poisoned.
+int svc_retire(ugo_fec* c) {
+  c->svc_on = false;
+  if (!c->svc_box || !c->svc_stream) return UGO_FEC_OK;
+  ugo::kern::SvcBox* b = c->svc_box;
+  if (svc_ld(b->alive)) (void)svc_post(c, ugo::kern::kSvcStop, nullptr, 0, 0, 0, 0, nullptr);
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto grace = std::chrono::milliseconds(c->svc_grace_ms);
+  for (uint32_t spin = 0;; ++spin) {
+    if ((spin & 255u) == 0) {
+      const hipError_t q = hipStreamQuery(c->svc_stream);
+      if (q == hipSuccess) return UGO_FEC_OK;  // drained: alive is 0 or the block never ran
+      if (q != hipErrorNotReady) return UGO_FEC_OK;  // faulted: the block is dead
+      if (std::chrono::steady_clock::now() - t0 > grace) break;
+    }
+    svc_relax();
+  }
+  c->poisoned = true;
+  return UGO_FEC_ERR_HIP;
+}
+
 // One request: op on `groups` (<= kSvcMaxGroups) groups of the pinned
 // group-major batch at `mapped` (device view).  Statuses as the launch path.
 int svc_call(ugo_fec* c, uint32_t op, uint8_t* mapped, size_t groups, size_t S, size_t pitch, unsigned flags,
              const uint64_t* present, int8_t* status) {
   ugo::kern::SvcBox* b = c->svc_box;
-  if (!svc_ld(b->alive) && svc_launch(c) != UGO_FEC_OK) return UGO_FEC_ERR_HIP;
+  if (!svc_ld(b->alive) && svc_launch(c, c->svc_seq) != UGO_FEC_OK) return UGO_FEC_ERR_HIP;
   const uint32_t sq = svc_post(c, op, mapped, groups, S, pitch, flags, present);
   const auto t0 = std::chrono::steady_clock::now();
+  const auto limit = std::chrono::milliseconds(c->svc_timeout_ms);
   for (uint32_t spin = 0; svc_ld(b->done) != sq; ++spin) {
     if (!svc_ld(b->alive)) {  // it left before it saw this request
       if (svc_ld(b->done) == sq) break;
-      if (svc_launch(c) != UGO_FEC_OK) return UGO_FEC_ERR_HIP;
+      if (svc_launch(c, sq - 1) != UGO_FEC_OK) {
+        (void)svc_retire(c);
+        return UGO_FEC_ERR_HIP;
+      }
     }
-    if ((spin & 1023u) == 0 &&
-        (hipStreamQuery(c->svc_stream) == hipErrorLaunchFailure || std::chrono::steady_clock::now() - t0 > kSvcTimeout)) {
-      c->svc_on = false;  // a faulted or silent block: later calls take the launch path
+    if ((spin & 1023u) == 0 && (svc_faulted(c) || std::chrono::steady_clock::now() - t0 > limit)) {
+      // a faulted or silent block: it must be gone before this call returns (it
+      // may still be serving sq into the caller's batch); later calls take the
+      // launch path, or fail if it never leaves (poisoned)
+      (void)svc_retire(c);
       return UGO_FEC_ERR_HIP;
     }
     svc_relax();
@@ -708,17 +768,7 @@ int svc_call(ugo_fec* c, uint32_t op, uint8_t* mapped, size_t groups, size_t S, 
 
 int svc_stop(ugo_fec* c) {
   if (!c->svc_box) return UGO_FEC_OK;
-  c->svc_on = false;
-  ugo::kern::SvcBox* b = c->svc_box;
-  if (svc_ld(b->alive)) {
-    (void)svc_post(c, ugo::kern::kSvcStop, nullptr, 0, 0, 0, 0, nullptr);
-    const auto t0 = std::chrono::steady_clock::now();
-    while (svc_ld(b->alive)) {
-      if (std::chrono::steady_clock::now() - t0 > kSvcTimeout) return UGO_FEC_ERR_HIP;
-      svc_relax();
-    }
-  }
-  return hip_status(hipStreamSynchronize(c->svc_stream));
+  return svc_retire(c);
 }
 
 // Host path: chunks of stage_groups groups round-robin over kStreams streams:
@@ -912,6 +962,9 @@ int ugo_fec_create(int device, int data_shards, int parity_shards, ugo_fec** out
       for (int k = 0; k < d; ++k) ed[4 + c->dpad + c->epad + size_t(i) * c->dpad + k] = c->M[size_t(d + i) * d + k];
     if (hipMalloc(&c->d_encdesc, ed.size()) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
     if (hipMemcpy(c->d_encdesc, ed.data(), ed.size(), hipMemcpyHostToDevice) != hipSuccess) return fail(UGO_FEC_ERR_HIP);
+    if (hipMalloc(&c->d_rxseen, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_rxseen, 0, sizeof(unsigned long long)) != hipSuccess)
+      return fail(UGO_FEC_ERR_HIP);
   }
   if (n <= c->table_max && n <= 20) {
     const size_t entries = size_t(1) << n;
@@ -958,6 +1011,7 @@ int ugo_fec_encode_strided(ugo_fec* c, uint8_t* shards, size_t groups, size_t S,
 
 int ugo_fec_encode(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch, void* stream) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (pitch < S) return S == 0 ? UGO_FEC_ERR_SHARD_NO_DATA : UGO_FEC_ERR_INVALID_ARG;
   return ugo_fec_encode_strided(c, shards, groups, S, pitch, size_t(c->n) * pitch, stream);
 }
@@ -1009,6 +1063,7 @@ int ugo_fec_reconstruct_into(ugo_fec* c, const uint8_t* shards, const uint64_t* 
 int ugo_fec_reconstruct(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
                         size_t pitch, unsigned flags, int8_t* status, void* stream) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (pitch < S) return S == 0 ? UGO_FEC_ERR_SHARD_NO_DATA : UGO_FEC_ERR_INVALID_ARG;
   return ugo_fec_reconstruct_strided(c, shards, present, groups, S, pitch, size_t(c->n) * pitch, flags, status,
                                      stream);
@@ -1018,6 +1073,7 @@ int ugo_fec_reconstruct_rows(ugo_fec* c, const uint8_t* const* rows, const uint6
                              size_t S, uint8_t* out, size_t out_row_stride, size_t out_group_stride, unsigned flags,
                              int8_t* status, void* stream) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
   if (groups == 0) return UGO_FEC_OK;
   if (S > 0xffffffffu || c->n > 64 || !rows || !present || !out) return UGO_FEC_ERR_INVALID_ARG;
@@ -1099,6 +1155,7 @@ int ugo_fec_device_address(const ugo_fec* c, const void* p, void** dev) {
 
 int ugo_fec_service_start(ugo_fec* c, unsigned idle_us) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
   if (!c->svc_box) {
@@ -1118,19 +1175,33 @@ int ugo_fec_service_start(ugo_fec* c, unsigned idle_us) {
   // ugo_fec_destroy leaves no long-running wave behind
   const uint64_t us = std::min<uint64_t>(idle_us ? idle_us : 2000u, 1000000u);
   c->svc_idle_ticks = us * uint64_t(khz) / 1000u;
+  c->svc_khz = uint64_t(khz);
   c->svc_on = true;
   return UGO_FEC_OK;
 }
 
 int ugo_fec_service_stop(ugo_fec* c) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
   return svc_stop(c);
 }
 
+int ugo_fec_service_config(ugo_fec* c, unsigned timeout_ms, unsigned grace_ms, unsigned test_stall_us) {
+  if (!c || test_stall_us > 10000000u) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;
+  c->svc_timeout_ms = timeout_ms ? timeout_ms : 5000u;
+  c->svc_grace_ms = grace_ms ? grace_ms : 5000u;
+  c->svc_stall_us = test_stall_us;
+  return UGO_FEC_OK;
+}
+
+int ugo_fec_poisoned(const ugo_fec* c) { return c && c->poisoned ? 1 : 0; }
+
 int ugo_fec_encode_host(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (pitch < S) return S == 0 ? UGO_FEC_ERR_SHARD_NO_DATA : UGO_FEC_ERR_INVALID_ARG;
   int st = check_batch(c, shards, groups, S, interleaved(c, pitch));
   if (st || groups == 0 || c->p == 0) return st;
@@ -1143,6 +1214,7 @@ int ugo_fec_encode_host(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, si
 int ugo_fec_reconstruct_host(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
                              size_t pitch, unsigned flags, int8_t* status) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (pitch < S) return S == 0 ? UGO_FEC_ERR_SHARD_NO_DATA : UGO_FEC_ERR_INVALID_ARG;
   int st = check_batch(c, shards, groups, S, interleaved(c, pitch));
   if (st || groups == 0) return st;
@@ -1158,6 +1230,7 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
                         size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats,
                         void* stream) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
   if (npk == 0) return UGO_FEC_OK;
   if (!wire || !lens || !shards || !present || groups == 0 || c->n > 64 || npk >= 0xffffffffull)
@@ -1200,13 +1273,17 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   uint64_t* prev = static_cast<uint64_t*>(scratch);
   uint32_t* win = reinterpret_cast<uint32_t*>(prev + groups);
   uint32_t* dup = win + words;
-  // call entry: dup = 0 and the presence snapshot -- a (group, row) an earlier
-  // call placed keeps that call's copy (ugo/fec.go:123-129 keeps the first)
-  st = hip_status(ugo::kern::launch_rx_begin(present, prev, groups, dup, s));
+  // call entry, one launch: dup = 0, the presence snapshot -- a (group, row)
+  // an earlier call placed keeps that call's copy (ugo/fec.go:123-129 keeps the
+  // first) -- the claim words, and whether any presence bit was set at all (if
+  // none was, the place pass skips its per-packet snapshot lookups)
+  const unsigned long long call = ++c->rx_calls;
+  st = hip_status(ugo::kern::launch_rx_begin(present, prev, groups, dup, win, words, c->d_rxseen, call, s));
   a.dup = dup;
   a.prev = prev;
+  a.seen = c->d_rxseen;
+  a.call = call;
   if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
-  if (!st) st = hip_status(ugo::kern::launch_rx_fill(win, words, dup, s));
   ugo::kern::RxArgs f = a;  // the gated claim and re-place of the first copies
   f.win = win;
   f.gate = dup;
@@ -1223,6 +1300,7 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
                         uint32_t first_seq, const uint8_t* pad, size_t max_len, uint8_t* wire, size_t slot_out,
                         uint16_t* wire_lens, int8_t* status, void* stream) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (groups == 0) return UGO_FEC_OK;
   const uint64_t n = static_cast<uint64_t>(c->n);
   const uint32_t paws = static_cast<uint32_t>((0xffffffffull / n - 1) * n);  // ugo/fec.go:58
@@ -1273,6 +1351,7 @@ int ugo_fec_packet_decode(ugo_fec* c, const uint8_t* pkts, size_t slot, const ui
   static_assert(sizeof(ugo_pkt_info) == 64, "ugo_pkt_info is 64 bytes");
   static_assert(sizeof(ugo_pkt_segment) == 16, "ugo_pkt_segment is 16 bytes");
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (npk == 0) return UGO_FEC_OK;
   if (!pkts || !lens || !info || slot % 16 || slot == 0 || slot > 0xffff ||
       reinterpret_cast<uintptr_t>(pkts) % 16 || (pad && reinterpret_cast<uintptr_t>(pad) % 16) ||
@@ -1307,6 +1386,7 @@ int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size
 }
 
 int ugo_fec_timing_begin(ugo_fec* c, size_t max_launches) {
+  if (c && c->poisoned) return UGO_FEC_ERR_HIP;
   if (!c || max_launches == 0 || max_launches > (size_t(1) << 20)) return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
@@ -1356,6 +1436,10 @@ int ugo_fec_timing_end(ugo_fec* c, ugo_fec_launch_time* out, size_t cap, size_t*
 int ugo_fec_host_alloc(size_t bytes, void** out) {
   if (!out) return UGO_FEC_ERR_INVALID_ARG;
   *out = nullptr;
+  // fault injection for tests: UGO_FEC_HOST_ALLOC_LIMIT=<bytes> refuses larger
+  // pinned allocations (as a host out of pinnable memory would)
+  if (const char* lim = std::getenv("UGO_FEC_HOST_ALLOC_LIMIT"))
+    if (*lim && bytes > std::strtoull(lim, nullptr, 10)) return UGO_FEC_ERR_HIP;
   return hip_status(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
 }
 

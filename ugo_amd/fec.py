@@ -128,6 +128,8 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_reconstruct_host.argtypes = [vp, vp, vp, sz, sz, sz, u, vp]
     lib.ugo_fec_service_start.argtypes = [vp, u]
     lib.ugo_fec_service_stop.argtypes = [vp]
+    lib.ugo_fec_service_config.argtypes = [vp, u, u, u]
+    lib.ugo_fec_poisoned.argtypes = [vp]
     lib.ugo_fec_check_shards.argtypes = [i, vp, i, ctypes.POINTER(sz)]
     lib.ugo_fec_host_alloc.argtypes = [sz, ctypes.POINTER(vp)]
     lib.ugo_fec_host_free.argtypes = [vp]
@@ -409,6 +411,18 @@ class Encoder:
 
     def service_stop(self):
         _raise(load_library().ugo_fec_service_stop(self._h))
+
+    def service_config(self, timeout_ms: int = 0, grace_ms: int = 0, test_stall_us: int = 0):
+        """The service's watchdog (ugo_fec_service_config): a call's wait for an
+        answer and the wait for the workgroup to leave after a timeout (0 = 5000
+        ms each); test_stall_us (tests only) delays every request it serves."""
+        _raise(load_library().ugo_fec_service_config(self._h, timeout_ms, grace_ms, test_stall_us))
+
+    @property
+    def poisoned(self) -> bool:
+        """True if a service workgroup never left after a failed call (every call
+        on this context now fails; include/ugo_fec.h)."""
+        return bool(load_library().ugo_fec_poisoned(self._h))
 
     def encode_host(self, shards: np.ndarray, shard_size: Optional[int] = None):
         _require(shards.dtype == np.uint8 and shards.flags["C_CONTIGUOUS"] and shards.ndim == 3)
