@@ -103,6 +103,9 @@ def parse(argv=None):
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the PCIe-inclusive host_path leg (N = 1): pinned-host encode / reconstruct of "
                          "(10+3)x1350 x 65,536 and (32+8)x9000 x 8,192 groups")
+    ap.add_argument("--no-rx-tx", action="store_true",
+                    help="skip the rx_tx leg (N = 1): RX / TX assembly, data-only recovery and packet decode "
+                         "kernels with their nt-copy ceilings")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
@@ -226,6 +229,18 @@ def reduce_max(values, world: int):
         import torch.distributed as dist
 
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
+def reduce_sum(values, world: int):
+    """Element-wise sum over ranks of a list of numbers (host tensors)."""
+    import torch
+
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t.tolist()
 
 
@@ -427,13 +442,17 @@ def cpu_baseline(args, d, p, S, n):
 
     try:
         c0 = [sample(1) for _ in range(threads)]
-        v_all, n_all, t_all = leg(c0, 1, args.cpu_baseline_seconds)
-        v_one, n_one, t_one = leg(c0[:1], 1, args.cpu_baseline_seconds)
-        # per call on 1 core (the drop-in per-group path's CPU figure):
-        # the C loop makes one Encode / Reconstruct per group, no ctypes in between
+        # per call on 1 core (the drop-in per-group path's CPU figure),
+        # timed FIRST, before the all-core leg can leave the cgroup's quota
+        # throttled: the C loop makes one Encode / Reconstruct per group, no
+        # ctypes in between; 1 s of untimed calls first (clocks up)
         sh, masks = c0[0]
+        t_end = time.perf_counter() + 1.0
+        while time.perf_counter() < t_end:
+            rs_ref.c_encode(d, p, sh, threads=1)
+            rs_ref.c_reconstruct(d, p, sh, masks, threads=1)
         per = {"encode": [], "reconstruct_1loss": []}
-        for _ in range(20):
+        for _ in range(40):
             t0 = time.perf_counter()
             rs_ref.c_encode(d, p, sh, threads=1)
             t1 = time.perf_counter()
@@ -442,6 +461,11 @@ def cpu_baseline(args, d, p, S, n):
             per["encode"].append((t1 - t0) / sh.shape[0] * 1e6)
             per["reconstruct_1loss"].append((t2 - t1) / sh.shape[0] * 1e6)
         per_us = {k: round(sorted(v)[len(v) // 2], 3) for k, v in per.items()}
+        v_one, n_one, t_one = leg(c0[:1], 1, args.cpu_baseline_seconds)
+        v_all, n_all, t_all = leg(c0, 1, args.cpu_baseline_seconds)
+        # the pair time the steady single-core rate implies (agrees with per_us within ~10%)
+        pair_bytes = (d + p) * S + (d + 1) * S
+        pair_us_steady = round(pair_bytes / (v_one * 2**30) * 1e6, 3)
         del c0
         c2 = [sample(args.erasures) for _ in range(threads)]
         v_two, n_two, t_two = leg(c2, args.erasures, args.cpu_baseline_seconds / 2)
@@ -456,7 +480,12 @@ def cpu_baseline(args, d, p, S, n):
                      f"[{simd}], a C restatement of the klauspost algorithm and its SIMD strategy (the Go "
                      f"reference cannot run: go toolchain {info['go_toolchain']})",
            "single_core": {"value": v_one, "unit": "GiB/s", "cores": 1, "passes": n_one,
-                           "seconds": round(t_one, 2), "per_group_us": per_us},
+                           "seconds": round(t_one, 2), "per_group_us": per_us,
+                           "pair_us_per_group": round(per_us["encode"] + per_us["reconstruct_1loss"], 3),
+                           "pair_us_from_steady_rate": pair_us_steady,
+                           "note": "per_group_us timed before the all-core leg (no throttled quota); "
+                                   "pair_us_from_steady_rate = (encode + 1-loss reconstruct bytes per group) / "
+                                   "this leg's GiB/s"},
            "two_erasure": {"value": v_two, "unit": "GiB/s", "cores": threads, "passes": n_two,
                            "seconds": round(t_two, 2),
                            "sample": f"{threads} instances x 1024 groups, encode + {args.erasures}-erasure "
@@ -557,6 +586,23 @@ def strong_leg(args, enc, rank, world, dev, stream):
     es = erased.sort(dim=1).values.to(dev)
     ok = all(bool(torch.equal(out[j, :, :S], view[gi, es[:, j], :S])) for j in range(e))
     ok = all_ranks_ok(ok, world)
+    # the ceiling at this size: the encode's compute-free twin on this same
+    # batch (after the round trip: it writes wrong parity on purpose)
+    twin = None
+    if d == 10 and p == 3:
+        try:
+            import ctypes
+
+            import numpy as np
+
+            ms = np.zeros(4, np.float32)
+            bases = (ctypes.c_void_p * 1)(sh.data_ptr())
+            if probe_library().ugo_probe_encode_twin(bases, 1, G, S, pitch, sh.stride(0), 4, stream.cuda_stream,
+                                                     ms.ctypes.data) == 0:
+                twin = float(ms[1:].mean())
+        except Exception:  # noqa: BLE001
+            twin = None
+        twin = reduce_max([twin if twin is not None else -1.0], world)[0]
     step_bytes = total * (n * S + (d + e) * S)
     res = {"workload": f"BASELINE configs[3]: {total} groups ({d}+{p})x{S}B total, strong over {world} rank(s): "
                        f"{G} groups on rank 0, one cold planar batch per rank, encode + {e}-erasure "
@@ -566,16 +612,26 @@ def strong_leg(args, enc, rank, world, dev, stream):
            "ms_per_step": round(elapsed / args.c4_steps * 1e3, 4),
            "kernels_rank_max": kernel_stats(enc_ms, dec_ms, G * n * S, G * (d + e) * S, G * d * S),
            "verify_round_trip_full_size": ok}
+    if twin and twin > 0:
+        res["encode_twin_ms"] = round(twin, 4)
+        res["encode_frac_of_twin"] = round(twin / enc_ms, 4)
+        res["note"] = ("below the 65,536-group rate at N = 1: the loss is the access pattern's own at this "
+                       "footprint (HBM placement of a 74-GB batch), not the kernel -- encode_twin_ms is the "
+                       "encode's compute-free twin on this same batch, and the encode runs at encode_frac_of_twin "
+                       "of it (builder runs: profiles/r2/tlbprobe_r2.jsonl, profiles/r2/c4/c4_same_box_*.json, "
+                       "profiles/r3/capprobe_4m*.jsonl)")
     del sh, out, masks, view
     torch.cuda.empty_cache()
     return res
 
 
-def host_path_leg(args, dev_index):
+def host_path_leg(args, dev_index, rank=0, world=1, reps=3):
     """The PCIe-inclusive rate north_star asks for (the path starts and ends in
-    host memory: UDP socket buffers, /root/reference/ugo/conn.go:387-406).
-    Batches in pinned host memory (ugo_fec_host_alloc), group-major as a
-    packet ring lays them out:
+    host memory: UDP socket buffers, /root/reference/ugo/conn.go:387-406), on
+    every rank at once.  Each rank first binds itself to the
+    NUMA node of its GPU (ugo_amd/numa.py: hipDeviceGetPCIBusId -> sysfs
+    numa_node -> that node's CPUs), then allocates its pinned batches
+    (ugo_fec_host_alloc), group-major as a packet ring lays them out:
       * (10+3)x1350 x 65,536 groups: ugo_fec_encode_host, then 2 uniformly
         random erasures per group and ugo_fec_reconstruct_host;
       * (32+8)x9000 x 8,192 groups (BASELINE configs[4]): encode, then a
@@ -584,69 +640,118 @@ def host_path_leg(args, dev_index):
     The encode stages through device buffers (H2D of the data rows -> kernel
     -> D2H of the parity rows, pipelined over 3 streams); the reconstruct of a
     pinned batch runs zero-copy on its device mapping.  Each
-    call: 1 untimed + 3 timed, median.  Verified: every rebuilt batch equals
-    the encoded batch it was erased from (compared on the device)."""
+    call: 1 untimed, then `reps` timed, each rep started by a barrier over the
+    ranks; the rep's time is the max over ranks, the reported time the median
+    rep.  Aggregate GB/s = all ranks' bytes / that time.  Verified on every
+    rank: each rebuilt batch equals the encoded batch it was erased from
+    (compared on the device).  The process's CPU affinity is restored after."""
     import numpy as np
     import torch
 
-    from ugo_amd import fec
+    from ugo_amd import fec, numa
 
     dev = torch.device("cuda", dev_index)
-    res = {}
-    for d, p, S, G, mixed in ((10, 3, 1350, 65536, False), (32, 8, 9000, 8192, True)):
-        n = d + p
-        pitch = (S + 15) // 16 * 16
-        enc = fec.New(d, p, device=dev_index)
-        raw = fec.host_alloc(G * n * pitch)
+    place = numa.gpu_numa_node(dev_index)
+    saved = os.sched_getaffinity(0)
+    bound = numa.bind_to_node(place)
+    res = {"ranks": world}
+    all_ok = True
+    try:
+        for d, p, S, G, mixed in ((10, 3, 1350, 65536, False), (32, 8, 9000, 8192, True)):
+            n = d + p
+            pitch = (S + 15) // 16 * 16
+            enc = fec.New(d, p, device=dev_index)
+            raw = fec.host_alloc(G * n * pitch)
+            try:
+                buf = raw.reshape(G, n, pitch)
+                gen = torch.Generator(device=dev).manual_seed(args.seed + d + 7919 * rank)
+                torch.from_numpy(buf).copy_(torch.randint(0, 256, (G, n, pitch), dtype=torch.uint8, device=dev,
+                                                          generator=gen))
+
+                def timed(call):
+                    call()  # untimed
+                    return timed_reps(call, reps, world)
+
+                t_enc, t_enc_mine = timed(lambda: enc.encode_host(buf, S))
+                ref = torch.from_numpy(buf).to(dev)
+                rng = np.random.default_rng(args.seed + 7 * d + 104729 * rank)
+                ranks_ = rng.random((G, n)).argsort(axis=1).argsort(axis=1)  # rank of row r in a random order
+                ne = rng.integers(0, p + 1, G) if mixed else np.full(G, args.erasures)
+                erased = ranks_ < ne[:, None]  # ne[g] distinct rows, uniform
+                masks = np.zeros(G, np.uint64)
+                for r in range(n):
+                    masks |= (~erased[:, r]).astype(np.uint64) << np.uint64(r)
+                gi, ri = np.nonzero(erased)
+                buf[gi, ri] = 0
+                rcs = []
+
+                def rec():
+                    rcs.append(enc.reconstruct_host(buf, masks, S))
+
+                t_rec, t_rec_mine = timed(rec)
+                ok = all(rc == 0 for rc in rcs) and bool(
+                    torch.equal(torch.from_numpy(buf).to(dev)[:, :, :S], ref[:, :, :S]))
+                all_ok = all_ok and ok
+                del ref
+                e_tot = int(ne.sum())
+                lossy = int((ne > 0).sum())
+                b_enc = G * n * S
+                b_rec = lossy * d * S + e_tot * S
+                b_rec_all = int(reduce_sum([b_rec], world)[0])  # erasure counts differ by rank
+                key = f"{d}+{p}x{S}"
+                res[key] = {
+                    "groups_per_rank": G, "erasures": "U[0,%d] per group" % p if mixed else f"{args.erasures} per group",
+                    "encode_ms": round(t_enc * 1e3, 3), "encode_GBps": round(world * b_enc / t_enc / 1e9, 2),
+                    "encode_pcie_GBps": round(world * G * (d * pitch + p * S) / t_enc / 1e9, 2),
+                    "reconstruct_ms": round(t_rec * 1e3, 3),
+                    "reconstruct_GBps": round(b_rec_all / t_rec / 1e9, 2),
+                    "reconstruct_pcie_GBps": round(b_rec_all / t_rec / 1e9, 2),
+                    "rank0_alone_encode_ms": round(t_enc_mine * 1e3, 3),
+                    "rank0_alone_reconstruct_ms": round(t_rec_mine * 1e3, 3),
+                    "verify_round_trip": ok}
+            finally:
+                fec.host_free(raw)
+                enc.close()
+    finally:
         try:
-            buf = raw.reshape(G, n, pitch)
-            gen = torch.Generator(device=dev).manual_seed(args.seed + d)
-            torch.from_numpy(buf).copy_(torch.randint(0, 256, (G, n, pitch), dtype=torch.uint8, device=dev,
-                                                      generator=gen))
-            times = []
-            for k in range(4):
-                t0 = time.perf_counter()
-                enc.encode_host(buf, S)
-                times.append(time.perf_counter() - t0)
-            t_enc = sorted(times[1:])[1]
-            ref = torch.from_numpy(buf).to(dev)
-            rng = np.random.default_rng(args.seed + 7 * d)
-            ranks = rng.random((G, n)).argsort(axis=1).argsort(axis=1)  # rank of row r in a random order
-            ne = rng.integers(0, p + 1, G) if mixed else np.full(G, args.erasures)
-            erased = ranks < ne[:, None]  # ne[g] distinct rows, uniform
-            masks = np.zeros(G, np.uint64)
-            for r in range(n):
-                masks |= (~erased[:, r]).astype(np.uint64) << np.uint64(r)
-            gi, ri = np.nonzero(erased)
-            buf[gi, ri] = 0
-            times = []
-            for k in range(4):
-                t0 = time.perf_counter()
-                rc = enc.reconstruct_host(buf, masks, S)
-                times.append(time.perf_counter() - t0)
-                assert rc == 0, rc
-            t_rec = sorted(times[1:])[1]
-            ok = bool(torch.equal(torch.from_numpy(buf).to(dev)[:, :, :S], ref[:, :, :S]))
-            del ref
-            e_tot = int(ne.sum())
-            lossy = int((ne > 0).sum())
-            b_enc = G * n * S
-            b_rec = lossy * d * S + e_tot * S
-            key = f"{d}+{p}x{S}"
-            res[key] = {
-                "groups": G, "erasures": "U[0,%d] per group" % p if mixed else f"{args.erasures} per group",
-                "encode_ms": round(t_enc * 1e3, 3), "encode_GBps": round(b_enc / t_enc / 1e9, 2),
-                "encode_pcie_GBps": round(G * (d * pitch + p * S) / t_enc / 1e9, 2),
-                "reconstruct_ms": round(t_rec * 1e3, 3), "reconstruct_GBps": round(b_rec / t_rec / 1e9, 2),
-                "reconstruct_pcie_GBps": round(b_rec / t_rec / 1e9, 2),
-                "verify_round_trip": ok}
-        finally:
-            fec.host_free(raw)
-            enc.close()
-    res["note"] = ("pinned host batches, group-major; GBps = algorithmic bytes ((d+p)*S encode, (d+e)*S per lossy "
-                   "group reconstruct) / wall time of the synchronous call; pcie_GBps = bytes crossing PCIe (encode: "
-                   "d padded rows in + p rows out, staged; reconstruct: d survivor rows in + e rows out, zero-copy)")
+            os.sched_setaffinity(0, saved)
+        except OSError:
+            pass
+    res["verify_all_ranks"] = all_ranks_ok(all_ok, world)
+    me = {"rank": rank, "device": dev_index, "pci_bus_id": place["pci_bus_id"], "numa_node": place["numa_node"],
+          "bound": bound.get("bound", False), "cpus": bound.get("cpus")}
+    res["placement"] = gather_objects(me, world)
+    res["note"] = ("pinned host batches, group-major, allocated after each rank bound itself to its GPU's NUMA node; "
+                   "times: median over reps of the max over ranks (each rep starts at a barrier); GBps = all ranks' "
+                   "algorithmic bytes ((d+p)*S encode, (d+e)*S per lossy group reconstruct) / that time; pcie_GBps "
+                   "= bytes crossing PCIe (encode: d padded rows in + p rows out, staged; reconstruct: d survivor "
+                   "rows in + e rows out, zero-copy); bound: sum of per-GPU PCIe links and host DRAM (DESIGN.md §6)")
     return res
+
+
+def timed_reps(call, reps, world):
+    """`reps` calls, each started by a barrier over the ranks and timed on each
+    rank; returns (median over reps of the max over ranks, this rank's own
+    median): the job's time for one call when all ranks run it at once."""
+    ts = []
+    for _ in range(reps):
+        barrier(world)
+        t0 = time.perf_counter()
+        call()
+        ts.append(time.perf_counter() - t0)
+    mine = sorted(ts)[len(ts) // 2]
+    return sorted(reduce_max(ts, world))[len(ts) // 2], mine
+
+
+def gather_objects(obj, world):
+    """[obj of rank 0, ..., obj of rank world-1] (gloo/host)."""
+    if world <= 1:
+        return [obj]
+    import torch.distributed as dist
+
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def per_call_leg(args, dev_index):
@@ -658,7 +763,9 @@ def per_call_leg(args, dev_index):
     (ctypes: ~1 us of Python call overhead included) 2,000 times after 200
     untimed, median per call; first on the launch path, then with the per-call
     service on (ugo_fec_service_start).  Verified: the service's parity and
-    rebuilt shard equal the launch path's."""
+    rebuilt shard equal the launch path's.  Then what a resident service costs
+    everyone else (interference): the bench step and a PCIe-inclusive encode,
+    each timed alternately with and without a resident service block."""
     import ctypes
 
     import numpy as np
@@ -718,14 +825,391 @@ def per_call_leg(args, dev_index):
         enc.service_stop()
         res["service"]["same_bytes_as_launch"] = all(
             bool(np.array_equal(x, y)) for x, y in zip(outs["launch"], outs["service"]))
+        try:  # a secondary measurement: a failure is reported, never loses the leg
+            res["interference"] = service_interference(args, dev_index, enc, raw)
+        except Exception as ex:  # noqa: BLE001
+            res["interference"] = {"error": repr(ex)[:300]}
     finally:
+        enc.service_stop()
         fec.host_free(raw)
         enc.close()
     res["note"] = ("one (10+3) group per call through the C-ABI from Python (ctypes), the cgo shim's staging: "
                    "launch = one kernel launch + stream synchronize per call; service = ugo_fec_service_start "
-                   "(a resident workgroup polls a pinned mailbox); one GFNI CPU core: ~0.67 us Encode, ~0.48 us "
-                   "1-loss Reconstruct (DESIGN.md §4)")
+                   "(a resident workgroup polls a pinned mailbox); cpu_one_core_us: the same calls on one core of "
+                   "this host (cpu_baseline.single_core)")
     return res
+
+
+def service_interference(args, dev_index, enc, raw, rounds=3, steps=20):
+    """What a resident per-call service block (one CU held, a PCIe poll of its
+    pinned mailbox) costs concurrent batch work on the same GPU: the bench step
+    (encode + reconstruct_into of 65,536 (10+3) groups, 2 cold planar batches)
+    and the (10+3) x 65,536 pinned-host encode (PCIe-inclusive, launch path),
+    each timed `rounds` times alternately without and with the service
+    resident (started with a 1-s idle window and one served call just before
+    the timed work); medians.  Timing uses a dedicated stream and its events
+    (a device-wide synchronize would wait for the resident block)."""
+    import numpy as np
+    import torch
+
+    from ugo_amd import fec
+
+    d, p, S, G = 10, 3, 1350, 65536
+    n, pitch = d + p, 1360
+    dev = torch.device("cuda", dev_index)
+    s = torch.cuda.Stream(device=dev)
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 0x1F)
+    work = fec.New(d, p, device=dev_index)
+    bats = [torch.randint(0, 256, (n, G, pitch), dtype=torch.uint8, device=dev, generator=gen) for _ in range(2)]
+    outs = [torch.empty((p, G, pitch), dtype=torch.uint8, device=dev) for _ in range(2)]
+    masks, _ = make_masks(G, n, 2, args.seed + 0x2F, dev)
+    hraw = fec.host_alloc(G * n * pitch)
+    hbuf = hraw.reshape(G, n, pitch)
+    hbuf[:] = 7
+    one = raw[: n * 1472].reshape(1, n, 1472)
+    torch.cuda.synchronize()
+    try:
+        def step_ms():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(s):
+                for k in range(4):  # warm
+                    work.encode_batch(bats[k % 2], shard_size=S, stream=s, shard_major=True)
+                    work.reconstruct_into(bats[k % 2], masks, outs[k % 2], shard_size=S, stream=s, shard_major=True)
+                e0.record(s)
+                for k in range(steps):
+                    work.encode_batch(bats[k % 2], shard_size=S, stream=s, shard_major=True)
+                    work.reconstruct_into(bats[k % 2], masks, outs[k % 2], shard_size=S, stream=s, shard_major=True)
+                e1.record(s)
+            e1.synchronize()
+            return e0.elapsed_time(e1) / steps
+
+        def host_ms():
+            t0 = time.perf_counter()
+            work.encode_host(hbuf, S)
+            return (time.perf_counter() - t0) * 1e3
+
+        rows = {"off": {"step": [], "host": []}, "on": {"step": [], "host": []}}
+        for _ in range(rounds):
+            for mode in ("off", "on"):
+                if mode == "on":
+                    enc.service_start(idle_us=1_000_000)
+                    assert enc.encode_host(one, 1470) is None  # served: the block is now resident
+                rows[mode]["step"].append(step_ms())
+                rows[mode]["host"].append(host_ms())
+                if mode == "on":
+                    enc.service_stop()
+        med = {m: {k: float(np.median(v)) for k, v in r.items()} for m, r in rows.items()}
+        return {"step_ms_without": round(med["off"]["step"], 4), "step_ms_with_service": round(med["on"]["step"], 4),
+                "step_slowdown": round(med["on"]["step"] / med["off"]["step"] - 1, 4),
+                "host_encode_ms_without": round(med["off"]["host"], 3),
+                "host_encode_ms_with_service": round(med["on"]["host"], 3),
+                "host_encode_slowdown": round(med["on"]["host"] / med["off"]["host"] - 1, 4),
+                "rounds": rounds, "steps": steps,
+                "note": "service started with a 1-s idle window and one served call before each 'with' sample, "
+                        "so its block is resident (polling) through the sample"}
+    finally:
+        fec.host_free(hraw)
+        work.close()
+
+
+def probe_library():
+    """libugoprobe.so: the measurement kernels (ugo_amd/csrc/probe_kernels.hip)
+    behind the ceilings -- a separate library the product path never loads."""
+    import ctypes
+
+    path = os.path.join(ROOT, "ugo_amd", "libugoprobe.so")
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built: run `make -C ugo_amd/csrc`")
+    lib = ctypes.CDLL(path)
+    vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    lib.ugo_probe_encode_twin.argtypes = [vp, i, sz, sz, sz, sz, i, vp, vp]
+    lib.ugo_probe_nt_copy.argtypes = [vp, vp, i, sz, i, vp, vp]
+    return lib
+
+
+def probe_nt_copy_ms(srcs, dsts, nbytes, reps, stream):
+    """Average duration of `reps` nt copies of nbytes (srcs[r % n] -> dsts[r % n],
+    device pointers), each launch timed by its own start/stop events."""
+    import ctypes
+
+    import numpy as np
+
+    lib = probe_library()
+    nb = len(srcs)
+    S = (ctypes.c_void_p * nb)(*srcs)
+    D = (ctypes.c_void_p * nb)(*dsts)
+    ms = np.zeros(reps, np.float32)
+    rc = lib.ugo_probe_nt_copy(S, D, nb, nbytes // 16 * 16, reps, stream, ms.ctypes.data)
+    if rc:
+        raise RuntimeError(f"ugo_probe_nt_copy failed ({rc})")
+    return float(ms[1:].mean()) if reps > 1 else float(ms[0])
+
+
+def ceilings(args, batches, G, S, pitch, enc_bytes, stream):
+    """the encode's ceiling measured in this run, on the
+    same cold rotated batches (launch r on batch r % B): the compute-free twin
+    of k_encode_g (same loads, LDS stage, residency and nt stores; XOR instead
+    of the GF network) and a plain nt copy moving the same 1.15 GB (half a
+    batch read, the other half written).  Each launch timed with its own
+    hipExtLaunchKernel start/stop events, as the kernel pass times the encode.
+    The twin writes wrong parity on purpose: run after the verification."""
+    import ctypes
+
+    import numpy as np
+
+    lib = probe_library()
+    reps = max(8, min(args.steps, 40))
+    nb = len(batches)
+    bases = (ctypes.c_void_p * nb)(*[b.data_ptr() for b in batches])
+    ms = np.zeros(reps, np.float32)
+    rs = batches[0].stride(0)  # planar: bytes between row streams
+    rc = lib.ugo_probe_encode_twin(bases, nb, G, S, pitch, rs, reps, stream.cuda_stream, ms.ctypes.data)
+    if rc:
+        raise RuntimeError(f"ugo_probe_encode_twin failed ({rc})")
+    twin_ms = float(ms[1:].mean())
+    half = (batches[0].numel() // 2) // 16 * 16
+    copy_bytes = enc_bytes // 2 // 16 * 16  # read + written = the encode's algorithmic bytes
+    assert copy_bytes <= half
+    copy_ms = probe_nt_copy_ms([b.data_ptr() for b in batches], [b.data_ptr() + half for b in batches], copy_bytes,
+                               reps, stream.cuda_stream)
+    return {"encode_twin_ms": round(twin_ms, 5), "encode_twin_GBps": round(enc_bytes / (twin_ms * 1e-3) / 1e9, 1),
+            "nt_copy_ms": round(copy_ms, 5), "nt_copy_GBps": round(2 * copy_bytes / (copy_ms * 1e-3) / 1e9, 1),
+            "reps": reps}
+
+
+def rc4_pad(nbytes, dev):
+    import torch
+
+    from ugo_amd import fec
+
+    return torch.frombuffer(bytearray(fec.rc4_keystream(b"1234567890123456", nbytes)), dtype=torch.uint8).to(dev)
+
+
+def rx_tx_leg(args, dev_index, reps=12):
+    """The §8f kernels on the driver's clock, N = 1, after
+    the main line (nothing here feeds `value`).  Device-resident, cold: every
+    call alternates between 2 copies of its inputs and outputs.
+      * rx_assemble (ugo/conn.go:387-406 decrypt, ugo/fec.go:78-89 decode,
+        :107-175 grouping / dedupe / placement): a ring of 65,536 (10+3) groups
+        minus 5% uniform loss, 1476-B packets in 1488-B slots, RC4, into a
+        planar [13][G][1472] batch (S = 1470); arrival in seqid order (what a
+        UDP flow mostly delivers) and shuffled (worst case);
+      * reconstruct_into, data only, of the lossy groups of that batch
+        (input's Reconstruct, ugo/fec.go:196-207);
+      * tx_assemble (ugo/conn.go:643-685 sender loop + :634 encrypt): 65,536
+        groups of 10 full 1476-B packets -> 13 wire packets each, RC4;
+      * packet_decode (ugo/packet.go:138-177 after conn.go:387-419): 851,968
+        FEC-framed RC4 packets, one segment, a quarter with a SACK.
+    Kernel times from hipExtLaunchKernel events (every launch of the call),
+    bytes: RX packet bytes read + payload written; TX data packets read + wire
+    packets written; reconstruct d survivor rows read + e data rows written per
+    lossy group.  Next to each, an nt copy moving the same bytes in this
+    process (libugoprobe): the copy ceiling."""
+    import numpy as np
+    import torch
+
+    from ugo_amd import fec
+
+    d, p, n, S, pitch, slot = 10, 3, 13, 1470, 1472, 1488
+    G = 65536
+    dev = torch.device("cuda", dev_index)
+    stream = torch.cuda.current_stream(dev)
+    enc = fec.New(d, p, device=dev_index)
+    pad = rc4_pad(slot, dev)
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 0x5A)
+    out = {}
+
+    def kernel_ms(fn, kid, calls):
+        enc.timing_begin(16 * calls)
+        for r in range(calls):
+            fn(r)
+        recs, _ = enc.timing_end()
+        ids = kid if isinstance(kid, tuple) else (kid,)
+        return float(recs["ms"][np.isin(recs["kernel"], ids)].sum()) / calls
+
+    def wall_ms(fn, calls):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for r in range(calls):
+            fn(r)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / calls
+
+    def frac(b, ms):
+        return round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+
+    # ---- RX + data-only recovery
+    seq_all = torch.arange(G * n, device=dev, dtype=torch.int64)
+    keep = torch.rand(G * n, device=dev, generator=gen) >= 0.05
+    for order in ("in_order", "shuffled"):
+        seq = seq_all[keep]
+        if order == "shuffled":
+            seq = seq[torch.randperm(seq.numel(), device=dev, generator=gen)]
+        npk = seq.numel()
+        rings = []
+        for _ in range(2):
+            w = torch.randint(0, 256, (npk, slot), dtype=torch.uint8, device=dev, generator=gen)
+            hdr = torch.zeros((npk, 6), dtype=torch.uint8, device=dev)
+            for b in range(4):
+                hdr[:, b] = ((seq >> (8 * b)) & 0xFF).to(torch.uint8)
+            hdr[:, 4] = torch.where(seq % n < d, 0xF1, 0xF2).to(torch.uint8)
+            w[:, :6] = hdr ^ pad[:6]
+            rings.append(w)
+        lens = torch.full((npk,), 1476, dtype=torch.int16, device=dev)
+        bats = [torch.empty((n, G, pitch), dtype=torch.uint8, device=dev) for _ in range(2)]
+        pres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
+        outs = [torch.empty((p, G, pitch), dtype=torch.uint8, device=dev) for _ in range(2)]
+        st = torch.zeros(5, dtype=torch.int32, device=dev)
+
+        def rx(r):
+            i = r % 2
+            pres[i].zero_()
+            enc.rx_assemble(rings[i], lens, bats[i], pres[i], shard_size=S, pad=pad, stats=st)
+
+        def rec(r):
+            i = r % 2
+            enc.reconstruct_into(bats[i], pres[i], outs[i], shard_size=S, data_only=True, shard_major=True)
+
+        for r in range(4):
+            rx(r)
+            rec(r)
+        st.zero_()
+        rx(0)
+        torch.cuda.synchronize()
+        stats = st.tolist()
+        # spot check of the placement: 4,096 packets' payloads, decrypted, in their rows
+        pick = torch.randint(0, npk, (4096,), device=dev, generator=gen)
+        sq = seq[pick]
+        want = rings[0][pick, 6:6 + S] ^ pad[6:6 + S]
+        got = bats[0][sq % n, sq // n, :S]
+        ok = stats == [npk, 0, 0, 0, 0] and bool(torch.equal(got, want))
+        rx_k = kernel_ms(rx, fec.KERNEL_IDS["rx_assemble"], reps)
+        rx_w = wall_ms(rx, reps)
+        rec_k = kernel_ms(rec, (fec.KERNEL_IDS["reconstruct"], fec.KERNEL_IDS["prepare"]), reps)
+        m = pres[0].cpu().numpy().view(np.uint64)
+        lost_data = np.zeros(G, np.int64)
+        for r in range(d):
+            lost_data += ((m >> np.uint64(r)) & np.uint64(1)) == 0
+        pop = np.zeros(G, np.int64)
+        for r in range(n):
+            pop += ((m >> np.uint64(r)) & np.uint64(1)).astype(np.int64)
+        recoverable = (lost_data > 0) & (pop >= d)
+        rec_bytes = int((recoverable * (d + lost_data)).sum()) * S
+        rx_bytes = npk * (1476 + S)
+        copy_ms = probe_nt_copy_ms([rings[i].data_ptr() for i in range(2)], [bats[(i + 1) % 2].data_ptr()
+                                                                            for i in range(2)],
+                                   rx_bytes // 2, reps, stream.cuda_stream)
+        out[f"rx_{order}"] = {
+            "packets": npk, "groups": G, "loss": 0.05, "rc4": True,
+            "rx_assemble_ms": round(rx_k, 4), "rx_assemble_wall_ms": round(rx_w, 4),
+            "rx_GBps": round(rx_bytes / (rx_k * 1e-3) / 1e9, 1), "rx_frac": frac(rx_bytes, rx_k),
+            "rx_Mpkt_per_s": round(npk / (rx_k * 1e-3) / 1e6, 1),
+            "nt_copy_same_bytes_ms": round(copy_ms, 4), "nt_copy_frac": frac(rx_bytes, copy_ms),
+            "rx_frac_of_copy": round(copy_ms / rx_k, 4),
+            "recover_lossy_groups": int(recoverable.sum()), "reconstruct_into_data_only_ms": round(rec_k, 4),
+            "reconstruct_GBps": round(rec_bytes / (rec_k * 1e-3) / 1e9, 1), "reconstruct_frac": frac(rec_bytes, rec_k),
+            "stats": stats, "verify_spot_4096": ok}
+        del rings, bats, pres, outs
+        torch.cuda.empty_cache()
+
+    # ---- TX
+    max_len = 1476
+    pks = [torch.randint(0, 256, (G * d, slot), dtype=torch.uint8, device=dev, generator=gen) for _ in range(2)]
+    tl = torch.full((G * d,), max_len, dtype=torch.int16, device=dev)
+    wires = [torch.empty((G * n, slot), dtype=torch.uint8, device=dev) for _ in range(2)]
+    wls = [torch.empty(G * n, dtype=torch.int16, device=dev) for _ in range(2)]
+
+    def tx(r):
+        i = r % 2
+        enc.tx_assemble(pks[i], tl, wires[i], wls[i], pad=pad, max_len=max_len)
+
+    for r in range(4):
+        tx(r)
+    torch.cuda.synchronize()
+    # spot check: data packet k of group g on the wire = header + payload, encrypted
+    g = 12345
+    w0 = (wires[1][g * n: g * n + d, :max_len] ^ pad[:max_len])
+    ok_tx = bool(torch.equal(w0[:, 6:], pks[1][g * d: g * d + d, 6:max_len])) and bool(
+        (wls[1][g * n: g * n + n] == max_len).all())
+    tx_k = kernel_ms(tx, fec.KERNEL_IDS["tx_assemble"], reps)
+    tx_bytes = G * (d + n) * max_len
+    copy_ms = probe_nt_copy_ms([pks[i].data_ptr() for i in range(2)], [wires[i].data_ptr() for i in range(2)],
+                               tx_bytes // 2, reps, stream.cuda_stream)
+    out["tx"] = {"groups": G, "packets_out": G * n, "rc4": True, "tx_assemble_ms": round(tx_k, 4),
+                 "tx_GBps": round(tx_bytes / (tx_k * 1e-3) / 1e9, 1), "tx_frac": frac(tx_bytes, tx_k),
+                 "tx_Mpkt_per_s": round(G * n / (tx_k * 1e-3) / 1e6, 1),
+                 "nt_copy_same_bytes_ms": round(copy_ms, 4), "nt_copy_frac": frac(tx_bytes, copy_ms),
+                 "tx_frac_of_copy": round(copy_ms / tx_k, 4), "verify_spot": ok_tx}
+    del pks, wires, wls
+    torch.cuda.empty_cache()
+
+    # ---- packet decode
+    out["packet_decode"] = packet_decode_case(enc, dev, reps, kernel_ms)
+    out["note"] = ("kernel ms = sum of the call's launches (hipExtLaunchKernel events); frac = algorithmic bytes / "
+                   "kernel time / 8 TB/s; nt_copy = libugoprobe's one-chunk-per-thread nt copy moving the same "
+                   "bytes on the same cold buffers; rx_wall includes the caller's present.zero_() per call")
+    enc.close()
+    return out
+
+
+def packet_decode_case(enc, dev, reps, kernel_ms, npk=851968):
+    """ugo_fec_packet_decode over npk received packets: FEC-framed, RC4, flags
+    PSH (a quarter with a SACK frame), 3-byte packet number, one 1400-B segment."""
+    import numpy as np
+    import torch
+
+    from ugo_amd import fec
+
+    slot = 1488
+    rng = np.random.default_rng(11)
+    host = rng.integers(0, 256, (npk, slot), dtype=np.uint8)
+    seqn = np.arange(npk, dtype=np.uint64)
+    host[:, 0:4] = seqn.astype("<u4").view(np.uint8).reshape(npk, 4)
+    host[:, 4] = 0xF1
+    host[:, 5] = 0
+
+    def uvarint(v, nbytes):
+        o = np.zeros((v.size, nbytes), np.uint8)
+        for j in range(nbytes):
+            o[:, j] = ((v >> np.uint64(7 * j)) & np.uint64(0x7F)).astype(np.uint8)
+            if j < nbytes - 1:
+                o[:, j] |= 0x80
+        return o
+
+    ack = rng.random(npk) < 0.25
+    pos = np.full(npk, 7)
+    host[:, 6] = np.where(ack, 0xA0, 0x20)
+    sack = np.concatenate([np.zeros((npk, 1), np.uint8), uvarint(seqn + np.uint64(1 << 15), 3),
+                           np.full((npk, 2), 7, np.uint8), np.full((npk, 1), 5, np.uint8)], axis=1)
+    rows = np.nonzero(ack)[0]
+    host[rows[:, None], 7 + np.arange(7)[None, :]] = sack[rows]
+    pos[ack] += 7
+    hdr = np.concatenate([uvarint(seqn + np.uint64(1 << 15), 3), uvarint(seqn * np.uint64(1400), 4),
+                          np.tile(np.array([[1400 >> 8, 1400 & 0xFF]], np.uint8), (npk, 1))], axis=1)
+    for j in range(9):
+        host[np.arange(npk), pos + j] = hdr[:, j]
+    lens = (pos + 9 + 1400).astype(np.int16)
+    ks = np.frombuffer(fec.rc4_keystream(b"1234567890123456", slot), np.uint8)
+    host ^= ks[None, :]
+    d_pk = torch.from_numpy(host).to(dev)
+    d_len = torch.from_numpy(lens).to(dev)
+    pad = torch.from_numpy(ks.copy()).to(dev)
+    bufs = enc.packet_decode(d_pk, d_len, pad=pad, framed=True, max_ranges=4, max_segments=2)
+    torch.cuda.synchronize()
+    info = bufs[0].cpu().numpy().view(fec.PKT_INFO_DTYPE).reshape(-1)
+    ok = bool((info["status"] == 0).all() and (info["n_segments"] == 1).all())
+
+    def run(_r):
+        enc.packet_decode(d_pk, d_len, pad=pad, framed=True, max_ranges=4, max_segments=2, out=bufs)
+
+    for r in range(3):
+        run(r)
+    ms = kernel_ms(run, fec.KERNEL_IDS["packet_decode"], reps)
+    return {"packets": npk, "packet_decode_ms": round(ms, 4), "Mpkt_per_s": round(npk / (ms * 1e-3) / 1e6, 1),
+            "bound": "latency (one thread per packet parses ~64 B; segment data is located, not read)",
+            "verify_all_decode": ok}
 
 
 def run_rank(args):
@@ -839,19 +1323,38 @@ def run_rank(args):
         verify = {"round_trip_full_size": ok_rt, "encode_idempotent": ok_idem}
         verify["all_ranks_ok"] = all_ranks_ok(ok_rt and ok_idem, world)
 
+    # 2b. Ceilings on the same cold rotated batches (after the verification:
+    #     the compute-free twin writes wrong parity on purpose).
+    ceil = None
+    if planar and args.row_pad == 0 and d == 10 and p == 3 and nb >= 1:
+        try:
+            ceil = ceilings(args, batches, G, S, pitch, G * n * S, stream)
+        except Exception as ex:  # noqa: BLE001 -- a secondary measurement never loses the line
+            ceil = {"error": repr(ex)[:300]}
+
     # 3. Secondary legs, after the main line's measurement (nothing in them
     #    feeds `value`): BASELINE configs[3] strong over the ranks, and at N = 1
     #    the PCIe-inclusive host path (configs[4] among it).
     batches = outs = shards = view = None
     torch.cuda.empty_cache()
     strong = strong_leg(args, enc, rank, world, dev, stream) if args.c4_total_groups > 0 else None
-    host = host_path_leg(args, dev_index) if (world == 1 and not args.no_host_path) else None
-    per_call = None
+    host = None
+    if not args.no_host_path:
+        try:  # every rank at once, NUMA-local (a secondary leg: failures are reported, never lose the line)
+            host = host_path_leg(args, dev_index, rank, world)
+        except Exception as ex:  # noqa: BLE001
+            host = {"error": repr(ex)[:300]}
+    per_call = rx_tx = None
     if world == 1 and not args.no_host_path:
-        try:  # a secondary leg: a failure here is reported in the line, never loses it
+        try:
             per_call = per_call_leg(args, dev_index)
         except Exception as ex:  # noqa: BLE001
             per_call = {"error": repr(ex)[:300]}
+    if world == 1 and not args.no_rx_tx:
+        try:
+            rx_tx = rx_tx_leg(args, dev_index)
+        except Exception as ex:  # noqa: BLE001
+            rx_tx = {"error": repr(ex)[:300]}
 
     if rank == 0:
         payload = G * d * S  # klauspost's convention: data bytes per call (BASELINE.md secondary column)
@@ -869,13 +1372,25 @@ def run_rank(args):
                         "MI355X_MICROARCH.md), not counters read in this run") if traffic else None
         ach = kern[dom]["GBps"]
         roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic}
+        if ceil and "encode_twin_GBps" in ceil and dom == "encode":
+            roof["ceiling_GBps"] = ceil["encode_twin_GBps"]
+            roof["frac_of_ceiling"] = round(ach / ceil["encode_twin_GBps"], 4)
+            roof["nt_copy_GBps"] = ceil["nt_copy_GBps"]
+            roof["ceiling"] = dict(ceil, what=(
+                "measured in this run on the same 2 cold rotated batches: encode_twin = k_encode_g's compute-free "
+                "twin (same LDS-DMA / register loads, 52-KiB stage = 3 blocks per CU, nt stores; XOR instead of the "
+                "GF network), GBps of the encode's algorithmic bytes; nt_copy = a 1-chunk-per-thread nt copy "
+                "moving the same 1.15 GB (libugoprobe.so, ugo_amd/csrc/probe_kernels.hip)"))
+        elif ceil:
+            roof["ceiling"] = ceil
+        roof.update({
                 "note": f"achieved = algorithmic bytes per launch ({'(d+p)*S' if dom == 'encode' else '(d+e)*S'}"
                         f" per group x {G} groups) / avg kernel duration over a kernel-timing pass of the same "
                         f"{args.steps} steps right after the timed region, from hipExtLaunchKernel start/stop "
                         f"events on the launch stream (ms_per_step of that pass: "
                         f"{elapsed_timing_pass / args.steps * 1e3:.4f})"
-                        + (f"; {traffic_note}" if traffic_note else "")}
+                        + (f"; {traffic_note}" if traffic_note else "")})
         if scaling == "strong":
             workload = f"{total_groups} groups total, strong: {G} groups on rank 0"
         else:
@@ -908,8 +1423,15 @@ def run_rank(args):
             out["host_path"] = host
         if per_call is not None:
             out["per_call"] = per_call
+        if rx_tx is not None:
+            out["rx_tx"] = rx_tx
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, d, p, S, n)
+            if per_call is not None and "launch" in per_call:
+                sc = out["cpu_baseline"]["single_core"]
+                per_call["cpu_one_core_us"] = {"encode": sc["per_group_us"]["encode"],
+                                               "reconstruct_1loss": sc["per_group_us"]["reconstruct_1loss"],
+                                               "pair_from_steady_rate": sc["pair_us_from_steady_rate"]}
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -43,6 +43,26 @@ def main():
     masks = np.full(G, ((1 << n) - 1) & ~(1 << 2) & ~(1 << 11), np.uint64)
     rs_ref.c_reconstruct(d, p, erased, masks)
     ok = ok and bool(np.array_equal(erased, mine))
+    # host-path coordination (bench.host_path_leg): NUMA placement from a fake
+    # sysfs, barrier-started reps timed as max over ranks, summed bytes
+    host = None
+    sysfs = os.environ.get("BENCH_TEST_SYSFS")
+    if sysfs:
+        from ugo_amd import numa
+
+        bdf = ["0000:0b:00.0", "0000:8c:00.0"][rank % 2]
+        place = numa.gpu_numa_node(rank, sysfs=sysfs, bdf=bdf)
+        saved = os.sched_getaffinity(0)
+        bound = numa.bind_to_node(place)
+        now = sorted(os.sched_getaffinity(0))
+        os.sched_setaffinity(0, saved)
+        import time
+
+        t_job, t_mine = bench.timed_reps(lambda: time.sleep(0.01 * (1 + 2 * rank)), 3, world)
+        total_bytes = bench.reduce_sum([1000 * (rank + 1)], world)[0]
+        placement = bench.gather_objects({"rank": rank, "numa_node": place["numa_node"], "cpus": now,
+                                          "bound": bound["bound"]}, world)
+        host = {"t_job": t_job, "t_mine": t_mine, "bytes": total_bytes, "placement": placement}
     tmax, gmax, ranks = bench.reduce_max([0.5 + rank, G, rank], world)
     covered = bench.reduce_max([g0 + G if rank == world - 1 else 0], world)[0]
     all_ok = bench.all_ranks_ok(ok, world)
@@ -50,7 +70,8 @@ def main():
     if rank == 0:
         print(json.dumps({"metric": "test", "n_gpus": world, "scaling": scaling, "total_groups": tot,
                           "tmax": tmax, "gmax": gmax, "max_rank": ranks, "covered": covered, "all_ok": all_ok,
-                          "one_bad": one_bad, "elapsed_pos": elapsed > 0, "cw_steps": cw_steps}), flush=True)
+                          "one_bad": one_bad, "elapsed_pos": elapsed > 0, "cw_steps": cw_steps, "host": host}),
+              flush=True)
     else:
         print("rank %d noise on stdout" % rank, flush=True)
     import torch.distributed as dist

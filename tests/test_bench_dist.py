@@ -152,3 +152,61 @@ def test_cgroup_quota_parsing(tmp_path, monkeypatch):
     monkeypatch.setattr("builtins.open", fake_open)
     q, src = bench.cgroup_cpu_quota()
     assert q == 16.0 and src.endswith("a/cpu.max")
+
+
+def _fake_sysfs(root, cpus):
+    """Two GPUs on two NUMA nodes, each node with half of `cpus`."""
+    half = len(cpus) // 2 or 1
+    nodes = {0: cpus[half:] or cpus, 1: cpus[:half]}
+    for bdf, node in (("0000:0b:00.0", 1), ("0000:8c:00.0", 0)):
+        d = os.path.join(root, "bus", "pci", "devices", bdf)
+        os.makedirs(d)
+        with open(os.path.join(d, "numa_node"), "w") as f:
+            f.write(f"{node}\n")
+    for node, cs in nodes.items():
+        d = os.path.join(root, "devices", "system", "node", f"node{node}")
+        os.makedirs(d)
+        with open(os.path.join(d, "cpulist"), "w") as f:
+            f.write(",".join(str(c) for c in cs) + "\n")
+    return nodes
+
+
+def test_numa_lookup_and_binding_on_a_fake_sysfs(tmp_path):
+    from ugo_amd import numa
+
+    cpus = sorted(os.sched_getaffinity(0))
+    nodes = _fake_sysfs(str(tmp_path), cpus)
+    assert numa.parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    info = numa.gpu_numa_node(0, sysfs=str(tmp_path), bdf="0000:0b:00.0")
+    assert info["numa_node"] == 1 and info["node_cpus"] == nodes[1]
+    assert numa.gpu_numa_node(0, sysfs=str(tmp_path), bdf="0000:ff:00.0")["numa_node"] is None
+    saved = os.sched_getaffinity(0)
+    try:
+        r = numa.bind_to_node(info)
+        assert r["bound"] and sorted(os.sched_getaffinity(0)) == nodes[1]
+    finally:
+        os.sched_setaffinity(0, saved)
+    assert not numa.bind_to_node({"node_cpus": []})["bound"]
+
+
+def test_host_path_coordination_two_ranks(tmp_path, capfd, monkeypatch):
+    """bench.host_path_leg's multi-rank pieces on 2 gloo ranks: each rank finds
+    its GPU's NUMA node in (a fake) sysfs and binds to that node's CPUs; a rep
+    starts at a barrier and counts as the slowest rank's time; bytes are summed
+    over ranks; every rank's placement reaches rank 0's line."""
+    cpus = sorted(os.sched_getaffinity(0))
+    nodes = _fake_sysfs(str(tmp_path), cpus)
+    monkeypatch.setenv("BENCH_TEST_SYSFS", str(tmp_path))
+    monkeypatch.setenv("BENCH_TEST_TOTAL", "100")
+    rc = bench.launch(["--gpus", "2"], 2, script=RANK_SCRIPT, timeout=240)
+    out, err = capfd.readouterr()
+    assert rc == 0, err[-2000:]
+    r = json.loads([ln for ln in out.splitlines() if ln.strip()][0])
+    h = r["host"]
+    assert 0.029 <= h["t_job"] < 0.5, "the job's time is the slower rank's (30 ms)"
+    assert 0.0099 <= h["t_mine"] < h["t_job"], "rank 0's own time is its own (10 ms)"
+    assert h["bytes"] == 3000
+    pl = h["placement"]
+    assert [x["rank"] for x in pl] == [0, 1]
+    assert pl[0]["numa_node"] == 1 and pl[0]["cpus"] == nodes[1] and pl[0]["bound"]
+    assert pl[1]["numa_node"] == 0 and pl[1]["cpus"] == nodes[0] and pl[1]["bound"]

@@ -100,6 +100,7 @@ PKT_INFO_DTYPE = np.dtype([("packet_number", "<u8"), ("stop_waiting", "<u8"), ("
 # include/ugo_fec.h launch timing
 KERNEL_NAMES = {1: "encode", 2: "reconstruct", 3: "prepare", 4: "bytes", 5: "rx_assemble", 6: "tx_assemble",
                 7: "packet_decode"}
+KERNEL_IDS = {v: k for k, v in KERNEL_NAMES.items()}
 LAUNCH_TIME_DTYPE = np.dtype([("kernel", "<u4"), ("ms", "<f4")])
 PKT_SEGMENT_DTYPE = np.dtype([("offset", "<u8"), ("data_off", "<u4"), ("len", "<u2"), ("avail", "<u2")])
 assert PKT_INFO_DTYPE.itemsize == 64 and PKT_SEGMENT_DTYPE.itemsize == 16
