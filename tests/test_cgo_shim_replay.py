@@ -55,9 +55,10 @@ class GoShim:
         self.stage, self.stageN = ctypes.c_void_p(), 0
 
     def close(self):  # func (e *Encoder) Close
-        if self.stage:
-            self.lib.ugo_fec_host_free(self.stage)
+        poisoned = self.lib.ugo_fec_poisoned(self.ctx) != 0
         self.lib.ugo_fec_destroy(self.ctx)
+        if self.stage and not poisoned:
+            self.lib.ugo_fec_host_free(self.stage)
 
     def ServiceStart(self, idle_us):  # func (e *Encoder) ServiceStart(idleUs uint) error
         status_err(self.lib.ugo_fec_service_start(self.ctx, idle_us))

@@ -405,6 +405,28 @@ int main(int argc, char** argv) {
                   k_pat_gather1<<<(G * n * 92 + 255) / 256, 256>>>(rot[k].wire, rot[k].shards, d_sidx, G * n);
                 }, {}});
   for (const Var& v : vars) ts.push_back({v.name, [&, v] { run(v, rot[cnt++ % 3], nullptr); }, {}});
+  uint32_t* d_cnt;
+  CK(hipMalloc(&d_cnt, 4 * 32 * 4));
+  auto chunk_variant = [&](int nt) {
+    return [&, nt] {
+      RxArgs a = rot[cnt++ % 3];
+      CK(hipMemsetAsync(a.present, 0, a.groups * 8, nullptr));
+      const unsigned long long call = ++call_id;
+      CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, nullptr));
+      CK(hipMemsetAsync(d_cnt, 0, 4 * 32 * 4, nullptr));
+      a.prev = prev;
+      a.seen = d_seen;
+      a.call = call;
+      const uint64_t items = a.npk * 92;
+      if (nt == 3)
+        k_rx_chunk<3><<<(items + 255) / 256, 256>>>(a, 92, d_cnt);
+      else
+        k_rx_chunk<2><<<(items + 255) / 256, 256>>>(a, 92, d_cnt);
+    };
+  };
+  ts.push_back({"chunk-per-thread place, full grid, nt loads+stores (+memset present, begin, memset counters)",
+                chunk_variant(3), {}});
+  ts.push_back({"chunk-per-thread place, full grid, plain loads, nt stores (+memsets, begin)", chunk_variant(2), {}});
   ts.push_back({"index only (fill + index)", [&] {
                   RxArgs a = rot[cnt++ % 3];
                   a.win = win;

@@ -368,6 +368,116 @@ __global__ __launch_bounds__(256) void k_rx_sum_parts(const uint32_t* parts, uin
 }
 
 // ---------------------------------------------------------------------------
+// One 16-B output chunk per thread, full grid (k_rx_chunk).
+//
+// Thread t owns chunk m = t % nq of packet i = t / nq (nq = ceil(S / 16)
+// chunks per row): every load it needs -- the packet's header chunk and
+// length (shared by the packet's threads: one line per wave), its own payload
+// chunk, the keystream -- depends on t alone, so all are issued at once; the
+// neighbour chunk the 6-B realignment needs comes from lane + 1 by DPP (a
+// separate load only at a packet's last chunk and in lane 63).  Nothing waits
+// on a second round trip in the usual case: with no presence bit set at call
+// entry (a->seen, k_rx_begin) there is no snapshot lookup, and the presence
+// bit is OR-ed by the packet's chunk-0 thread with a no-return atomic.  A
+// duplicate is found afterwards instead (k_rx_count: per group, the bits this
+// call set against the packets it accepted).  The per-call counters go to
+// 32 sharded words (cnt[k * 32 + shard], shard = block % 32): bad flag, out of
+// window, too short -- rare -- and accepted packets, one add per block.
+// This is the access shape of the fastest scatter measured
+// (tools/rxgather.hip P2: one chunk per thread, full grid).
+constexpr uint32_t kRxShards = 32;
+
+template <int NT = 3>
+__global__ __launch_bounds__(256) void k_rx_chunk(RxArgs a, uint32_t nq, uint32_t* cnt) {
+  __shared__ uint32_t bacc;
+  if (threadIdx.x == 0) bacc = 0;
+  __syncthreads();
+  const uint64_t t = blockIdx.x * 256ull + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool live = t < a.npk * nq;
+  const uint64_t i = live ? t / nq : 0;
+  const uint32_t m = static_cast<uint32_t>(t - i * nq);
+  const uint32_t o = 16u * m;
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  const uint8_t* pk = a.wire + i * a.slot;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  // all loads first: header chunk, length, payload chunk, keystream
+  u32x4 h = live ? ld16(pk) : zero;
+  const uint32_t len = live ? min(static_cast<uint32_t>(a.lens[i]), slot) : 0u;
+  u32x4 A = (live && o + 16u <= slot) ? ((NT & 1) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + o))
+                                                  : ld16(pk + o))
+                                      : zero;
+  const bool own_b = lane == 63u || m + 1u == nq;  // the neighbour chunk is not in lane + 1
+  u32x4 B = zero;
+  if (live && own_b && o + 32u <= slot) B = ld16(pk + o + 16u);
+  if (a.pad) {
+    h ^= ld16(a.pad);
+    if (o + 16u <= slot) A ^= ld16(a.pad + o);
+    if (own_b && o + 32u <= slot) B ^= ld16(a.pad + o + 16u);
+  }
+  const bool chk_prev = a.prev && !(a.seen && *a.seen < a.call);
+  uint32_t why = live ? 0u : 5u;
+  const uint32_t seqid = h.x;
+  const uint32_t flag = h.y & 0xffffu;
+  if (why == 0 && len < 6u) why = 3;
+  else if (why == 0 && flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
+  const uint32_t row = seqid % a.n;
+  const uint64_t grp = seqid / a.n;
+  if (why == 0 && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
+  const uint64_t gs = grp - a.first_group;
+  if (why == 0 && chk_prev && ((a.prev[gs] >> row) & 1ull)) why = 4;  // an earlier call's seqid
+  // neighbour chunk (packet bytes [o+16, o+32)) from lane + 1, converged
+  const uint32_t nx = from_next_lane(A.x), ny = from_next_lane(A.y);
+  const uint32_t bx = own_b ? B.x : nx, by = own_b ? B.y : ny;
+  if (why == 0 && o < a.S) {
+    const uint32_t L = min(len - 6u, a.S);  // payload bytes kept
+    uint32_t w[4];
+    w[0] = __builtin_amdgcn_alignbyte(A.z, A.y, 2);
+    w[1] = __builtin_amdgcn_alignbyte(A.w, A.z, 2);
+    w[2] = __builtin_amdgcn_alignbyte(bx, A.w, 2);
+    w[3] = __builtin_amdgcn_alignbyte(by, bx, 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
+      const uint32_t b0 = o + 4u * j;
+      const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
+      w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+    }
+    uint8_t* dst = a.shards + row * a.rstride + gs * a.gstride + o;
+    const uint32_t nb = a.S - o;
+    if (nb >= 16u) {
+      const u32x4 v = {w[0], w[1], w[2], w[3]};
+      if constexpr (NT & 2)
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+      else
+        *reinterpret_cast<u32x4*>(dst) = v;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = 4u * j;
+        if (nb >= lo + 4u) {
+          *reinterpret_cast<uint32_t*>(dst + lo) = w[j];
+        } else if (nb > lo) {
+          for (uint32_t q = 0; q < nb - lo; ++q) dst[lo + q] = static_cast<uint8_t>(w[j] >> (8u * q));
+        }
+      }
+    }
+  }
+  if (m == 0 && live) {
+    const uint32_t shard = blockIdx.x % kRxShards;
+    if (why == 0) {
+      atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
+      atomicAdd(&bacc, 1u);
+    } else if (why < 4 && cnt) {
+      atomicAdd(&cnt[why * kRxShards + shard], 1u);
+    }
+  }
+  if (cnt) {
+    __syncthreads();
+    if (threadIdx.x == 0 && bacc) atomicAdd(&cnt[blockIdx.x % kRxShards], bacc);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Destination-ordered RX (index + gather).
 //
 // k_rx_place writes each packet where its seqid says, in ring order: a block's
