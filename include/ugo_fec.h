@@ -99,7 +99,7 @@ int ugo_fec_encode(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_si
  * ugo_fec_encode(pitch) == strided(row_stride = pitch, group_stride = (d+p)*pitch).
  * The shard-major ("planar") batch layout [d+p][groups][pitch] -- row_stride =
  * groups*pitch, group_stride = pitch -- turns every shard index into one
- * sequential HBM stream and is the fastest layout on MI355X (DESIGN.md §4).
+ * sequential HBM stream and is the fastest layout on MI355X (DESIGN.md §3).
  * No two shard slots may overlap: the smaller stride must be >= shard_size and
  * the larger one must clear a whole run of the smaller ((count - 1) * smaller
  * + shard_size), else UGO_FEC_ERR_INVALID_ARG before any launch (the same rule
@@ -109,7 +109,7 @@ int ugo_fec_encode(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_si
  * row_stride multiples of 16) take the vector kernels too: encode folds
  * 16/gcd(shard_size, 16) groups into one 16-B-whole pseudo-group; reconstruct
  * (d <= 16, p <= 4, shard_size >= 1009) runs on the rows' aligned chunks.
- * Padded 16-B pitches stay the faster reconstruct layout. */
+ * Padded 16-B pitches stay the faster reconstruct layout (DESIGN_HISTORY.md §3.4). */
 int ugo_fec_encode_strided(ugo_fec* ctx, uint8_t* shards, size_t groups, size_t shard_size,
                            size_t row_stride, size_t group_stride, void* stream);
 

@@ -17,7 +17,7 @@ using namespace ugo::kern;
 // k_apply_qa (wave-aligned groups) is production since round 2 (fec_kernels.hip).
 
 // ---------------------------------------------- k_apply_gq (A/B only)
-// Round-2 attempt at fusing k_prepare into the jumbo apply:
+// Round-2 attempt at fusing k_prepare into the jumbo apply (DESIGN_HISTORY.md §3.4):
 // bit-exact, but 634.6 us against 569.3 us for k_prepare + k_apply_q
 // (jvar_r2h.jsonl).  Kept here, out of the product, as the record.
 constexpr uint32_t kMaxDescBytes = 1024;

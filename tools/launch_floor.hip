@@ -1,6 +1,6 @@
 // launch_floor.hip -- the per-call floor of the drop-in path on MI355X: one
 // tiny kernel launch + one synchronize, the shape of every per-group call
-// (DESIGN.md §4 "drop-in per-group path").  Variants: default device flags vs
+// (DESIGN_HISTORY.md §4 "drop-in per-group path").  Variants: default device flags vs
 // hipDeviceScheduleSpin, stream synchronize vs event synchronize, and a
 // kernel that touches a pinned (mapped) host buffer like the zero-copy calls.
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/launch_floor tools/launch_floor.hip

@@ -11,7 +11,7 @@
 //   persist K/B the same tiles on a persistent grid of B blocks per CU, so
 //               the blocks start their phases together and, with equal work,
 //               stay roughly in step chip-wide (no grid barrier)
-// The question is DESIGN.md §8.1's: a 10-read + 3-write mix runs at 6.0 TB/s
+// The question is DESIGN_HISTORY.md §8.1's: a 10-read + 3-write mix runs at 6.0 TB/s
 // where 10 read streams alone run at 6.9 and one write stream at 6.8
 // (profiles/r2/tlbprobe_r2.jsonl).  Not product code.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/phase_probe tools/phase_probe.hip

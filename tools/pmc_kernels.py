@@ -6,7 +6,7 @@ SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE).  For every
 kernel name: dispatches, average duration, VALU instructions per wave, and the
 VALU issue time = VALU/wave x waves x 4 cycles / 1024 SIMDs / 2.4 GHz (a wave64
 VALU instruction occupies a SIMD for 4 cycles), the "both roofs" table of
-DESIGN.md §4.  One JSON line per kernel on stdout.
+DESIGN_HISTORY.md §4.  One JSON line per kernel on stdout.
 """
 import csv
 import glob

@@ -9,7 +9,7 @@
 // planar row stride (G * pitch + row_pad), to see whether the row streams'
 // relative alignment (G * 9008 = 2^17 * 563 at 8,192 groups) matters.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/qaprobe tools/qaprobe.hip
-// Round-3 results: profiles/r3/qaprobe_r3m.jsonl (DESIGN.md §3.4 "Jumbo floor").
+// Round-3 results: profiles/r3/qaprobe_r3m.jsonl (DESIGN_HISTORY.md §3.4 "Jumbo floor").
 // Not product code: it includes the kernel TU to instantiate the variants.
 #include "../ugo_amd/csrc/fec_kernels.hip"
 

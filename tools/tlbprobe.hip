@@ -1,6 +1,6 @@
 // tlbprobe.hip -- streaming read / write / encode-pattern rate vs footprint on MI355X: does a sweep
 // over tens of GB run at the rate of a 1-GB sweep?  (Large FEC batches, see
-// DESIGN.md §4 "batch size".)  Read-only nt stream, one 16-B chunk per thread,
+// DESIGN_HISTORY.md §4 "batch size".)  Read-only nt stream, one 16-B chunk per thread,
 // full grid, each footprint swept repeatedly after 200 ms of warm load.
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/tlbprobe tools/tlbprobe.hip
 #include <hip/hip_runtime.h>

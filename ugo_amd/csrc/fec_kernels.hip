@@ -2,7 +2,7 @@
 // encode / erasure recovery: the arithmetic below reedsolomon.Encoder.Encode
 // (ugo/fec.go:238) and .Reconstruct (ugo/fec.go:202).
 //
-// Work decomposition: a batch is shards[g][row][pitch].  One
+// Work decomposition (DESIGN_HISTORY.md §3): a batch is shards[g][row][pitch].  One
 // work item = one 16-byte column chunk of one group: the lane loads that chunk
 // of each input row (global_load_dwordx4; consecutive lanes take consecutive
 // chunks, so a wave's load of one row is 1 KiB contiguous), computes every
@@ -11,7 +11,7 @@
 // HBM-bound byte-field codecs, no MFMA.  The headline encode (k_encode_g)
 // stages most of its row loads through LDS by LDS-DMA (global_load_lds_dwordx4
 // nt, 1 KiB per row per wave); loads and stores are nontemporal, the policy
-// that wins on a batch that is not in the Infinity Cache.
+// that wins on a batch that is not in the Infinity Cache (DESIGN_HISTORY.md §3.4).
 //
 // GF(2^8) multiply-accumulate on 4 packed bytes per dword uses Horner's rule
 // over the coefficient bits (bit 7 first):
@@ -46,7 +46,7 @@
 //  * Every reconstruct kernel writes output i (the i-th erased row) either in
 //    place or, when Batch::out is set (ugo_fec_reconstruct_into), to slot i of
 //    a separate output batch: then no row stream of the input mixes reads with
-//    writes, 10% faster.
+//    writes, 10% faster (DESIGN_HISTORY.md §3.4).
 //  * k_prepare: per-group decode descriptor on device (first d present rows
 //    -> d x d sub-matrix -> Gauss-Jordan in LDS -> reconstruct coefficients).
 #include <hip/hip_runtime.h>
@@ -93,7 +93,7 @@ __device__ __forceinline__ void load_rows(V4* x, const uint8_t* gp, uint64_t rst
 }
 
 // One 16-byte column chunk per thread over a full grid (items / 256 blocks).
-// Measured on MI355X (tools/kvariants.hip): a full grid at
+// Measured on MI355X (tools/kvariants.hip, DESIGN_HISTORY.md §4): a full grid at
 // 8 waves/SIMD (62 VGPRs) beats persistent grids and software-pipelined
 // (ping-pong) forms, whose second register set halves occupancy.
 template <int D, int P, int NT, int SWZ = 0>
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 }
 
 // ----------------------------------------------- descriptor-driven kernels
-// Descriptor, byte offsets:
+// Descriptor (DESIGN_HISTORY.md §3.3), byte offsets:
 //   [0] e_total  [1] e_data  [2] status  [3] reserved
 //   [4, 4+dpad)            input rows (survivors / data rows)
 //   [4+dpad, 4+dpad+epad)  output rows: erased data rows, then erased parity
@@ -209,7 +209,7 @@ __device__ __forceinline__ const uint8_t* desc_for(const Batch& a, uint64_t g) {
 // One 16-byte chunk per thread over a full grid; the descriptor (presence
 // mask -> table entry, or the group's workspace entry) is read per thread from
 // L2.  Staging descriptors per tile in LDS and software-pipelining the next
-// item measured slower (fewer waves per SIMD), see DESIGN.md §4.
+// item measured slower (fewer waves per SIMD), see DESIGN_HISTORY.md §4.
 template <int DMAX, int MODE, int NT>
 __global__ __launch_bounds__(256) void k_apply(Batch a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
 // and descriptors are fetched with scalar loads (wave-uniform addresses), and
 // each lane selects its group's words with v_cndmask.  This removes the
 // per-lane mask -> descriptor -> data dependent vector-load chain of k_apply
-// and the per-lane descriptor loads.
+// and the per-lane descriptor loads (DESIGN_HISTORY.md §4).
 //
 // CPT > 1: a thread owns CPT chunks `a.pass` items apart (a.pass % 64 == 0, so
 // every range is still wave-aligned); all CPT sets of survivor loads are
@@ -476,7 +476,7 @@ template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1, int EMAX = 4, b
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_p(Batch a) {
   // GLR > 0 (A/B only): survivors 0..GLR-1 by LDS-DMA nt.  It ties register
   // loads on a cold batch (201.0 vs 201.0 us) and in a warm loop (187.3 vs
-  // 188.0 us): DESIGN.md §3.4.
+  // 188.0 us): DESIGN_HISTORY.md §3.4.
   static_assert(GLR == 0 || (DMAX == 10 && (GLR == 8 || GLR == 10)), "LDS-DMA survivor staging: d = 10");
   __shared__ u32x4 stage[GLR ? 4 : 1][GLR ? GLR : 1][64];
   const uint32_t bid = block_id<SWZ>();
@@ -1802,7 +1802,7 @@ static inline uint32_t blocks_for(uint64_t items, uint32_t bs) {
   return static_cast<uint32_t>((items + bs - 1) / bs);
 }
 
-// Launch policy (tuned with tools/kvariants.hip on MI355X).
+// Launch policy (tuned with tools/kvariants.hip on MI355X, DESIGN_HISTORY.md §3.4).
 // Store policy is chosen for the cold-HBM regime -- a batch whose lines are
 // not in the 256-MB Infinity Cache, as every fresh batch of packets is
 // (`kvariants 65536 21 cold`, each sample after a cache-evicting sweep):

@@ -27,7 +27,7 @@
 // words, take per (group, row) the smallest packet index (atomicMin,
 // k_rx_claim) and re-place exactly the winners over whatever the racing
 // copies left.  Without duplicates that costs three empty launches instead of
-// a claim pass over every header before placement.
+// a claim pass over every header before placement (DESIGN_HISTORY.md §4).
 //
 // The packet sits at a 16-aligned slot, so its payload (offset 6) is
 // misaligned: each thread loads the two aligned chunks covering its 16 output
@@ -386,6 +386,10 @@ __global__ __launch_bounds__(256) void k_rx_sum_parts(const uint32_t* parts, uin
 // This is the access shape of the fastest scatter measured
 // (tools/rxgather.hip P2: one chunk per thread, full grid).
 constexpr uint32_t kRxShards = 32;
+#ifndef UGO_RX_CHUNK  // 1: the chunk path for rows of packets that fit it; 0: the packet-per-half-wave path
+#define UGO_RX_CHUNK 0
+#endif
+constexpr bool kRxChunk = UGO_RX_CHUNK != 0;
 
 template <int NT = 3>
 __global__ __launch_bounds__(256) void k_rx_chunk(RxArgs a, uint32_t nq, uint32_t* cnt) {
@@ -711,7 +715,31 @@ __global__ __launch_bounds__(256) void k_rx_gather(RxArgs a, const uint32_t* par
 // flag), classifies it exactly as the place kernels do, and takes the
 // smallest index per (group, row).  ~8 B read per 1.5-KB packet.
 __global__ __launch_bounds__(256) void k_rx_claim(RxArgs a) {
-  if (rx_gated_off(a)) return;
+  if (a.cnt) {  // chunk path: the gate is "some piece claimed twice" (accepted claims > pieces placed)
+    __shared__ uint32_t sums[5];
+    if (threadIdx.x < 5) {
+      uint32_t v = 0;
+      for (uint32_t k = 0; k < kRxShards; ++k) v += a.cnt[threadIdx.x * kRxShards + k];
+      sums[threadIdx.x] = v;
+    }
+    __syncthreads();
+    const bool twice = sums[0] > sums[4];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (a.dup) *a.dup = twice ? 1u : 0u;  // the re-place pass's gate
+      if (a.stats) {  // accepted = pieces placed; duplicates = valid packets not placed
+        const uint32_t placed = sums[4], bad = sums[1], oow = sums[2], shrt = sums[3];
+        atomicAdd(&a.stats[0], placed);
+        if (bad) atomicAdd(&a.stats[1], bad);
+        if (oow) atomicAdd(&a.stats[2], oow);
+        if (shrt) atomicAdd(&a.stats[3], shrt);
+        const uint32_t dups = static_cast<uint32_t>(a.npk) - placed - bad - oow - shrt;
+        if (dups) atomicAdd(&a.stats[4], dups);
+      }
+    }
+    if (!twice) return;
+  } else if (rx_gated_off(a)) {
+    return;
+  }
   const uint64_t nthreads = gridDim.x * 256ull;
   uint32_t k0 = 0u, k1 = 0u;
   if (a.pad) {
@@ -740,10 +768,11 @@ __global__ __launch_bounds__(256) void k_rx_fill(uint32_t* win, uint64_t words, 
 
 __global__ __launch_bounds__(256) void k_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups,
                                                   uint32_t* dup, uint32_t* win, uint64_t words,
-                                                  unsigned long long* seen, unsigned long long call) {
+                                                  unsigned long long* seen, unsigned long long call, uint32_t* cnt) {
   const uint64_t t = blockIdx.x * 256ull + threadIdx.x;
   const uint64_t nt = gridDim.x * 256ull;
   if (t == 0) *dup = 0u;
+  if (cnt && t < kRxCntWords) cnt[t] = 0u;
   uint64_t any = 0;
   for (uint64_t g = t; g < groups; g += nt) {
     const uint64_t m = present[g];
@@ -756,12 +785,51 @@ __global__ __launch_bounds__(256) void k_rx_begin(const uint64_t* present, uint6
 }
 
 hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, uint32_t* win,
-                           uint64_t words, unsigned long long* seen, unsigned long long call, hipStream_t s) {
+                           uint64_t words, unsigned long long* seen, unsigned long long call, hipStream_t s,
+                           uint32_t* cnt) {
   uint64_t blocks = (groups + 255) / 256;
   if (blocks == 0) blocks = 1;
   if (blocks > 1024u) blocks = 1024u;
   launch(kKRx, k_rx_begin, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, present, prev, groups, dup, win,
-         words, seen, call);
+         words, seen, call, cnt);
+  return hipGetLastError();
+}
+
+// Per group, the presence bits this call set (present & ~prev): their sum is
+// the number of (group, row) pieces the call placed.  Sharded adds, one per block.
+__global__ __launch_bounds__(256) void k_rx_count(const uint64_t* present, const uint64_t* prev, uint64_t groups,
+                                                  uint32_t* cnt) {
+  __shared__ uint32_t tot;
+  if (threadIdx.x == 0) tot = 0;
+  __syncthreads();
+  uint32_t c = 0;
+  for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < groups; g += gridDim.x * 256ull)
+    c += __popcll(present[g] & ~prev[g]);
+  if (c) atomicAdd(&tot, c);
+  __syncthreads();
+  if (threadIdx.x == 0 && tot) atomicAdd(&cnt[4 * kRxShards + blockIdx.x % kRxShards], tot);
+}
+
+hipError_t launch_rx_count(const RxArgs& a, hipStream_t s) {
+  uint64_t blocks = (a.groups + 255) / 256;
+  if (blocks == 0) blocks = 1;
+  if (blocks > 512u) blocks = 512u;
+  launch(kKRx, k_rx_count, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a.present, a.prev, a.groups, a.cnt);
+  return hipGetLastError();
+}
+
+bool rx_chunk_ok(const RxArgs& a) {
+  const uint64_t nq = (a.S + 15u) / 16u;
+  // a packet's chunks must cover its payload: nq chunks of packet bytes [16m, 16m + 16) for m < nq,
+  // plus the neighbour (realignment) -- within the slot
+  return kRxChunk && nq >= 1 && a.npk * nq < (1ull << 31) && 16u * nq <= a.slot;
+}
+
+hipError_t launch_rx_chunk(const RxArgs& a, hipStream_t s) {
+  const uint32_t nq = (a.S + 15u) / 16u;
+  const uint64_t items = a.npk * nq;
+  if (items == 0) return hipSuccess;
+  launch(kKRx, k_rx_chunk<3>, dim3(static_cast<uint32_t>((items + 255) / 256)), dim3(256), 0, s, a, nq, a.cnt);
   return hipGetLastError();
 }
 

@@ -26,6 +26,8 @@ struct RxArgs {
                            // presence bit set at call entry (or a concurrent later call's did); below
                            // call, none did, and the place pass skips its per-packet `prev` lookups
   unsigned long long call; // this call's id (per context, increasing)
+  uint32_t* cnt;           // chunk path: per-call counters, [5][kRxShards] u32 (accepted claims, bad flag,
+                           // out of window, too short, bits set), zeroed by k_rx_begin; or null
   uint64_t npk;
   uint64_t slot;
   uint64_t first_group;
@@ -44,10 +46,21 @@ struct RxArgs {
 // 0xffffffff (claim words; win may be null), and atomicMax(seen, call) by
 // every block that finds a presence bit set (seen may be null).
 hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, uint32_t* win,
-                           uint64_t words, unsigned long long* seen, unsigned long long call, hipStream_t s);
+                           uint64_t words, unsigned long long* seen, unsigned long long call, hipStream_t s,
+                           uint32_t* cnt = nullptr);
 hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, hipStream_t s);
 hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s);
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s);
+
+// Chunk path (one 16-B output chunk per thread, full grid): taken when
+// rx_chunk_ok(a).  Sequence: launch_rx_begin (with a.cnt) -> launch_rx_chunk
+// -> launch_rx_count -> launch_rx_claim (a.cnt set: gated on "some (group,
+// row) claimed twice", which it also writes to a.dup, and block 0 adds the
+// call's stats) -> launch_rx_scatter with fixup (gated on a.dup).
+constexpr uint32_t kRxCntWords = 5 * 32;
+bool rx_chunk_ok(const RxArgs& a);
+hipError_t launch_rx_chunk(const RxArgs& a, hipStream_t s);
+hipError_t launch_rx_count(const RxArgs& a, hipStream_t s);
 
 }  // namespace kern
 }  // namespace ugo

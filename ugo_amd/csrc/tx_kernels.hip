@@ -17,7 +17,7 @@
 // Group buffers are zero-filled past each data packet's length (the reference
 // loop reuses its 13 buffers without clearing them, so its parity bytes past a
 // short packet depend on earlier groups; a fresh FEC -- or this batch -- sees
-// zeros).  DESIGN.md §6 states this contract.
+// zeros).  DESIGN.md §2 states this contract.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

@@ -1265,32 +1265,51 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   // (rx_kernels.hip): place everything, flag a (group, row) taken twice, and
   // only then -- gated on the flag, on the device -- claim and re-place.
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  // scratch: presence snapshot [groups] u64 | claim words [groups][n] u32 | dup flag
+  // scratch: presence snapshot [groups] u64 | claim words [groups][n] u32 | dup flag | chunk-path counters
   const uint64_t words = groups * uint64_t(c->n);
   void* scratch = nullptr;
-  int st = scratch_alloc(c, groups * sizeof(uint64_t) + words * sizeof(uint32_t) + 16, s, &scratch);
+  int st = scratch_alloc(c, groups * sizeof(uint64_t) + (words + 16 + ugo::kern::kRxCntWords) * sizeof(uint32_t), s,
+                         &scratch);
   if (st) return st;
   uint64_t* prev = static_cast<uint64_t*>(scratch);
   uint32_t* win = reinterpret_cast<uint32_t*>(prev + groups);
   uint32_t* dup = win + words;
+  uint32_t* cnt = dup + 16;
+  const bool chunk = ugo::kern::rx_chunk_ok(a);
   // call entry, one launch: dup = 0, the presence snapshot -- a (group, row)
   // an earlier call placed keeps that call's copy (ugo/fec.go:123-129 keeps the
   // first) -- the claim words, and whether any presence bit was set at all (if
   // none was, the place pass skips its per-packet snapshot lookups)
   const unsigned long long call = ++c->rx_calls;
-  st = hip_status(ugo::kern::launch_rx_begin(present, prev, groups, dup, win, words, c->d_rxseen, call, s));
+  st = hip_status(ugo::kern::launch_rx_begin(present, prev, groups, dup, win, words, c->d_rxseen, call, s,
+                                             chunk ? cnt : nullptr));
   a.dup = dup;
   a.prev = prev;
   a.seen = c->d_rxseen;
   a.call = call;
-  if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
   ugo::kern::RxArgs f = a;  // the gated claim and re-place of the first copies
   f.win = win;
   f.gate = dup;
   f.dup = nullptr;
   f.stats = nullptr;
   f.fixup = 1;
-  if (!st) st = hip_status(ugo::kern::launch_rx_claim(f, s));
+  if (chunk) {
+    // one output chunk per thread; duplicates found afterwards by counting the
+    // bits the call set against the packets it accepted (k_rx_count), which
+    // also gates the claim -- whose block 0 adds the call's stats
+    a.cnt = cnt;
+    if (!st) st = hip_status(ugo::kern::launch_rx_chunk(a, s));
+    if (!st) st = hip_status(ugo::kern::launch_rx_count(a, s));
+    ugo::kern::RxArgs cl = f;
+    cl.cnt = cnt;
+    cl.dup = dup;  // written by the claim: the re-place pass's gate
+    cl.stats = stats;
+    cl.gate = nullptr;
+    if (!st) st = hip_status(ugo::kern::launch_rx_claim(cl, s));
+  } else {
+    if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
+    if (!st) st = hip_status(ugo::kern::launch_rx_claim(f, s));
+  }
   if (!st) st = hip_status(ugo::kern::launch_rx_scatter(f, s));
   const int fr = scratch_free(c, scratch, s);
   return st ? st : fr;
