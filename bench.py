@@ -197,7 +197,11 @@ def dist_setup(backend: str):
         # the loopback device too (the container hostname may not resolve)
         if backend == "gloo" and os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost"):
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-        dist.init_process_group(backend, init_method="env://")
+        import datetime
+
+        # a rank that fails surfaces as an error within minutes instead of
+        # leaving the others in a collective for gloo's default 30
+        dist.init_process_group(backend, init_method="env://", timeout=datetime.timedelta(seconds=600))
     return rank, local_rank, world
 
 
@@ -658,21 +662,36 @@ def host_path_leg(args, dev_index, rank=0, world=1, reps=3):
     all_ok = True
     try:
         for d, p, S, G, mixed in ((10, 3, 1350, 65536, False), (32, 8, 9000, 8192, True)):
+            # every rank makes the same collective calls whatever fails locally
+            # (a failure is recorded and the rank's calls become no-ops), so a
+            # failing rank cannot leave the others waiting in a barrier
             n = d + p
             pitch = (S + 15) // 16 * 16
-            enc = fec.New(d, p, device=dev_index)
-            raw = fec.host_alloc(G * n * pitch)
-            try:
+            st = {"err": None}
+            enc = raw = buf = ref = None
+            masks = ne = None
+            rcs = []
+
+            def guarded(fn):
+                def g():
+                    if st["err"] is None:
+                        try:
+                            fn()
+                        except Exception as ex:  # noqa: BLE001
+                            st["err"] = repr(ex)[:200]
+                return g
+
+            def setup():
+                nonlocal enc, raw, buf
+                enc = fec.New(d, p, device=dev_index)
+                raw = fec.host_alloc(G * n * pitch)
                 buf = raw.reshape(G, n, pitch)
                 gen = torch.Generator(device=dev).manual_seed(args.seed + d + 7919 * rank)
                 torch.from_numpy(buf).copy_(torch.randint(0, 256, (G, n, pitch), dtype=torch.uint8, device=dev,
                                                           generator=gen))
 
-                def timed(call):
-                    call()  # untimed
-                    return timed_reps(call, reps, world)
-
-                t_enc, t_enc_mine = timed(lambda: enc.encode_host(buf, S))
+            def erase():
+                nonlocal ref, masks, ne
                 ref = torch.from_numpy(buf).to(dev)
                 rng = np.random.default_rng(args.seed + 7 * d + 104729 * rank)
                 ranks_ = rng.random((G, n)).argsort(axis=1).argsort(axis=1)  # rank of row r in a random order
@@ -683,20 +702,22 @@ def host_path_leg(args, dev_index, rank=0, world=1, reps=3):
                     masks |= (~erased[:, r]).astype(np.uint64) << np.uint64(r)
                 gi, ri = np.nonzero(erased)
                 buf[gi, ri] = 0
-                rcs = []
 
-                def rec():
-                    rcs.append(enc.reconstruct_host(buf, masks, S))
-
-                t_rec, t_rec_mine = timed(rec)
-                ok = all(rc == 0 for rc in rcs) and bool(
+            try:
+                guarded(setup)()
+                enc_call = guarded(lambda: enc.encode_host(buf, S))
+                enc_call()  # untimed
+                t_enc, t_enc_mine = timed_reps(enc_call, reps, world)
+                guarded(erase)()
+                rec_call = guarded(lambda: rcs.append(enc.reconstruct_host(buf, masks, S)))
+                rec_call()  # untimed
+                t_rec, t_rec_mine = timed_reps(rec_call, reps, world)
+                ok = st["err"] is None and all(rc == 0 for rc in rcs) and bool(
                     torch.equal(torch.from_numpy(buf).to(dev)[:, :, :S], ref[:, :, :S]))
                 all_ok = all_ok and ok
-                del ref
-                e_tot = int(ne.sum())
-                lossy = int((ne > 0).sum())
+                ref = None
                 b_enc = G * n * S
-                b_rec = lossy * d * S + e_tot * S
+                b_rec = 0 if ne is None else int((ne > 0).sum()) * d * S + int(ne.sum()) * S
                 b_rec_all = int(reduce_sum([b_rec], world)[0])  # erasure counts differ by rank
                 key = f"{d}+{p}x{S}"
                 res[key] = {
@@ -709,9 +730,13 @@ def host_path_leg(args, dev_index, rank=0, world=1, reps=3):
                     "rank0_alone_encode_ms": round(t_enc_mine * 1e3, 3),
                     "rank0_alone_reconstruct_ms": round(t_rec_mine * 1e3, 3),
                     "verify_round_trip": ok}
+                if st["err"]:
+                    res[key]["error_rank0"] = st["err"]
             finally:
-                fec.host_free(raw)
-                enc.close()
+                if raw is not None:
+                    fec.host_free(raw)
+                if enc is not None:
+                    enc.close()
     finally:
         try:
             os.sched_setaffinity(0, saved)
