@@ -24,7 +24,12 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 KERNELS = {"k_encode_c": "encode", "k_encode_g": "encode", "k_encode_frs": "encode", "k_apply_p<": "reconstruct", "k_apply_pd<": "reconstruct", "k_apply_w<": "reconstruct", "k_apply<": "reconstruct", "k_apply_bytes": "reconstruct_bytes",
-           "k_prepare": "prepare"}
+           "k_prepare": "prepare",
+           # the rx_tx leg and the ceilings (round 4)
+           "k_rx_place": "rx_place", "k_rx_chunk": "rx_chunk", "k_rx_begin": "rx_begin", "k_rx_count": "rx_count",
+           "k_rx_claim": "rx_claim", "k_tx_g": "tx", "k_tx_c": "tx", "k_packet_decode": "packet_decode",
+           "k_encode_twin": "encode_twin", "k_nt_copy": "nt_copy"}
+BENCH_KINDS = ("encode", "reconstruct")  # the kinds whose last `steps` dispatches are the bench's timed steps
 
 
 def kind(name):
@@ -86,7 +91,7 @@ def main():
             if k:
                 durs[k].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
         for k, v in durs.items():
-            if steps and len(v) >= steps:
+            if k in BENCH_KINDS and steps and len(v) >= steps:
                 timed[k]["timed_steps"] = steps
                 timed[k]["timed_avg_ns"] = sum(v[-steps:]) / steps
     summary = {"tag": tag, "bench_config": cfg, "kernels": {}, "dispatch_durations": timed}

@@ -396,14 +396,14 @@ __global__ __launch_bounds__(256) void k_rx_chunk(RxArgs a, uint32_t nq, uint32_
   __shared__ uint32_t bacc;
   if (threadIdx.x == 0) bacc = 0;
   __syncthreads();
-  const uint64_t t = blockIdx.x * 256ull + threadIdx.x;
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;  // < 2^31 (rx_chunk_ok)
   const uint32_t lane = threadIdx.x & 63u;
   const bool live = t < a.npk * nq;
-  const uint64_t i = live ? t / nq : 0;
-  const uint32_t m = static_cast<uint32_t>(t - i * nq);
+  const uint32_t i = live ? t / nq : 0u;
+  const uint32_t m = t - i * nq;
   const uint32_t o = 16u * m;
   const uint32_t slot = static_cast<uint32_t>(a.slot);
-  const uint8_t* pk = a.wire + i * a.slot;
+  const uint8_t* pk = a.wire + uint64_t(i) * a.slot;
   const u32x4 zero = {0u, 0u, 0u, 0u};
   // all loads first: header chunk, length, payload chunk, keystream
   u32x4 h = live ? ld16(pk) : zero;
