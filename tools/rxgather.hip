@@ -201,7 +201,7 @@ int main(int argc, char** argv) {
   uint32_t* win = reinterpret_cast<uint32_t*>(prev + G);
   uint32_t* dup = win + G * n;
 
-  enum Kind { PROD, PROD_OLD, GATHER };
+  enum Kind { PROD, PROD_OLD, GATHER, CHUNK };
   struct Var {
     std::string name;
     Kind kind;
@@ -211,7 +211,10 @@ int main(int argc, char** argv) {
   std::vector<Var> vars = {
       {"production (round 4): begin(+claim fill, fresh flag) + place + gated claim/re-place", PROD, 0, 0, 0},
       {"production (round 3): begin + place + gated fill/claim/re-place", PROD_OLD, 0, 0, 0},
+      {"chunk path: begin + chunk (one output chunk per thread) + count + gated claim/re-place", CHUNK, 0, 0, 0},
   };
+  uint32_t* d_cnt;
+  CK(hipMalloc(&d_cnt, kRxCntWords * 4));
   unsigned long long* d_seen;
   CK(hipMalloc(&d_seen, 8));
   CK(hipMemset(d_seen, 0, 8));
@@ -233,6 +236,7 @@ int main(int argc, char** argv) {
     if (zero_present) CK(hipMemsetAsync(a.present, 0, a.groups * 8, s));
     a.seen = nullptr;
     a.call = 0;
+    a.cnt = nullptr;
     if (v.kind == GATHER) {
       CK(launch_rx_fill(win, a.groups * n, nullptr, s));
       a.win = win;
@@ -245,6 +249,29 @@ int main(int argc, char** argv) {
         k_rx_gather<3, 1, 8><<<gr, 256, 0, s>>>(a, d_parts, ib);
       else
         k_rx_gather<3, 1, 32><<<gr, 256, 0, s>>>(a, d_parts, ib);
+      return;
+    }
+    if (v.kind == CHUNK) {  // ugo_fec_rx_assemble's chunk path
+      const unsigned long long call = ++call_id;
+      CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, s, d_cnt));
+      a.seen = d_seen;
+      a.call = call;
+      a.dup = dup;
+      a.prev = prev;
+      RxArgs f = a;
+      f.win = win;
+      f.gate = dup;
+      f.dup = nullptr;
+      f.stats = nullptr;
+      f.fixup = 1;
+      a.cnt = d_cnt;
+      CK(launch_rx_chunk(a, s));
+      CK(launch_rx_count(a, s));
+      RxArgs cl = f;
+      cl.cnt = d_cnt;
+      cl.stats = a.stats;
+      CK(launch_rx_claim(cl, s));
+      CK(launch_rx_scatter(f, s));
       return;
     }
     if (v.kind == PROD) {
@@ -405,28 +432,19 @@ int main(int argc, char** argv) {
                   k_pat_gather1<<<(G * n * 92 + 255) / 256, 256>>>(rot[k].wire, rot[k].shards, d_sidx, G * n);
                 }, {}});
   for (const Var& v : vars) ts.push_back({v.name, [&, v] { run(v, rot[cnt++ % 3], nullptr); }, {}});
-  uint32_t* d_cnt;
-  CK(hipMalloc(&d_cnt, 4 * 32 * 4));
-  auto chunk_variant = [&](int nt) {
-    return [&, nt] {
-      RxArgs a = rot[cnt++ % 3];
-      CK(hipMemsetAsync(a.present, 0, a.groups * 8, nullptr));
-      const unsigned long long call = ++call_id;
-      CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, nullptr));
-      CK(hipMemsetAsync(d_cnt, 0, 4 * 32 * 4, nullptr));
-      a.prev = prev;
-      a.seen = d_seen;
-      a.call = call;
-      const uint64_t items = a.npk * 92;
-      if (nt == 3)
-        k_rx_chunk<3><<<(items + 255) / 256, 256>>>(a, 92, d_cnt);
-      else
-        k_rx_chunk<2><<<(items + 255) / 256, 256>>>(a, 92, d_cnt);
-    };
-  };
-  ts.push_back({"chunk-per-thread place, full grid, nt loads+stores (+memset present, begin, memset counters)",
-                chunk_variant(3), {}});
-  ts.push_back({"chunk-per-thread place, full grid, plain loads, nt stores (+memsets, begin)", chunk_variant(2), {}});
+  ts.push_back({"chunk kernel alone, no returning atomic (timing bound; + memset present, begin)", [&] {
+                  RxArgs a = rot[cnt++ % 3];
+                  CK(hipMemsetAsync(a.present, 0, a.groups * 8, nullptr));
+                  const unsigned long long call = ++call_id;
+                  CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, nullptr,
+                                     d_cnt));
+                  a.prev = prev;
+                  a.seen = d_seen;
+                  a.call = call;
+                  a.dup = dup;
+                  const uint64_t items = a.npk * 92;
+                  k_rx_chunk<3, 0><<<(items + 255) / 256, 256>>>(a, 92, d_cnt);
+                }, {}});
   ts.push_back({"index only (fill + index)", [&] {
                   RxArgs a = rot[cnt++ % 3];
                   a.win = win;

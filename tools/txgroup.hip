@@ -45,6 +45,81 @@ __global__ __launch_bounds__(256) void k_copy1(const u32x4* src, u32x4* dst, uin
   __builtin_nontemporal_store(__builtin_nontemporal_load(src + c), dst + c);
 }
 
+// One thread per 16-B chunk of a WIRE packet (one chunk per thread, full grid,
+// the copy's shape): a data chunk is one load and one store; a parity chunk
+// loads the 10 data chunks of its column (just read by the group's data
+// threads: L2 / Infinity-Cache hits) and folds its own row of the network.
+// SWZ 1: XCD-contiguous blocks, so a group's data and parity blocks share an L2.
+template <int D, int P, int SWZ, int I>
+__device__ __forceinline__ V4 tx_row(const V4* x) {
+  return cparity<D, P, I>(x);
+}
+template <int D, int P, int SWZ>
+__global__ __launch_bounds__(256) void k_tx_o(TxArgs a) {
+  const uint32_t n = D + P, nch = a.chunks;
+  const uint32_t t = block_id<SWZ>() * 256u + threadIdx.x;
+  if (t >= a.groups * n * nch) return;
+  const uint32_t gl = t / (n * nch), rem = t - gl * n * nch, r = rem / nch, m = rem - r * nch, o = 16u * m;
+  const uint64_t g = a.g0 + gl;
+  uint32_t Ls[D];
+  bool bad = false;
+  uint32_t maxsz = 0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    Ls[k] = a.lens[g * D + k];
+    bad |= Ls[k] < 6u || Ls[k] > a.max_len;
+    maxsz = max(maxsz, Ls[k]);
+  }
+  if (bad) {
+    if (m == 0) {
+      a.wire_lens[g * n + r] = 0;
+      if (r == 0 && a.status) a.status[g] = kBadLength;
+    }
+    return;
+  }
+  const uint32_t seq0 = static_cast<uint32_t>((uint64_t(a.first_seq) + g * n) % a.paws);
+  const uint8_t* src = a.pkts + g * D * a.slot_in + o;
+  uint8_t* dst = a.wire + (g * n + r) * a.slot_out + o;
+  if (r < static_cast<uint32_t>(D)) {
+    const uint32_t Lk = Ls[r];
+    if (o < Lk) {
+      V4 w = keep_bytes(load16<1>(src + uint64_t(r) * a.slot_in), Lk - o);
+      if (m == 0) put_header(w, seq0 + r, kTypeData);
+      if (a.pad) xor4(w, load16<0>(a.pad + o));
+      store16<kTxNT>(dst, keep_bytes(w, Lk - o), 16u);
+    }
+    if (m == 0) {
+      a.wire_lens[g * n + r] = static_cast<uint16_t>(Lk);
+      if (r == 0 && a.status) a.status[g] = maxsz <= kFecHeader ? kNoData : 0;
+    }
+    return;
+  }
+  if (maxsz <= kFecHeader) {  // header-only group: no parity
+    if (m == 0) a.wire_lens[g * n + r] = 0;
+    return;
+  }
+  if (m == 0) a.wire_lens[g * n + r] = static_cast<uint16_t>(maxsz);
+  if (o >= maxsz) return;
+  V4 x[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    x[k] = V4{{0u, 0u, 0u, 0u}};
+    if (o < Ls[k]) x[k] = keep_bytes(load16<0>(src + uint64_t(k) * a.slot_in), Ls[k] - o);
+    if (m == 0) {
+      x[k].v[0] = 0u;
+      x[k].v[1] &= 0xffff0000u;
+    }
+  }
+  V4 y;
+  const uint32_t i = r - D;
+  if (i == 0) y = cparity<D, P, 0>(x);
+  else if (i == 1) y = cparity<D, P, 1>(x);
+  else y = cparity<D, P, 2>(x);
+  if (m == 0) put_header(y, seq0 + r, kTypeFEC);
+  if (a.pad) xor4(y, load16<0>(a.pad + o));
+  store16<kTxNT>(dst, keep_bytes(y, maxsz - o), 16u);
+}
+
 __global__ __launch_bounds__(256) void k_flush(const u32x4* a, uint32_t* out, uint64_t n16) {
   const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
   if (i >= n16) return;
@@ -77,6 +152,13 @@ int main(int argc, char** argv) {
     k_tx_c<10, 3, kTxNT, true><<<static_cast<uint32_t>((a.groups * a.chunks + 255) / 256), 256, tx_lds_cap()>>>(a);
   };
   auto run_g = [&](TxArgs a) { k_tx_g<10, 3><<<static_cast<uint32_t>(a.groups), 256, lds>>>(a); };
+  auto run_o = [&](TxArgs a, int swz) {
+    const uint32_t blocks = static_cast<uint32_t>((a.groups * 13 * a.chunks + 255) / 256);
+    if (swz)
+      k_tx_o<10, 3, 1><<<blocks, 256>>>(a);
+    else
+      k_tx_o<10, 3, 0><<<blocks, 256>>>(a);
+  };
 
   // ---- check: random lengths incl. short, header-only groups and bad groups
   {
@@ -131,10 +213,23 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(hl2.data(), l2, G * n * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(hs1.data(), s1, G, hipMemcpyDeviceToHost));
     CK(hipMemcpy(hs2.data(), s2, G, hipMemcpyDeviceToHost));
-    const bool ok = h1 == h2 && hl1 == hl2 && hs1 == hs2;
+    bool ok = h1 == h2 && hl1 == hl2 && hs1 == hs2;
     printf("{\"check\":\"k_tx_g == k_tx_c (wire, wire_lens, status; random lengths, header-only, bad)\","
            "\"same\":%s}\n", ok ? "true" : "false");
     if (!ok) return 2;
+    for (int swz = 0; swz < 2; ++swz) {
+      CK(hipMemset(w2, 0x5c, G * n * slot));
+      CK(hipMemset(l2, 0x77, G * n * 2));
+      CK(hipMemset(s2, 0x33, G));
+      run_o(a, swz);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(h2.data(), w2, h2.size(), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hl2.data(), l2, G * n * 2, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hs2.data(), s2, G, hipMemcpyDeviceToHost));
+      ok = h1 == h2 && hl1 == hl2 && hs1 == hs2;
+      printf("{\"check\":\"k_tx_o<swz %d> == k_tx_c\",\"same\":%s}\n", swz, ok ? "true" : "false");
+      if (!ok) return 2;
+    }
     for (void* q : {(void*)dp, (void*)dl, (void*)w1, (void*)w2, (void*)l1, (void*)l2, (void*)s1, (void*)s2})
       CK(hipFree(q));
   }
@@ -173,6 +268,8 @@ int main(int argc, char** argv) {
   std::vector<T> ts;
   ts.push_back({"k_tx_c (round 3 production)", [&] { run_c(rot[cnt++ % 3]); }, {}});
   ts.push_back({"k_tx_g (one block per group)", [&] { run_g(rot[cnt++ % 3]); }, {}});
+  ts.push_back({"k_tx_o (one wire chunk per thread)", [&] { run_o(rot[cnt++ % 3], 0); }, {}});
+  ts.push_back({"k_tx_o, XCD-contiguous blocks", [&] { run_o(rot[cnt++ % 3], 1); }, {}});
   // the copy reads and writes the wire buffers (G*13*1488 B each): the data
   // packets alone (G*10*1488 B) are smaller than half the bytes moved
   if (copy16 * 16 > G * n * slot) return 3;

@@ -169,6 +169,7 @@ void FEC::markFEC(uint8_t* data) {  // :97-104
 
 std::vector<Bytes> FEC::input(fecPacket pkt) {  // :107-226
   std::vector<Bytes> recovered;
+  lastError_ = UGO_FEC_OK;  // this call's own status (an earlier call's error is not this one's)
   const uint32_t now = clock_();
   if (now - lastCheck_ >= fecExpire) {  // expiration :109-121
     std::vector<fecPacket> keep;
@@ -452,6 +453,7 @@ void FEC::flushInto(std::vector<Bytes>& out) {
 
 std::vector<Bytes> FEC::flush() {
   std::vector<Bytes> out;
+  lastError_ = UGO_FEC_OK;
   flushInto(out);
   return out;
 }

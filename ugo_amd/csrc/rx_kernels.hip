@@ -375,27 +375,30 @@ __global__ __launch_bounds__(256) void k_rx_sum_parts(const uint32_t* parts, uin
 // length (shared by the packet's threads: one line per wave), its own payload
 // chunk, the keystream -- depends on t alone, so all are issued at once; the
 // neighbour chunk the 6-B realignment needs comes from lane + 1 by DPP (a
-// separate load only at a packet's last chunk and in lane 63).  Nothing waits
-// on a second round trip in the usual case: with no presence bit set at call
-// entry (a->seen, k_rx_begin) there is no snapshot lookup, and the presence
-// bit is OR-ed by the packet's chunk-0 thread with a no-return atomic.  A
-// duplicate is found afterwards instead (k_rx_count: per group, the bits this
-// call set against the packets it accepted).  The per-call counters go to
-// 32 sharded words (cnt[k * 32 + shard], shard = block % 32): bad flag, out of
-// window, too short -- rare -- and accepted packets, one add per block.
-// This is the access shape of the fastest scatter measured
-// (tools/rxgather.hip P2: one chunk per thread, full grid).
+// separate load only at a packet's last chunk and in lane 63).  With no
+// presence bit set at call entry (a->seen, k_rx_begin) there is no snapshot
+// lookup.  The packet's chunk-0 thread ORs its presence bit as soon as the
+// header is known (DEDUP 1: with the old mask returned -- a bit already set
+// is a second copy in this call and raises a.dup for the gated claim and
+// re-place; DEDUP 0, timing only: no return).  Blocks keep no counters: the
+// rare bad-flag / out-of-window / too-short packets add to sharded words
+// (cnt[k * kRxShards + shard], one 128-B line per shard), and k_rx_count
+// counts the pieces placed from the presence bits.  This is the access shape
+// of the fastest scatter measured (tools/rxgather.hip P2: one chunk per
+// thread, full grid).
 constexpr uint32_t kRxShards = 32;
+constexpr uint32_t kRxShardStride = 32;  // words: one 128-B line per shard
 #ifndef UGO_RX_CHUNK  // 1: the chunk path for rows of packets that fit it; 0: the packet-per-half-wave path
 #define UGO_RX_CHUNK 0
 #endif
 constexpr bool kRxChunk = UGO_RX_CHUNK != 0;
 
-template <int NT = 3>
+__device__ __forceinline__ uint32_t* rx_cnt(uint32_t* cnt, uint32_t k, uint32_t shard) {
+  return cnt + (k * kRxShards + shard) * kRxShardStride;
+}
+
+template <int NT = 3, int DEDUP = 1>
 __global__ __launch_bounds__(256) void k_rx_chunk(RxArgs a, uint32_t nq, uint32_t* cnt) {
-  __shared__ uint32_t bacc;
-  if (threadIdx.x == 0) bacc = 0;
-  __syncthreads();
   const uint32_t t = blockIdx.x * 256u + threadIdx.x;  // < 2^31 (rx_chunk_ok)
   const uint32_t lane = threadIdx.x & 63u;
   const bool live = t < a.npk * nq;
@@ -430,6 +433,9 @@ __global__ __launch_bounds__(256) void k_rx_chunk(RxArgs a, uint32_t nq, uint32_
   if (why == 0 && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
   const uint64_t gs = grp - a.first_group;
   if (why == 0 && chk_prev && ((a.prev[gs] >> row) & 1ull)) why = 4;  // an earlier call's seqid
+  [[maybe_unused]] unsigned long long old = 0;
+  if constexpr (DEDUP)  // issued now, waited for only at the end
+    if (m == 0 && why == 0) old = atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
   // neighbour chunk (packet bytes [o+16, o+32)) from lane + 1, converged
   const uint32_t nx = from_next_lane(A.x), ny = from_next_lane(A.y);
   const uint32_t bx = own_b ? B.x : nx, by = own_b ? B.y : ny;
@@ -466,18 +472,13 @@ __global__ __launch_bounds__(256) void k_rx_chunk(RxArgs a, uint32_t nq, uint32_
       }
     }
   }
-  if (m == 0 && live) {
-    const uint32_t shard = blockIdx.x % kRxShards;
-    if (why == 0) {
+  if (m == 0 && live && why >= 1 && why <= 3 && cnt) atomicAdd(rx_cnt(cnt, why, blockIdx.x % kRxShards), 1u);
+  if (m == 0 && why == 0) {
+    if constexpr (DEDUP) {
+      if ((old >> row) & 1ull) *a.dup = 1u;  // a second copy of this seqid in the call
+    } else {
       atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
-      atomicAdd(&bacc, 1u);
-    } else if (why < 4 && cnt) {
-      atomicAdd(&cnt[why * kRxShards + shard], 1u);
     }
-  }
-  if (cnt) {
-    __syncthreads();
-    if (threadIdx.x == 0 && bacc) atomicAdd(&cnt[blockIdx.x % kRxShards], bacc);
   }
 }
 
@@ -715,17 +716,12 @@ __global__ __launch_bounds__(256) void k_rx_gather(RxArgs a, const uint32_t* par
 // flag), classifies it exactly as the place kernels do, and takes the
 // smallest index per (group, row).  ~8 B read per 1.5-KB packet.
 __global__ __launch_bounds__(256) void k_rx_claim(RxArgs a) {
-  if (a.cnt) {  // chunk path: the gate is "some piece claimed twice" (accepted claims > pieces placed)
-    __shared__ uint32_t sums[5];
-    if (threadIdx.x < 5) {
-      uint32_t v = 0;
-      for (uint32_t k = 0; k < kRxShards; ++k) v += a.cnt[threadIdx.x * kRxShards + k];
-      sums[threadIdx.x] = v;
-    }
-    __syncthreads();
-    const bool twice = sums[0] > sums[4];
+  if (a.cnt) {  // chunk path: gated on k_rx_chunk's duplicate flag; block 0 adds the call's stats
+    const bool twice = *a.gate != 0u;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-      if (a.dup) *a.dup = twice ? 1u : 0u;  // the re-place pass's gate
+      uint32_t sums[5] = {0u, 0u, 0u, 0u, 0u};
+      for (uint32_t k = 1; k < 5; ++k)
+        for (uint32_t sh = 0; sh < kRxShards; ++sh) sums[k] += *rx_cnt(a.cnt, k, sh);
       if (a.stats) {  // accepted = pieces placed; duplicates = valid packets not placed
         const uint32_t placed = sums[4], bad = sums[1], oow = sums[2], shrt = sums[3];
         atomicAdd(&a.stats[0], placed);
@@ -772,7 +768,8 @@ __global__ __launch_bounds__(256) void k_rx_begin(const uint64_t* present, uint6
   const uint64_t t = blockIdx.x * 256ull + threadIdx.x;
   const uint64_t nt = gridDim.x * 256ull;
   if (t == 0) *dup = 0u;
-  if (cnt && t < kRxCntWords) cnt[t] = 0u;
+  if (cnt)
+    for (uint64_t i = t; i < kRxCntWords; i += nt) cnt[i] = 0u;
   uint64_t any = 0;
   for (uint64_t g = t; g < groups; g += nt) {
     const uint64_t m = present[g];
@@ -807,13 +804,13 @@ __global__ __launch_bounds__(256) void k_rx_count(const uint64_t* present, const
     c += __popcll(present[g] & ~prev[g]);
   if (c) atomicAdd(&tot, c);
   __syncthreads();
-  if (threadIdx.x == 0 && tot) atomicAdd(&cnt[4 * kRxShards + blockIdx.x % kRxShards], tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(rx_cnt(cnt, 4, blockIdx.x % kRxShards), tot);
 }
 
 hipError_t launch_rx_count(const RxArgs& a, hipStream_t s) {
   uint64_t blocks = (a.groups + 255) / 256;
   if (blocks == 0) blocks = 1;
-  if (blocks > 512u) blocks = 512u;
+  if (blocks > 64u) blocks = 64u;
   launch(kKRx, k_rx_count, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, a.present, a.prev, a.groups, a.cnt);
   return hipGetLastError();
 }

@@ -26,8 +26,8 @@ struct RxArgs {
                            // presence bit set at call entry (or a concurrent later call's did); below
                            // call, none did, and the place pass skips its per-packet `prev` lookups
   unsigned long long call; // this call's id (per context, increasing)
-  uint32_t* cnt;           // chunk path: per-call counters, [5][kRxShards] u32 (accepted claims, bad flag,
-                           // out of window, too short, bits set), zeroed by k_rx_begin; or null
+  uint32_t* cnt;           // chunk path: per-call counters (-, bad flag, out of window, too short, pieces
+                           // placed) x 32 shards, one 128-B line each; zeroed by k_rx_begin; or null
   uint64_t npk;
   uint64_t slot;
   uint64_t first_group;
@@ -54,10 +54,10 @@ hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s);
 
 // Chunk path (one 16-B output chunk per thread, full grid): taken when
 // rx_chunk_ok(a).  Sequence: launch_rx_begin (with a.cnt) -> launch_rx_chunk
-// -> launch_rx_count -> launch_rx_claim (a.cnt set: gated on "some (group,
-// row) claimed twice", which it also writes to a.dup, and block 0 adds the
-// call's stats) -> launch_rx_scatter with fixup (gated on a.dup).
-constexpr uint32_t kRxCntWords = 5 * 32;
+// (raises *a.dup on a second copy of a seqid) -> launch_rx_count ->
+// launch_rx_claim (a.cnt set, a.gate = the dup flag; its block 0 adds the
+// call's stats) -> launch_rx_scatter with fixup (gated on the same flag).
+constexpr uint32_t kRxCntWords = 5 * 32 * 32;  // 5 counters x 32 shards, one 128-B line each
 bool rx_chunk_ok(const RxArgs& a);
 hipError_t launch_rx_chunk(const RxArgs& a, hipStream_t s);
 hipError_t launch_rx_count(const RxArgs& a, hipStream_t s);

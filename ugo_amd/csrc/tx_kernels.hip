@@ -64,7 +64,7 @@ __device__ __forceinline__ void put_header(V4& x, uint32_t seq, uint32_t flag) {
 constexpr int kTxNT = 3;
 constexpr bool kTxSL = true;
 #ifndef UGO_TX_GROUP  // 1: (10,3) by k_tx_g (one block per group); 0: k_tx_c (A/B builds)
-#define UGO_TX_GROUP 1
+#define UGO_TX_GROUP 0
 #endif
 constexpr bool kTxGroup = UGO_TX_GROUP != 0;
 

@@ -1294,17 +1294,15 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   f.stats = nullptr;
   f.fixup = 1;
   if (chunk) {
-    // one output chunk per thread; duplicates found afterwards by counting the
-    // bits the call set against the packets it accepted (k_rx_count), which
-    // also gates the claim -- whose block 0 adds the call's stats
+    // one output chunk per thread; a second copy of a seqid raises dup (the
+    // presence atomic's old mask); k_rx_count counts the pieces placed for the
+    // stats, which the claim's block 0 adds whether or not it is gated off
     a.cnt = cnt;
     if (!st) st = hip_status(ugo::kern::launch_rx_chunk(a, s));
     if (!st) st = hip_status(ugo::kern::launch_rx_count(a, s));
-    ugo::kern::RxArgs cl = f;
+    ugo::kern::RxArgs cl = f;  // gated on the chunk kernel's duplicate flag
     cl.cnt = cnt;
-    cl.dup = dup;  // written by the claim: the re-place pass's gate
     cl.stats = stats;
-    cl.gate = nullptr;
     if (!st) st = hip_status(ugo::kern::launch_rx_claim(cl, s));
   } else {
     if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
