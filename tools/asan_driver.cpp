@@ -286,6 +286,93 @@ void tx_rx_batch() {
   ugo_fec_destroy(ctx);
 }
 
+// the per-call service's failure paths (round 4): a forced stall past the
+// watchdog timeout (the block leaves within the grace period: ERR_HIP, later
+// calls on the launch path), a restart, and a block that never leaves within
+// the grace period (poisoned context: every call fails, destroy leaks what the
+// block reads -- the stage stays allocated here until the block is done)
+void service_watchdog() {
+  const int d = 10, p = 3, n = d + p;
+  const size_t S = 1470, pitch = 1472;
+  uint8_t* g = nullptr;
+  EXPECT(ugo_fec_host_alloc(n * pitch, reinterpret_cast<void**>(&g)) == UGO_FEC_OK);
+  if (!g) return;
+  for (size_t i = 0; i < n * pitch; ++i) g[i] = rb();
+  std::vector<uint8_t> want(g, g + n * pitch);
+  ugo_fec* ref = nullptr;
+  EXPECT(ugo_fec_create(0, d, p, &ref) == UGO_FEC_OK);
+  EXPECT(ugo_fec_encode_host(ref, want.data(), 1, S, pitch) == UGO_FEC_OK);  // pageable: staged path
+  ugo_fec_destroy(ref);
+  ugo_fec* ctx = nullptr;
+  EXPECT(ugo_fec_create(0, d, p, &ctx) == UGO_FEC_OK);
+  EXPECT(ugo_fec_service_config(ctx, 50, 5000, 300000) == UGO_FEC_OK);
+  EXPECT(ugo_fec_service_start(ctx, 1000000) == UGO_FEC_OK);
+  EXPECT(ugo_fec_encode_host(ctx, g, 1, S, pitch) == UGO_FEC_ERR_HIP);  // timed out, block gone
+  EXPECT(ugo_fec_poisoned(ctx) == 0);
+  EXPECT(std::memcmp(g, want.data(), n * pitch) == 0);
+  EXPECT(ugo_fec_encode_host(ctx, g, 1, S, pitch) == UGO_FEC_OK);  // launch path
+  EXPECT(ugo_fec_service_config(ctx, 0, 0, 0) == UGO_FEC_OK);
+  EXPECT(ugo_fec_service_start(ctx, 1000000) == UGO_FEC_OK);
+  for (int i = 0; i < 20; ++i) {  // served; stop / start while the block is resident
+    EXPECT(ugo_fec_encode_host(ctx, g, 1, S, pitch) == UGO_FEC_OK);
+    if (i % 5 == 4) {
+      EXPECT(ugo_fec_service_stop(ctx) == UGO_FEC_OK);
+      EXPECT(ugo_fec_service_start(ctx, 1000000) == UGO_FEC_OK);
+    }
+  }
+  EXPECT(std::memcmp(g, want.data(), n * pitch) == 0);
+  ugo_fec_destroy(ctx);
+  // poisoned: stall 1.2 s, timeout 50 ms, grace 100 ms
+  ctx = nullptr;
+  EXPECT(ugo_fec_create(0, d, p, &ctx) == UGO_FEC_OK);
+  EXPECT(ugo_fec_service_config(ctx, 50, 100, 1200000) == UGO_FEC_OK);
+  EXPECT(ugo_fec_service_start(ctx, 1000000) == UGO_FEC_OK);
+  EXPECT(ugo_fec_encode_host(ctx, g, 1, S, pitch) == UGO_FEC_ERR_HIP);
+  EXPECT(ugo_fec_poisoned(ctx) == 1);
+  EXPECT(ugo_fec_encode_host(ctx, g, 1, S, pitch) == UGO_FEC_ERR_HIP);
+  EXPECT(ugo_fec_service_start(ctx, 0) == UGO_FEC_ERR_HIP);
+  ugo_fec_destroy(ctx);  // leaks the mailbox and tables the block still reads
+  EXPECT(hipDeviceSynchronize() == hipSuccess);  // the stalled block serves, sees the stop line, leaves
+  EXPECT(std::memcmp(g, want.data(), n * pitch) == 0);
+  ugo_fec_host_free(g);
+}
+
+// set_batch whose pinned batch cannot be allocated (UGO_FEC_HOST_ALLOC_LIMIT):
+// ERR_HIP, per-call mode, and input keeps working
+void fec_object_alloc_failure() {
+  ugo_fecconn* f = nullptr;
+  EXPECT(ugo_fecconn_new(64, 10, 3, 0, &f) == UGO_FEC_OK);
+  if (!f) return;
+  std::vector<uint8_t> out(64 * 10 * 1476);
+  int nrec = 0;
+  size_t rl = 0;
+  EXPECT(ugo_fecconn_set_batch(f, 4, out.data(), out.size(), &nrec, &rl) == UGO_FEC_OK);
+  setenv("UGO_FEC_HOST_ALLOC_LIMIT", "4096", 1);
+  EXPECT(ugo_fecconn_set_batch(f, 8, out.data(), out.size(), &nrec, &rl) == UGO_FEC_ERR_HIP);
+  unsetenv("UGO_FEC_HOST_ALLOC_LIMIT");
+  // one lossy group (data shard 2 lost) through input, per call now
+  std::vector<std::vector<uint8_t>> grp(13, std::vector<uint8_t>(1476));
+  std::vector<uint8_t*> ptr(13);
+  std::vector<size_t> lens(13, 1476);
+  for (int k = 0; k < 13; ++k) {
+    for (auto& b : grp[k]) b = rb();
+    ptr[k] = grp[k].data();
+  }
+  for (int k = 0; k < 10; ++k) EXPECT(ugo_fecconn_mark_data(f, grp[k].data()) == UGO_FEC_OK);
+  EXPECT(ugo_fecconn_calc_ecc(f, ptr.data(), lens.data(), 13, 6, 1476) == UGO_FEC_OK);
+  for (int k = 10; k < 13; ++k) EXPECT(ugo_fecconn_mark_fec(f, grp[k].data()) == UGO_FEC_OK);
+  int got = 0;
+  for (int k = 0; k < 13; ++k) {
+    if (k == 2) continue;
+    uint32_t sq = 0;
+    uint16_t fl = 0;
+    EXPECT(ugo_fecconn_input(f, grp[k].data(), 1476, &sq, &fl, out.data(), out.size(), &nrec, &rl) == UGO_FEC_OK);
+    got += nrec;
+  }
+  EXPECT(got == 1 && std::memcmp(out.data(), grp[2].data() + 6, 1470) == 0);
+  ugo_fecconn_free(f);
+}
+
 }  // namespace
 
 int main() {
@@ -309,6 +396,8 @@ int main() {
   fec_object(16, UGO_FECCONN_BATCH_OVERLAP);
   fec_object(4, 0, true);
   tx_rx_batch();
+  fec_object_alloc_failure();
+  service_watchdog();
   std::printf("{\"asan_driver\": \"%s\", \"failures\": %d}\n", failures ? "FAIL" : "ok", failures);
   return failures ? 1 : 0;
 }
