@@ -195,8 +195,11 @@ int ugo_fec_reconstruct_host(ugo_fec* ctx, uint8_t* shards, const uint64_t* pres
  * launch, no synchronize, same bytes and statuses.  The workgroup occupies one
  * CU while it waits; it leaves after `idle_us` (0 = 2000, at most 1000000)
  * without a request and is relaunched by the next call.  Every other call takes the usual path.
- * While it is resident, a device-wide synchronize (hipDeviceSynchronize) waits
- * for it to leave, i.e. up to idle_us after the last call.
+ * While it is resident, a device-wide synchronize (hipDeviceSynchronize, and
+ * hipFree, which synchronizes the device) waits for it to leave, i.e. up to
+ * idle_us after the last call.  Stream work does not: the block runs on a
+ * stream of its own priority class, so it has a hardware queue no ordinary
+ * stream shares (an ordinary stream placed on its queue would wait).
  * Failure: a call the service cannot complete (a GPU fault, or no answer
  * within the watchdog timeout, 5 s by default) turns the service off, asks the
  * workgroup to leave and waits up to the grace period (5 s by default) for it

@@ -337,3 +337,51 @@ def test_service_block_that_never_leaves_poisons_the_context(gpu):
         torch.cuda.synchronize()
     finally:
         fec.host_free(b.reshape(-1))
+
+
+def test_service_block_does_not_hold_other_streams(gpu):
+    """A resident block (1-s idle window) must not delay work on other streams:
+    its stream has a hardware queue of its own (create_service_stream).  Before
+    that, an ordinary stream that HIP's queue pool put on the service's queue
+    waited out the idle window -- a staged host encode on another context took
+    ~1 s instead of ~2 ms (tools/svc_sync_probe.cpp,
+    profiles/r4/svc_sync_probe_queue_ab.jsonl).  Device-wide synchronizes
+    (hipFree, torch.cuda.synchronize) still wait for the block, as documented."""
+    import torch
+
+    d, p, S = 10, 3, 1350
+    n, pitch = d + p, 1360
+    rng = np.random.default_rng(17)
+    svc, work = fec.New(d, p), fec.New(d, p)
+    one = _pinned(1, n, 1472, rng)
+    big = _pinned(8192, n, pitch, rng)  # 145 MB: past the zero-copy size, the staged 3-stream pipeline
+    try:
+        want = big.copy()
+        rs_ref.c_encode(d, p, want[:64], S=S)
+        work.encode_host(big, S)  # staging and streams allocated before the block is resident
+        x = torch.zeros(4, device="cuda")
+        x.add_(1)  # torch's kernel loaded before the block is resident
+        torch.cuda.synchronize()
+        svc.service_start(idle_us=1_000_000)
+        svc.encode_host(one, 1470)  # served: the block is resident for the next second
+        t0 = time.perf_counter()
+        work.encode_host(big, S)
+        host_ms = (time.perf_counter() - t0) * 1e3
+        worst = 0.0
+        for _ in range(8):
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                t0 = time.perf_counter()
+                x.add_(1)
+                s.synchronize()
+                worst = max(worst, (time.perf_counter() - t0) * 1e3)
+        svc.encode_host(one, 1470)
+        assert host_ms < 300, f"staged host encode waited for the service block: {host_ms:.1f} ms"
+        assert worst < 300, f"a fresh stream waited for the service block: {worst:.1f} ms"
+        assert np.array_equal(big[:64, :, :S], want[:64, :, :S])
+    finally:
+        svc.service_stop()
+        fec.host_free(one.reshape(-1))
+        fec.host_free(big.reshape(-1))
+        svc.close()
+        work.close()

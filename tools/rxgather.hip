@@ -1,5 +1,5 @@
 // rxgather.hip -- RX group assembly: the ring-ordered place kernel against the
-// destination-ordered index + gather pair (rx_kernels.hip), and the nt copy of
+// chunk path and the destination-ordered index + gather pair (rx_experiments.hpp), and the nt copy of
 // the same bytes, cold regime (rotating rings and batches, a cache-evicting
 // sweep before every sample), interleaved, medians.  Not product code.
 //
@@ -10,6 +10,7 @@
 // a ring with duplicates (different payloads), bad flags and short packets.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/rxgather tools/rxgather.hip
 #include "../ugo_amd/csrc/rx_kernels.hip"
+#include "rx_experiments.hpp"
 
 #include <algorithm>
 #include <cstdio>
@@ -232,11 +233,9 @@ int main(int argc, char** argv) {
     a.dup = nullptr;
     a.gate = nullptr;
     a.fixup = 0;
-    a.parts = nullptr;
     if (zero_present) CK(hipMemsetAsync(a.present, 0, a.groups * 8, s));
     a.seen = nullptr;
     a.call = 0;
-    a.cnt = nullptr;
     if (v.kind == GATHER) {
       CK(launch_rx_fill(win, a.groups * n, nullptr, s));
       a.win = win;
@@ -251,27 +250,8 @@ int main(int argc, char** argv) {
         k_rx_gather<3, 1, 32><<<gr, 256, 0, s>>>(a, d_parts, ib);
       return;
     }
-    if (v.kind == CHUNK) {  // ugo_fec_rx_assemble's chunk path
-      const unsigned long long call = ++call_id;
-      CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, s, d_cnt));
-      a.seen = d_seen;
-      a.call = call;
-      a.dup = dup;
-      a.prev = prev;
-      RxArgs f = a;
-      f.win = win;
-      f.gate = dup;
-      f.dup = nullptr;
-      f.stats = nullptr;
-      f.fixup = 1;
-      a.cnt = d_cnt;
-      CK(launch_rx_chunk(a, s));
-      CK(launch_rx_count(a, s));
-      RxArgs cl = f;
-      cl.cnt = d_cnt;
-      cl.stats = a.stats;
-      CK(launch_rx_claim(cl, s));
-      CK(launch_rx_scatter(f, s));
+    if (v.kind == CHUNK) {  // the round-4 chunk path (rx_experiments.hpp)
+      CK(launch_rx_chunk_path(a, prev, win, dup, d_cnt, d_seen, ++call_id, s));
       return;
     }
     if (v.kind == PROD) {
@@ -285,7 +265,7 @@ int main(int argc, char** argv) {
     a.dup = dup;
     a.prev = prev;
     const uint32_t blocks = rx_blocks(a);
-    k_rx_place<3, 0, 3, 0><<<blocks, 256, 0, s>>>(a);
+    k_rx_place<3, 0, 3><<<blocks, 256, 0, s>>>(a);
     if (v.kind == PROD_OLD) CK(launch_rx_fill(win, a.groups * n, dup, s));
     RxArgs f = a;
     f.win = win;
@@ -294,7 +274,7 @@ int main(int argc, char** argv) {
     f.stats = nullptr;
     f.fixup = 1;
     CK(launch_rx_claim(f, s));
-    k_rx_place<3, 0, 3, 0><<<blocks, 256, 0, s>>>(f);
+    k_rx_place<3, 0, 3><<<blocks, 256, 0, s>>>(f);
   };
 
   // ---- correctness: every variant against production on a ring with duplicates and junk
@@ -436,8 +416,8 @@ int main(int argc, char** argv) {
                   RxArgs a = rot[cnt++ % 3];
                   CK(hipMemsetAsync(a.present, 0, a.groups * 8, nullptr));
                   const unsigned long long call = ++call_id;
-                  CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, nullptr,
-                                     d_cnt));
+                  CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, nullptr));
+                  k_rx_zero_cnt<<<1, 256>>>(d_cnt);
                   a.prev = prev;
                   a.seen = d_seen;
                   a.call = call;

@@ -7,6 +7,7 @@
 // code.  argv: rounds.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/txgroup tools/txgroup.hip
 #include "../ugo_amd/csrc/tx_kernels.hip"
+#include "tx_experiments.hpp"
 
 #include <algorithm>
 #include <cstdio>

@@ -20,14 +20,10 @@ struct RxArgs {
   const uint64_t* prev;    // presence masks at call entry (launch_rx_begin's snapshot), or null: a packet
                            // whose bit was already set there is a duplicate of an earlier call's copy
   uint32_t fixup;          // re-place pass: claim winners only, no stats, presence already set
-  uint32_t* parts;         // if non-null: block b writes its five counters to parts[b*5 + k] instead of
-                           // adding them to stats (a full grid's blocks would contend on those words)
   const unsigned long long* seen;  // if non-null: k_rx_begin's record -- *seen >= call means some group had a
                            // presence bit set at call entry (or a concurrent later call's did); below
                            // call, none did, and the place pass skips its per-packet `prev` lookups
   unsigned long long call; // this call's id (per context, increasing)
-  uint32_t* cnt;           // chunk path: per-call counters (-, bad flag, out of window, too short, pieces
-                           // placed) x 32 shards, one 128-B line each; zeroed by k_rx_begin; or null
   uint64_t npk;
   uint64_t slot;
   uint64_t first_group;
@@ -41,26 +37,14 @@ struct RxArgs {
 // Claims every (group, row) for its first packet in ring order (atomicMin of
 // the packet index into a.win, which launch_rx_fill sets to 0xffffffff), then
 // places the winners.  a.win == null places every accepted packet.
-// Call entry: *dup = 0 and prev[g] = present[g] for every group (one launch).
 // Call entry, one launch: *dup = 0, prev[g] = present[g], win[0 .. words) =
 // 0xffffffff (claim words; win may be null), and atomicMax(seen, call) by
 // every block that finds a presence bit set (seen may be null).
 hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, uint32_t* win,
-                           uint64_t words, unsigned long long* seen, unsigned long long call, hipStream_t s,
-                           uint32_t* cnt = nullptr);
+                           uint64_t words, unsigned long long* seen, unsigned long long call, hipStream_t s);
 hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, hipStream_t s);
 hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s);
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s);
-
-// Chunk path (one 16-B output chunk per thread, full grid): taken when
-// rx_chunk_ok(a).  Sequence: launch_rx_begin (with a.cnt) -> launch_rx_chunk
-// (raises *a.dup on a second copy of a seqid) -> launch_rx_count ->
-// launch_rx_claim (a.cnt set, a.gate = the dup flag; its block 0 adds the
-// call's stats) -> launch_rx_scatter with fixup (gated on the same flag).
-constexpr uint32_t kRxCntWords = 5 * 32 * 32;  // 5 counters x 32 shards, one 128-B line each
-bool rx_chunk_ok(const RxArgs& a);
-hipError_t launch_rx_chunk(const RxArgs& a, hipStream_t s);
-hipError_t launch_rx_count(const RxArgs& a, hipStream_t s);
 
 }  // namespace kern
 }  // namespace ugo

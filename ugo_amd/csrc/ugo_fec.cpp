@@ -669,6 +669,37 @@ bool svc_eligible(const ugo_fec* c, const uint8_t* mapped, size_t groups, size_t
          (!recon || c->d_table);
 }
 
+// The service block's stream gets a hardware queue of its own.  HIP spreads
+// ordinary streams over a small pool of HSA queues (GPU_MAX_HW_QUEUES, 4 by
+// default) and a queue runs its packets in order: an ordinary stream that
+// landed on the service's queue would queue every launch and copy behind the
+// resident block, i.e. wait out the idle window (tools/svc_sync_probe.cpp:
+// a 65,536-group staged host encode took 1002 ms instead of 17 with a 1-s
+// window).
+#ifndef UGO_SVC_QUEUE
+#define UGO_SVC_QUEUE 2
+#endif
+hipError_t create_service_stream(ugo_fec* c) {
+#if UGO_SVC_QUEUE == 1
+  // a CU-masked stream is never pooled; but it is a blocking stream
+  hipDeviceProp_t prop{};
+  hipError_t e = hipGetDeviceProperties(&prop, c->device);
+  if (e != hipSuccess) return e;
+  const int cus = std::max(prop.multiProcessorCount, 1);
+  std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
+  if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+  return hipExtStreamCreateWithCUMask(&c->svc_stream, static_cast<uint32_t>(mask.size()), mask.data());
+#elif UGO_SVC_QUEUE == 2
+  // streams of another priority come from another queue pool
+  int lo = 0, hi = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(&c->svc_stream, hipStreamNonBlocking, hi);
+#else
+  return hipStreamCreateWithFlags(&c->svc_stream, hipStreamNonBlocking);
+#endif
+}
+
 // Writes one request (layout: SvcBox::line): every field, then the pieces'
 // tags, then seq; returns seq.
 uint32_t svc_post(ugo_fec* c, uint32_t op, const uint8_t* mapped, size_t groups, size_t S, size_t pitch,
@@ -1167,8 +1198,7 @@ int ugo_fec_service_start(ugo_fec* c, unsigned idle_us) {
     c->svc_dbox = c->svc_box;
     if (!device_view(c->svc_dbox)) return UGO_FEC_ERR_HIP;
   }
-  if (!c->svc_stream && hipStreamCreateWithFlags(&c->svc_stream, hipStreamNonBlocking) != hipSuccess)
-    return UGO_FEC_ERR_HIP;
+  if (!c->svc_stream && create_service_stream(c) != hipSuccess) return UGO_FEC_ERR_HIP;
   int khz = 0;  // wall_clock64's rate (100 MHz on gfx950)
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
   // at most 1 s resident after the last call: a process that exits without
@@ -1265,24 +1295,20 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   // (rx_kernels.hip): place everything, flag a (group, row) taken twice, and
   // only then -- gated on the flag, on the device -- claim and re-place.
   const hipStream_t s = static_cast<hipStream_t>(stream);
-  // scratch: presence snapshot [groups] u64 | claim words [groups][n] u32 | dup flag | chunk-path counters
+  // scratch: presence snapshot [groups] u64 | claim words [groups][n] u32 | dup flag
   const uint64_t words = groups * uint64_t(c->n);
   void* scratch = nullptr;
-  int st = scratch_alloc(c, groups * sizeof(uint64_t) + (words + 16 + ugo::kern::kRxCntWords) * sizeof(uint32_t), s,
-                         &scratch);
+  int st = scratch_alloc(c, groups * sizeof(uint64_t) + (words + 16) * sizeof(uint32_t), s, &scratch);
   if (st) return st;
   uint64_t* prev = static_cast<uint64_t*>(scratch);
   uint32_t* win = reinterpret_cast<uint32_t*>(prev + groups);
   uint32_t* dup = win + words;
-  uint32_t* cnt = dup + 16;
-  const bool chunk = ugo::kern::rx_chunk_ok(a);
   // call entry, one launch: dup = 0, the presence snapshot -- a (group, row)
   // an earlier call placed keeps that call's copy (ugo/fec.go:123-129 keeps the
   // first) -- the claim words, and whether any presence bit was set at all (if
   // none was, the place pass skips its per-packet snapshot lookups)
   const unsigned long long call = ++c->rx_calls;
-  st = hip_status(ugo::kern::launch_rx_begin(present, prev, groups, dup, win, words, c->d_rxseen, call, s,
-                                             chunk ? cnt : nullptr));
+  st = hip_status(ugo::kern::launch_rx_begin(present, prev, groups, dup, win, words, c->d_rxseen, call, s));
   a.dup = dup;
   a.prev = prev;
   a.seen = c->d_rxseen;
@@ -1293,21 +1319,8 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
   f.dup = nullptr;
   f.stats = nullptr;
   f.fixup = 1;
-  if (chunk) {
-    // one output chunk per thread; a second copy of a seqid raises dup (the
-    // presence atomic's old mask); k_rx_count counts the pieces placed for the
-    // stats, which the claim's block 0 adds whether or not it is gated off
-    a.cnt = cnt;
-    if (!st) st = hip_status(ugo::kern::launch_rx_chunk(a, s));
-    if (!st) st = hip_status(ugo::kern::launch_rx_count(a, s));
-    ugo::kern::RxArgs cl = f;  // gated on the chunk kernel's duplicate flag
-    cl.cnt = cnt;
-    cl.stats = stats;
-    if (!st) st = hip_status(ugo::kern::launch_rx_claim(cl, s));
-  } else {
-    if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
-    if (!st) st = hip_status(ugo::kern::launch_rx_claim(f, s));
-  }
+  if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
+  if (!st) st = hip_status(ugo::kern::launch_rx_claim(f, s));
   if (!st) st = hip_status(ugo::kern::launch_rx_scatter(f, s));
   const int fr = scratch_free(c, scratch, s);
   return st ? st : fr;
