@@ -949,6 +949,7 @@ def probe_library():
     vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     lib.ugo_probe_encode_twin.argtypes = [vp, i, sz, sz, sz, sz, i, vp, vp]
     lib.ugo_probe_nt_copy.argtypes = [vp, vp, i, sz, i, vp, vp]
+    lib.ugo_probe_reconstruct_twin.argtypes = [vp, vp, i, vp, sz, sz, sz, sz, sz, sz, i, vp, vp]
     return lib
 
 
@@ -971,14 +972,16 @@ def probe_nt_copy_ms(srcs, dsts, nbytes, reps, stream):
     return float(ms[1:].mean()) if reps > 1 else float(ms[0])
 
 
-def ceilings(args, batches, G, S, pitch, enc_bytes, stream):
+def ceilings(args, batches, G, S, pitch, enc_bytes, stream, masks=None, outs=None, dec_bytes=0):
     """the encode's ceiling measured in this run, on the
     same cold rotated batches (launch r on batch r % B): the compute-free twin
     of k_encode_g (same loads, LDS stage, residency and nt stores; XOR instead
     of the GF network) and a plain nt copy moving the same 1.15 GB (half a
     batch read, the other half written).  Each launch timed with its own
     hipExtLaunchKernel start/stop events, as the kernel pass times the encode.
-    The twin writes wrong parity on purpose: run after the verification."""
+    With masks and outs (the step's reconstruct into separate outputs): the
+    compute-free twin of k_apply_p too, on the same batches and outputs.
+    The twins write wrong bytes on purpose: run after the verification."""
     import ctypes
 
     import numpy as np
@@ -998,9 +1001,19 @@ def ceilings(args, batches, G, S, pitch, enc_bytes, stream):
     assert copy_bytes <= half
     copy_ms = probe_nt_copy_ms([b.data_ptr() for b in batches], [b.data_ptr() + half for b in batches], copy_bytes,
                                reps, stream.cuda_stream)
-    return {"encode_twin_ms": round(twin_ms, 5), "encode_twin_GBps": round(enc_bytes / (twin_ms * 1e-3) / 1e9, 1),
-            "nt_copy_ms": round(copy_ms, 5), "nt_copy_GBps": round(2 * copy_bytes / (copy_ms * 1e-3) / 1e9, 1),
-            "reps": reps}
+    res = {"encode_twin_ms": round(twin_ms, 5), "encode_twin_GBps": round(enc_bytes / (twin_ms * 1e-3) / 1e9, 1),
+           "nt_copy_ms": round(copy_ms, 5), "nt_copy_GBps": round(2 * copy_bytes / (copy_ms * 1e-3) / 1e9, 1),
+           "reps": reps}
+    if masks is not None and outs is not None and dec_bytes:
+        ob = (ctypes.c_void_p * nb)(*[o.data_ptr() for o in outs])
+        rc = lib.ugo_probe_reconstruct_twin(bases, ob, nb, masks.data_ptr(), G, S, pitch, rs, outs[0].stride(0),
+                                            outs[0].stride(1), reps, stream.cuda_stream, ms.ctypes.data)
+        if rc:
+            raise RuntimeError(f"ugo_probe_reconstruct_twin failed ({rc})")
+        rt_ms = float(ms[1:].mean())
+        res["reconstruct_twin_ms"] = round(rt_ms, 5)
+        res["reconstruct_twin_GBps"] = round(dec_bytes / (rt_ms * 1e-3) / 1e9, 1)
+    return res
 
 
 def rc4_pad(nbytes, dev):
@@ -1358,7 +1371,9 @@ def run_rank(args):
     ceil = None
     if planar and args.row_pad == 0 and d == 10 and p == 3 and nb >= 1:
         try:
-            ceil = ceilings(args, batches, G, S, pitch, G * n * S, stream)
+            oplan = into and oplanar and outs is not None
+            ceil = ceilings(args, batches, G, S, pitch, G * n * S, stream, masks if oplan else None,
+                            outs if oplan else None, dec_bytes)
         except Exception as ex:  # noqa: BLE001 -- a secondary measurement never loses the line
             ceil = {"error": repr(ex)[:300]}
 
@@ -1411,9 +1426,15 @@ def run_rank(args):
                 "measured in this run on the same 2 cold rotated batches: encode_twin = k_encode_g's compute-free "
                 "twin (same LDS-DMA / register loads, 52-KiB stage = 3 blocks per CU, nt stores; XOR instead of the "
                 "GF network), GBps of the encode's algorithmic bytes; nt_copy = a 1-chunk-per-thread nt copy "
-                "moving the same 1.15 GB (libugoprobe.so, ugo_amd/csrc/probe_kernels.hip)"))
+                "moving the same 1.15 GB; reconstruct_twin = k_apply_p's compute-free twin (same grid, the first d "
+                "present rows of each group by nt loads, one nt store per erased row into the same output batches; "
+                "XOR instead of the split-table products), GBps of the reconstruct's algorithmic bytes "
+                "(libugoprobe.so, ugo_amd/csrc/probe_kernels.hip)"))
         elif ceil:
             roof["ceiling"] = ceil
+        if ceil and "reconstruct_twin_GBps" in ceil and "reconstruct" in kern:
+            kern["reconstruct"]["twin_GBps"] = ceil["reconstruct_twin_GBps"]
+            kern["reconstruct"]["frac_of_twin"] = round(kern["reconstruct"]["GBps"] / ceil["reconstruct_twin_GBps"], 4)
         roof.update({
                 "note": f"achieved = algorithmic bytes per launch ({'(d+p)*S' if dom == 'encode' else '(d+e)*S'}"
                         f" per group x {G} groups) / avg kernel duration over a kernel-timing pass of the same "

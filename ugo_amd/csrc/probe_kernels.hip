@@ -9,6 +9,12 @@
 //     same nt stores of 3 parity rows with the same tail handling -- with each
 //     parity row a plain XOR of the inputs instead of the GF network (wrong
 //     bytes on purpose: it is the access pattern alone);
+//   * ugo_probe_reconstruct_twin: the compute-free twin of the (10,3)
+//     reconstruct into separate outputs, k_apply_p<10,1,3> -- the same grid
+//     (one 16-B chunk of one group per thread), the wave's two group masks by
+//     scalar loads, the first d present rows of the lane's group by nt loads,
+//     one nt store per erased row into the output batch -- with every output a
+//     plain XOR of the survivors instead of the split-table products;
 //   * ugo_probe_nt_copy: an nt copy, one 16-B chunk per thread over a full
 //     grid (the fastest copy form measured, tools/rxgather.hip).
 // Each launch is timed with hipExtLaunchKernel start/stop events (the same
@@ -67,6 +73,49 @@ __global__ __launch_bounds__(256) void k_encode_twin(Twin a) {
   }
 }
 
+struct RTwin {
+  const uint8_t* base;
+  uint8_t* out;
+  const uint64_t* present;
+  uint64_t rstride, gstride, orstride, ogstride;
+  uint32_t chunks, S, items;
+};
+
+// k_apply_p<10, MODE 1, NT 3>'s loads and stores for (10,3)
+__global__ __launch_bounds__(256) void k_reconstruct_twin(RTwin a) {
+  constexpr int D = 10, N = 13, P = 3;
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  if (wfirst >= a.items) return;
+  const uint32_t wlast = min(wfirst + 63u, a.items - 1u);
+  const uint32_t gA = wfirst / a.chunks, gB = wlast / a.chunks;
+  const uint64_t mA = a.present[gA], mB = a.present[gB];  // uniform: scalar loads
+  if (item >= a.items) return;
+  const uint32_t gl = item / a.chunks, c = item - gl * a.chunks;
+  const uint32_t m = static_cast<uint32_t>(gl == gA ? mA : mB) & ((1u << N) - 1u);
+  const uint8_t* gp = a.base + gl * a.gstride + static_cast<uint64_t>(c) * 16u;
+  const uint32_t nb = a.S - c * 16u;
+  V4 x[N];
+#pragma unroll
+  for (int r = 0; r < N; ++r) {  // the first D present rows
+    const bool take = ((m >> r) & 1u) && __builtin_popcount(m & ((1u << r) - 1u)) < D;
+    x[r] = take ? load16<1>(gp + static_cast<uint64_t>(r) * a.rstride) : V4{{0u, 0u, 0u, 0u}};
+  }
+  V4 y = x[0];
+#pragma unroll
+  for (int r = 1; r < N; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y.v[j] ^= x[r].v[j];
+  const uint32_t e = min(static_cast<uint32_t>(__builtin_popcount(~m & ((1u << N) - 1u))), static_cast<uint32_t>(P));
+  uint8_t* op = a.out + gl * a.ogstride + static_cast<uint64_t>(c) * 16u;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    if (i >= static_cast<int>(e)) continue;
+    y.v[0] ^= static_cast<uint32_t>(i);
+    store16<2>(op + static_cast<uint64_t>(i) * a.orstride, y, nb);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_nt_copy(const u32x4* src, u32x4* dst, uint64_t n16) {
   const uint64_t c = blockIdx.x * 256ull + threadIdx.x;
   if (c >= n16) return;
@@ -109,6 +158,30 @@ int ugo_probe_encode_twin(uint8_t* const* bases, int nbuf, size_t groups, size_t
         Twin a{bases[r % nbuf], row_stride, pitch, static_cast<uint32_t>(chunks), static_cast<uint32_t>(S),
                static_cast<uint32_t>(items)};
         hipExtLaunchKernelGGL(k_encode_twin, grid, block, 0, s, e0, e1, 0u, a);
+        return hipGetLastError();
+      },
+      reps, s, ms_out);
+}
+
+// reps launches of the reconstruct twin: launch r reads bases[r % nbuf]
+// (planar (10+3): rows at row_stride, groups at pitch) with the per-group
+// presence masks `present` (device) and writes outs[r % nbuf] (output slot i of
+// group g at i * out_row_stride + g * out_pitch); ms_out[r] = its duration.
+int ugo_probe_reconstruct_twin(const uint8_t* const* bases, uint8_t* const* outs, int nbuf, const uint64_t* present,
+                               size_t groups, size_t S, size_t pitch, size_t row_stride, size_t out_row_stride,
+                               size_t out_pitch, int reps, void* stream, float* ms_out) {
+  if (!bases || !outs || !present || nbuf <= 0 || !ms_out || reps <= 0 || S == 0 || pitch < S || pitch % 16 ||
+      row_stride % 16 || out_pitch < S || out_pitch % 16 || out_row_stride % 16)
+    return 2;
+  const uint64_t chunks = (S + 15) / 16, items = groups * chunks;
+  if (items == 0 || items > 0xffffffffull) return 2;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<uint32_t>((items + 255) / 256)), block(256);
+  return timed(
+      [&](int r, hipEvent_t e0, hipEvent_t e1) {
+        RTwin a{bases[r % nbuf], outs[r % nbuf], present, row_stride, pitch, out_row_stride, out_pitch,
+                static_cast<uint32_t>(chunks), static_cast<uint32_t>(S), static_cast<uint32_t>(items)};
+        hipExtLaunchKernelGGL(k_reconstruct_twin, grid, block, 0, s, e0, e1, 0u, a);
         return hipGetLastError();
       },
       reps, s, ms_out);
