@@ -5,7 +5,9 @@
 // launch_rx_claim) they use.  Not product code.
 //
 //  * chunk path: k_rx_chunk (one 16-B output chunk per thread, full grid) +
-//    k_rx_count + k_rx_chunk_claim, 597-600 us against production's 523-535 us;
+//    k_rx_count + k_rx_chunk_stats, 597-600 us against production's 523-535 us;
+//  * production's place kernel over a full grid + k_rx_tally: 712-722 us
+//    against 500-518 (every packet reloads its lane's keystream chunks);
 //  * destination-ordered index + gather (k_rx_index, k_rx_gather), slower still.
 #pragma once
 
@@ -170,6 +172,74 @@ inline hipError_t launch_rx_chunk_path(RxArgs a, uint64_t* prev, uint32_t* win, 
   if (blocks > 64u) blocks = 64u;
   k_rx_count<<<static_cast<uint32_t>(blocks ? blocks : 1), 256, 0, s>>>(a.present, prev, a.groups, cnt);
   if (a.stats) k_rx_chunk_stats<<<1, 1, 0, s>>>(cnt, a.stats, a.npk);
+  e = launch_rx_claim(f, s);
+  if (e != hipSuccess) return e;
+  return launch_rx_scatter(f, s);
+}
+
+// ---------------------------------------------------------------------------
+// Full-grid place: k_rx_place with one packet per half-wave (blocks =
+// ceil(npk / 8), the P3b shape) -- per-block stats adds would contend, so the
+// blocks add only the rare classes to the call's scratch counters rare[1..3]
+// (RARE = 1) and k_rx_tally turns the presence bits this call set into the
+// accepted count: stats[0] += placed, stats[1..3] += rare[1..3],
+// stats[4] += npk - placed - rare (every other valid packet was a duplicate).
+// Each block adds its share of placed (wrapping uint32 arithmetic).
+__global__ __launch_bounds__(256) void k_rx_tally(const uint64_t* present, const uint64_t* prev, uint64_t groups,
+                                                  const uint32_t* rare, uint32_t* stats, uint64_t npk) {
+  __shared__ uint32_t tot;
+  if (threadIdx.x == 0) tot = 0;
+  __syncthreads();
+  uint32_t c = 0;
+  for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < groups; g += gridDim.x * 256ull)
+    c += __popcll(present[g] & ~prev[g]);
+  if (c) atomicAdd(&tot, c);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (tot) {
+      atomicAdd(&stats[0], tot);
+      atomicSub(&stats[4], tot);
+    }
+    if (blockIdx.x == 0) {
+      const uint32_t r1 = rare[1], r2 = rare[2], r3 = rare[3];
+      if (r1) atomicAdd(&stats[1], r1);
+      if (r2) atomicAdd(&stats[2], r2);
+      if (r3) atomicAdd(&stats[3], r3);
+      atomicAdd(&stats[4], static_cast<uint32_t>(npk) - r1 - r2 - r3);
+    }
+  }
+}
+
+__global__ void k_rx_zero_rare(uint32_t* rare) {
+  if (threadIdx.x < 8) rare[threadIdx.x] = 0u;
+}
+
+// begin -> zero rare -> full-grid place (RARE) -> tally -> gated claim -> gated re-place (grid-stride)
+inline hipError_t launch_rx_full_path(RxArgs a, uint64_t* prev, uint32_t* win, uint32_t* dup, uint32_t* rare,
+                                      unsigned long long* seen, unsigned long long call, hipStream_t s) {
+  hipError_t e = launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * a.n, seen, call, s);
+  if (e != hipSuccess) return e;
+  k_rx_zero_rare<<<1, 64, 0, s>>>(rare);
+  a.seen = seen;
+  a.call = call;
+  a.dup = dup;
+  a.prev = prev;
+  RxArgs f = a;
+  f.win = win;
+  f.gate = dup;
+  f.dup = nullptr;
+  f.stats = nullptr;
+  f.fixup = 1;
+  uint32_t* user_stats = a.stats;
+  a.stats = user_stats ? rare : nullptr;
+  const uint32_t blocks = static_cast<uint32_t>((a.npk + 7) / 8);
+  if (blocks) k_rx_place<3, 0, 3, 1><<<blocks, 256, 0, s>>>(a);
+  if (user_stats) {
+    uint64_t tb = (a.groups + 255) / 256;
+    if (tb > 64u) tb = 64u;
+    k_rx_tally<<<static_cast<uint32_t>(tb ? tb : 1), 256, 0, s>>>(a.present, prev, a.groups, rare, user_stats,
+                                                               a.npk);
+  }
   e = launch_rx_claim(f, s);
   if (e != hipSuccess) return e;
   return launch_rx_scatter(f, s);

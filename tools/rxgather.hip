@@ -202,7 +202,7 @@ int main(int argc, char** argv) {
   uint32_t* win = reinterpret_cast<uint32_t*>(prev + G);
   uint32_t* dup = win + G * n;
 
-  enum Kind { PROD, PROD_OLD, GATHER, CHUNK };
+  enum Kind { PROD, PROD_OLD, GATHER, CHUNK, FULL };
   struct Var {
     std::string name;
     Kind kind;
@@ -213,6 +213,7 @@ int main(int argc, char** argv) {
       {"production (round 4): begin(+claim fill, fresh flag) + place + gated claim/re-place", PROD, 0, 0, 0},
       {"production (round 3): begin + place + gated fill/claim/re-place", PROD_OLD, 0, 0, 0},
       {"chunk path: begin + chunk (one output chunk per thread) + count + gated claim/re-place", CHUNK, 0, 0, 0},
+      {"full-grid place: begin + zero rare + place (one packet per half-wave, npk/8 blocks) + tally + gated claim/re-place", FULL, 0, 0, 0},
   };
   uint32_t* d_cnt;
   CK(hipMalloc(&d_cnt, kRxCntWords * 4));
@@ -248,6 +249,10 @@ int main(int argc, char** argv) {
         k_rx_gather<3, 1, 8><<<gr, 256, 0, s>>>(a, d_parts, ib);
       else
         k_rx_gather<3, 1, 32><<<gr, 256, 0, s>>>(a, d_parts, ib);
+      return;
+    }
+    if (v.kind == FULL) {
+      CK(launch_rx_full_path(a, prev, win, dup, d_cnt, d_seen, ++call_id, s));
       return;
     }
     if (v.kind == CHUNK) {  // the round-4 chunk path (rx_experiments.hpp)

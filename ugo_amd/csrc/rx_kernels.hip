@@ -195,7 +195,11 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 // MODE (A/B timing only, tools/rxvariants.hip): 0 = production, 1 = without
 // the presence atomics, 2 = the same loads and stores without the realignment.
 // NT: bit 0 nontemporal payload loads, bit 1 nontemporal stores.
-template <int NP, int MODE = 0, int NT = 0>
+// RARE (A/B only, tools/rx_experiments.hpp full-grid path): 1 = a block adds
+// only its bad-flag / out-of-window / too-short counts to a.stats (the call's
+// scratch counters; accepted and duplicates are tallied from the presence bits
+// afterwards).  The full grid lost: 712 vs 500 us.
+template <int NP, int MODE = 0, int NT = 0, int RARE = 0>
 __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
   if (rx_gated_off(a)) return;
   __shared__ uint32_t bstats[5];
@@ -335,7 +339,8 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
   if (hl == 0) acct.settle(a, bstats);
   if (a.stats) {
     __syncthreads();
-    if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+    const bool mine = RARE ? (threadIdx.x >= 1 && threadIdx.x <= 3) : threadIdx.x < 5;
+    if (mine && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
   }
 }
 
