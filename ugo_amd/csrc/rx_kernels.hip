@@ -46,6 +46,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) { return *reinterpret_cast<const u32x4*>(p); }
 
+// 16 bytes at any byte address (one global_load_dwordx4: gfx950 runs with
+// unaligned access enabled)
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+template <bool NTL>
+__device__ __forceinline__ u32x4 ldu16(const uint8_t* p) {
+  if constexpr (NTL)
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(p));
+  else
+    return *reinterpret_cast<const u32x4u*>(p);
+}
+
 __device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
   // DPP wave_shl:1 -- lane l receives lane l+1's value (lane 63 receives 0)
   return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x130, 0xf, 0xf, false));
@@ -192,8 +203,11 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 //    a packet are issued before its first store (the per-pass load -> store
 //    chain of k_rx_scatter kept one 1-KiB load in flight per wave);
 //  * lengths are clamped to the slot.
-// MODE (A/B timing only, tools/rxvariants.hip): 0 = production, 1 = without
-// the presence atomics, 2 = the same loads and stores without the realignment.
+// MODE: 0 = production (aligned loads realigned by DPP); A/B only
+// (tools/rxgather.hip, profiles/r4/rxgather_{attribution,unaligned}_*): 1 =
+// without the presence atomics (timing only, -5 us), 2 = the same loads and
+// stores without the realignment (timing only, -20 us), 3 = unaligned payload
+// loads instead of the realignment (bit-exact, but +13 us: 522 vs 509).
 // NT: bit 0 nontemporal payload loads, bit 1 nontemporal stores.
 // RARE (A/B only, tools/rx_experiments.hpp full-grid path): 1 = a block adds
 // only its bad-flag / out-of-window / too-short counts to a.stats (the call's
@@ -219,8 +233,12 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
     const uint32_t o = 16u * (32u * q + hl);
-    K[q] = (a.pad && o + 16u <= slot) ? ld16(a.pad + o) : zero;
     kbx[q] = kby[q] = 0u;
+    if constexpr (MODE == 3) {  // keystream at the payload's offsets, unaligned
+      K[q] = (a.pad && o + 22u <= slot) ? ldu16<false>(a.pad + 6u + o) : zero;
+      continue;
+    }
+    K[q] = (a.pad && o + 16u <= slot) ? ld16(a.pad + o) : zero;
     if (a.pad && hl == 31u && o + 32u <= slot) {
       const u32x4 B = ld16(a.pad + o + 16u);
       kbx[q] = B.x;
@@ -270,9 +288,13 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       const uint32_t o = 16u * (32u * q + hl);
+      bx[q] = by[q] = 0u;
+      if constexpr (MODE == 3) {  // payload bytes [o, o+16) directly (host: 16*floor((S-1)/16) + 22 <= slot)
+        A[q] = o < L ? ldu16<(NT & 1) != 0>(pk + 6u + o) : zero;
+        continue;
+      }
       A[q] = o < lim ? ((NT & 1) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + o)) : ld16(pk + o))
                      : zero;
-      bx[q] = by[q] = 0u;
       if (hl == 31u && o + 16u < lim) {
         const u32x4 B = ld16(pk + o + 16u);
         bx[q] = B.x;
@@ -288,14 +310,18 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
       const uint32_t o = 16u * (32u * q + hl);
       const u32x4 Aq = A[q] ^ K[q];  // bytes past lim are masked below
       // converged: neighbour's chunk (packet bytes [o+16, o+32)) by DPP
-      uint32_t nx = from_next_lane(Aq.x), ny = from_next_lane(Aq.y);
-      if (hl == 31u) {
-        nx = bx[q] ^ kbx[q];
-        ny = by[q] ^ kby[q];
+      uint32_t nx = 0u, ny = 0u;
+      if constexpr (MODE != 3) {
+        nx = from_next_lane(Aq.x);
+        ny = from_next_lane(Aq.y);
+        if (hl == 31u) {
+          nx = bx[q] ^ kbx[q];
+          ny = by[q] ^ kby[q];
+        }
       }
       if (!ok || o >= a.S) continue;
       uint32_t w[4];
-      if constexpr (MODE == 2) {
+      if constexpr (MODE == 2 || MODE == 3) {
         w[0] = Aq.x; w[1] = Aq.y; w[2] = Aq.z; w[3] = Aq.w;
       } else {
         // payload bytes [o, o+16) = packet bytes [o+6, o+22)
@@ -330,7 +356,7 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
       }
     }
     if (hl == 0) {
-      if constexpr (MODE == 0)
+      if constexpr (MODE == 0 || MODE == 3)
         acct.issue(a, bstats, why, grp - a.first_group, row);
       else if (why < 5)
         atomicAdd(&bstats[why], 1u);
