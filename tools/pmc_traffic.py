@@ -28,7 +28,7 @@ KERNELS = {"k_encode_c": "encode", "k_encode_g": "encode", "k_encode_frs": "enco
            # the rx_tx leg and the ceilings (round 4)
            "k_rx_place": "rx_place", "k_rx_chunk": "rx_chunk", "k_rx_begin": "rx_begin", "k_rx_count": "rx_count",
            "k_rx_claim": "rx_claim", "k_tx_g": "tx", "k_tx_c": "tx", "k_packet_decode": "packet_decode",
-           "k_encode_twin": "encode_twin", "k_nt_copy": "nt_copy"}
+           "k_encode_twin": "encode_twin", "k_reconstruct_twin": "reconstruct_twin", "k_nt_copy": "nt_copy"}
 BENCH_KINDS = ("encode", "reconstruct")  # the kinds whose last `steps` dispatches are the bench's timed steps
 
 

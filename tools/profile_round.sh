@@ -12,7 +12,7 @@ TAG=${1:-r1}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--steps 40 --warmup 50 --no-verify --no-cpu-baseline --no-host-path --c4-total-groups 0 ${BENCH_EXTRA:-}"
+ARGS="--steps 40 --warmup 50 --no-verify --no-cpu-baseline --no-host-path --no-rx-tx --c4-total-groups 0 ${BENCH_EXTRA:-}"
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 bench.py $ARGS \
