@@ -12,7 +12,8 @@
 //   * ugo_probe_reconstruct_twin: the compute-free twin of the (10,3)
 //     reconstruct into separate outputs, k_apply_p<10,1,3> -- the same grid
 //     (one 16-B chunk of one group per thread), the wave's two group masks by
-//     scalar loads, the first d present rows of the lane's group by nt loads,
+//     scalar loads, their survivor lists packed as the descriptor's row words
+//     and picked per lane, the first d present rows by nt loads,
 //     one nt store per erased row into the output batch -- with every output a
 //     plain XOR of the survivors instead of the split-table products;
 //   * ugo_probe_nt_copy: an nt copy, one 16-B chunk per thread over a full
@@ -92,20 +93,40 @@ __global__ __launch_bounds__(256) void k_reconstruct_twin(RTwin a) {
   const uint64_t mA = a.present[gA], mB = a.present[gB];  // uniform: scalar loads
   if (item >= a.items) return;
   const uint32_t gl = item / a.chunks, c = item - gl * a.chunks;
-  const uint32_t m = static_cast<uint32_t>(gl == gA ? mA : mB) & ((1u << N) - 1u);
+  const bool inB = gl != gA;
+  const uint32_t m = static_cast<uint32_t>(inB ? mB : mA) & ((1u << N) - 1u);
+  // survivor rows of the wave's two groups, packed 4 per word as k_apply_p's
+  // descriptor words hold them (uniform: scalar work), picked per lane
+  uint32_t rA[3] = {0u, 0u, 0u}, rB[3] = {0u, 0u, 0u};
+  {
+    uint32_t ka = 0, kb = 0;
+    const uint32_t ma = static_cast<uint32_t>(mA), mb = static_cast<uint32_t>(mB);
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      if (((ma >> r) & 1u) && ka < static_cast<uint32_t>(D)) {
+        rA[ka >> 2] |= static_cast<uint32_t>(r) << (8 * (ka & 3));
+        ++ka;
+      }
+      if (((mb >> r) & 1u) && kb < static_cast<uint32_t>(D)) {
+        rB[kb >> 2] |= static_cast<uint32_t>(r) << (8 * (kb & 3));
+        ++kb;
+      }
+    }
+  }
   const uint8_t* gp = a.base + gl * a.gstride + static_cast<uint64_t>(c) * 16u;
   const uint32_t nb = a.S - c * 16u;
-  V4 x[N];
+  V4 x[D];
 #pragma unroll
-  for (int r = 0; r < N; ++r) {  // the first D present rows
-    const bool take = ((m >> r) & 1u) && __builtin_popcount(m & ((1u << r) - 1u)) < D;
-    x[r] = take ? load16<1>(gp + static_cast<uint64_t>(r) * a.rstride) : V4{{0u, 0u, 0u, 0u}};
+  for (int k = 0; k < D; ++k) {
+    const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
+    const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
+    x[k] = load16<1>(gp + static_cast<uint64_t>(r) * a.rstride);
   }
   V4 y = x[0];
 #pragma unroll
-  for (int r = 1; r < N; ++r)
+  for (int k = 1; k < D; ++k)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) y.v[j] ^= x[r].v[j];
+    for (int j = 0; j < 4; ++j) y.v[j] ^= x[k].v[j];
   const uint32_t e = min(static_cast<uint32_t>(__builtin_popcount(~m & ((1u << N) - 1u))), static_cast<uint32_t>(P));
   uint8_t* op = a.out + gl * a.ogstride + static_cast<uint64_t>(c) * 16u;
 #pragma unroll
