@@ -78,6 +78,7 @@ struct RTwin {
   const uint8_t* base;
   uint8_t* out;
   const uint64_t* present;
+  const uint64_t* rows;  // [2^13]: the first d present rows of each mask, 4 bits each
   uint64_t rstride, gstride, orstride, ogstride;
   uint32_t chunks, S, items;
 };
@@ -95,31 +96,16 @@ __global__ __launch_bounds__(256) void k_reconstruct_twin(RTwin a) {
   const uint32_t gl = item / a.chunks, c = item - gl * a.chunks;
   const bool inB = gl != gA;
   const uint32_t m = static_cast<uint32_t>(inB ? mB : mA) & ((1u << N) - 1u);
-  // survivor rows of the wave's two groups, packed 4 per word as k_apply_p's
-  // descriptor words hold them (uniform: scalar work), picked per lane
-  uint32_t rA[3] = {0u, 0u, 0u}, rB[3] = {0u, 0u, 0u};
-  {
-    uint32_t ka = 0, kb = 0;
-    const uint32_t ma = static_cast<uint32_t>(mA), mb = static_cast<uint32_t>(mB);
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-      if (((ma >> r) & 1u) && ka < static_cast<uint32_t>(D)) {
-        rA[ka >> 2] |= static_cast<uint32_t>(r) << (8 * (ka & 3));
-        ++ka;
-      }
-      if (((mb >> r) & 1u) && kb < static_cast<uint32_t>(D)) {
-        rB[kb >> 2] |= static_cast<uint32_t>(r) << (8 * (kb & 3));
-        ++kb;
-      }
-    }
-  }
+  // survivor rows of the wave's two groups, packed as nibbles, from a table
+  // indexed by the presence mask (scalar loads, as production's descriptors)
+  const uint64_t pa = a.rows[mA & ((1u << N) - 1u)], pb = a.rows[mB & ((1u << N) - 1u)];
+  const uint64_t pr = inB ? pb : pa;
   const uint8_t* gp = a.base + gl * a.gstride + static_cast<uint64_t>(c) * 16u;
   const uint32_t nb = a.S - c * 16u;
   V4 x[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
-    const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
-    const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
+    const uint32_t r = static_cast<uint32_t>(pr >> (4 * k)) & 15u;
     x[k] = load16<1>(gp + static_cast<uint64_t>(r) * a.rstride);
   }
   V4 y = x[0];
@@ -197,12 +183,26 @@ int ugo_probe_reconstruct_twin(const uint8_t* const* bases, uint8_t* const* outs
   const uint64_t chunks = (S + 15) / 16, items = groups * chunks;
   if (items == 0 || items > 0xffffffffull) return 2;
   const hipStream_t s = static_cast<hipStream_t>(stream);
+  static uint64_t* rows = nullptr;  // built once per process
+  if (!rows) {
+    uint64_t h[1u << 13];
+    for (uint32_t m = 0; m < (1u << 13); ++m) {
+      uint64_t v = 0;
+      for (uint32_t r = 0, k = 0; r < 13 && k < 10; ++r)
+        if ((m >> r) & 1u) v |= static_cast<uint64_t>(r) << (4 * k++);
+      h[m] = v;
+    }
+    if (hipMalloc(&rows, sizeof(h)) != hipSuccess || hipMemcpy(rows, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess)
+      return 1;
+  }
   const dim3 grid(static_cast<uint32_t>((items + 255) / 256)), block(256);
   return timed(
       [&](int r, hipEvent_t e0, hipEvent_t e1) {
-        RTwin a{bases[r % nbuf], outs[r % nbuf], present, row_stride, pitch, out_row_stride, out_pitch,
+        RTwin a{bases[r % nbuf], outs[r % nbuf], present, rows, row_stride, pitch, out_row_stride, out_pitch,
                 static_cast<uint32_t>(chunks), static_cast<uint32_t>(S), static_cast<uint32_t>(items)};
-        hipExtLaunchKernelGGL(k_reconstruct_twin, grid, block, 0, s, e0, e1, 0u, a);
+        // 36 KiB of dynamic LDS it never touches: 4 blocks (4 waves per SIMD)
+        // per CU, k_apply_p<10,1,3>'s own occupancy (99 VGPRs)
+        hipExtLaunchKernelGGL(k_reconstruct_twin, grid, block, 36u * 1024u, s, e0, e1, 0u, a);
         return hipGetLastError();
       },
       reps, s, ms_out);
