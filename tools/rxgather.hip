@@ -210,15 +210,15 @@ int main(int argc, char** argv) {
     uint32_t grid;
   };
   std::vector<Var> vars = {
-      {"production (round 4): begin(+claim fill, fresh flag) + place + gated claim/re-place", PROD, 0, 0, 0},
-      {"production (round 3): begin + place + gated fill/claim/re-place", PROD_OLD, 0, 0, 0},
+      {"production (round 4): begin(+claim fill, fresh flag) + place (MODE 4, 8192 blocks) + gated claim/re-place", PROD, 0, 0, 0},
+      {"production (round 3): begin + place (MODE 0, 2048 blocks) + gated fill/claim/re-place", PROD_OLD, 0, 0, 2048},
       {"chunk path: begin + chunk (one output chunk per thread) + count + gated claim/re-place", CHUNK, 0, 0, 0},
       {"full-grid place: begin + zero rare + place (one packet per half-wave, npk/8 blocks) + tally + gated claim/re-place", FULL, 0, 0, 0},
-      {"production, place grid 8192 blocks", PROD, 0, 0, 8192},
+      {"round-4 first form: MODE 0 (DPP, lane-31 neighbour loads), place grid 2048", PROD, 5, 0, 2048},
       {"production with the place kernel's presence atomics removed (MODE 1, timing only)", PROD, 1, 0, 0},
       {"production with the place kernel's realignment removed (MODE 2, timing only)", PROD, 2, 0, 0},
       {"production with unaligned payload loads (MODE 3: no realignment, no neighbour loads)", PROD, 3, 0, 0},
-      {"production MODE 3, place grid 8192 blocks", PROD, 3, 0, 8192},
+
   };
   uint32_t* d_cnt;
   CK(hipMalloc(&d_cnt, kRxCntWords * 4));
@@ -275,7 +275,12 @@ int main(int argc, char** argv) {
     a.dup = dup;
     a.prev = prev;
     const uint32_t blocks = v.grid ? v.grid : rx_blocks(a);
-    if (v.kind == PROD && v.order == 1)
+    if (v.kind == PROD && (v.order == 0 || v.order == 5)) {
+      if (v.order == 5)
+        k_rx_place<3, 0, 3><<<blocks, 256, 0, s>>>(a);
+      else
+        k_rx_place<3, 4, 3><<<blocks, 256, 0, s>>>(a);  // production
+    } else if (v.kind == PROD && v.order == 1)
       k_rx_place<3, 1, 3><<<blocks, 256, 0, s>>>(a);
     else if (v.kind == PROD && v.order == 2)
       k_rx_place<3, 2, 3><<<blocks, 256, 0, s>>>(a);
@@ -291,7 +296,10 @@ int main(int argc, char** argv) {
     f.stats = nullptr;
     f.fixup = 1;
     CK(launch_rx_claim(f, s));
-    k_rx_place<3, 0, 3><<<blocks, 256, 0, s>>>(f);
+    if (v.kind == PROD && v.order == 0)
+      CK(launch_rx_scatter(f, s));  // production's re-place
+    else
+      k_rx_place<3, 0, 3><<<blocks, 256, 0, s>>>(f);
   };
 
   // ---- correctness: every variant against production on a ring with duplicates and junk

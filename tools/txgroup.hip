@@ -152,6 +152,9 @@ int main(int argc, char** argv) {
   auto run_c = [&](TxArgs a) {
     k_tx_c<10, 3, kTxNT, true><<<static_cast<uint32_t>((a.groups * a.chunks + 255) / 256), 256, tx_lds_cap()>>>(a);
   };
+  auto run_cl = [&](TxArgs a) {
+    k_tx_c<10, 3, kTxNT, true, true><<<static_cast<uint32_t>((a.groups * a.chunks + 255) / 256), 256, tx_lds_cap()>>>(a);
+  };
   auto run_g = [&](TxArgs a) { k_tx_g<10, 3><<<static_cast<uint32_t>(a.groups), 256, lds>>>(a); };
   auto run_o = [&](TxArgs a, int swz) {
     const uint32_t blocks = static_cast<uint32_t>((a.groups * 13 * a.chunks + 255) / 256);
@@ -218,6 +221,17 @@ int main(int argc, char** argv) {
     printf("{\"check\":\"k_tx_g == k_tx_c (wire, wire_lens, status; random lengths, header-only, bad)\","
            "\"same\":%s}\n", ok ? "true" : "false");
     if (!ok) return 2;
+    CK(hipMemset(w2, 0x5c, G * n * slot));
+    CK(hipMemset(l2, 0x77, G * n * 2));
+    CK(hipMemset(s2, 0x33, G));
+    run_cl(a);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h2.data(), w2, h2.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hl2.data(), l2, G * n * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hs2.data(), s2, G, hipMemcpyDeviceToHost));
+    ok = h1 == h2 && hl1 == hl2 && hs1 == hs2;
+    printf("{\"check\":\"k_tx_c with the keystream in LDS == k_tx_c\",\"same\":%s}\n", ok ? "true" : "false");
+    if (!ok) return 2;
     for (int swz = 0; swz < 2; ++swz) {
       CK(hipMemset(w2, 0x5c, G * n * slot));
       CK(hipMemset(l2, 0x77, G * n * 2));
@@ -268,9 +282,9 @@ int main(int argc, char** argv) {
   int cnt = 0;
   std::vector<T> ts;
   ts.push_back({"k_tx_c (round 3 production)", [&] { run_c(rot[cnt++ % 3]); }, {}});
-  ts.push_back({"k_tx_g (one block per group)", [&] { run_g(rot[cnt++ % 3]); }, {}});
-  ts.push_back({"k_tx_o (one wire chunk per thread)", [&] { run_o(rot[cnt++ % 3], 0); }, {}});
-  ts.push_back({"k_tx_o, XCD-contiguous blocks", [&] { run_o(rot[cnt++ % 3], 1); }, {}});
+  ts.push_back({"k_tx_c, keystream staged in LDS per block", [&] { run_cl(rot[cnt++ % 3]); }, {}});
+  ts.push_back({"k_tx_c (round 3 production), again", [&] { run_c(rot[cnt++ % 3]); }, {}});
+  ts.push_back({"k_tx_c, keystream staged in LDS per block, again", [&] { run_cl(rot[cnt++ % 3]); }, {}});
   // the copy reads and writes the wire buffers (G*13*1488 B each): the data
   // packets alone (G*10*1488 B) are smaller than half the bytes moved
   if (copy16 * 16 > G * n * slot) return 3;

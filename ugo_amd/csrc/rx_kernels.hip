@@ -203,11 +203,15 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 //    a packet are issued before its first store (the per-pass load -> store
 //    chain of k_rx_scatter kept one 1-KiB load in flight per wave);
 //  * lengths are clamped to the slot.
-// MODE: 0 = production (aligned loads realigned by DPP); A/B only
-// (tools/rxgather.hip, profiles/r4/rxgather_{attribution,unaligned}_*): 1 =
-// without the presence atomics (timing only, -5 us), 2 = the same loads and
-// stores without the realignment (timing only, -20 us), 3 = unaligned payload
-// loads instead of the realignment (bit-exact, but +13 us: 522 vs 509).
+// MODE: 4 = production: aligned loads realigned with the right neighbour's
+// chunk, which lane l of a half takes from lane l+1 and lane 31 from lane 0's
+// next-pass chunk, all by one ds_bpermute (no neighbour loads; 492.7 / 490.5
+// vs 504.3 / 499.1 us in order / shuffled, profiles/r4/rxgather_bperm_*);
+// 0 = the round-3 form (DPP from lane l+1, lane 31 loads its neighbour).  A/B
+// only (tools/rxgather.hip, profiles/r4/rxgather_{attribution,unaligned}_*):
+// 1 = MODE 0 without the presence atomics (timing only, -5 us), 2 = the same
+// loads and stores without the realignment (timing only, -20 us), 3 =
+// unaligned payload loads instead of the realignment (bit-exact, +13 us).
 // NT: bit 0 nontemporal payload loads, bit 1 nontemporal stores.
 // RARE (A/B only, tools/rx_experiments.hpp full-grid path): 1 = a block adds
 // only its bad-flag / out-of-window / too-short counts to a.stats (the call's
@@ -295,6 +299,7 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
       }
       A[q] = o < lim ? ((NT & 1) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + o)) : ld16(pk + o))
                      : zero;
+      if (MODE == 4 && q + 1 < NP) continue;  // lane 31's neighbour is lane 0's next chunk
       if (hl == 31u && o + 16u < lim) {
         const u32x4 B = ld16(pk + o + 16u);
         bx[q] = B.x;
@@ -311,7 +316,25 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
       const u32x4 Aq = A[q] ^ K[q];  // bytes past lim are masked below
       // converged: neighbour's chunk (packet bytes [o+16, o+32)) by DPP
       uint32_t nx = 0u, ny = 0u;
-      if constexpr (MODE != 3) {
+      if constexpr (MODE == 4) {
+        if (q + 1 < NP) {
+          // lane l of a half takes lane l+1's chunk; lane 31 takes lane 0's
+          // chunk of the next pass (packet bytes [o+16, o+32)), which lane 0
+          // sends instead of its own: no neighbour load
+          const u32x4 An = A[q + 1 < NP ? q + 1 : q] ^ K[q + 1 < NP ? q + 1 : q];
+          const uint32_t sx = hl == 0u ? An.x : Aq.x, sy = hl == 0u ? An.y : Aq.y;
+          const int src = static_cast<int>(hl == 31u ? lane - 31u : lane + 1u) * 4;
+          nx = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(sx)));
+          ny = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(sy)));
+        } else {
+          nx = from_next_lane(Aq.x);
+          ny = from_next_lane(Aq.y);
+          if (hl == 31u) {
+            nx = bx[q] ^ kbx[q];
+            ny = by[q] ^ kby[q];
+          }
+        }
+      } else if constexpr (MODE != 3) {
         nx = from_next_lane(Aq.x);
         ny = from_next_lane(Aq.y);
         if (hl == 31u) {
@@ -356,7 +379,7 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
       }
     }
     if (hl == 0) {
-      if constexpr (MODE == 0 || MODE == 3)
+      if constexpr (MODE == 0 || MODE == 3 || MODE == 4)
         acct.issue(a, bstats, why, grp - a.first_group, row);
       else if (why < 5)
         atomicAdd(&bstats[why], 1u);
@@ -439,7 +462,10 @@ hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, h
 static inline uint32_t rx_blocks(const RxArgs& a) {
   const uint64_t waves = (a.npk + 1) / 2;
   uint64_t blocks = (waves + 3) / 4;
-  if (blocks > 2048u) blocks = 2048u;  // 8 workgroups per CU, grid-stride over packet pairs
+  // grid-stride over packet pairs; 8192 blocks (~12 packets per half-wave on
+  // the bench ring, each keeping its keystream chunks in registers) run 1-1.4%
+  // faster than 2048 (profiles/r4/rxgather_grid_*.jsonl, _bperm_*)
+  if (blocks > 8192u) blocks = 8192u;
   return static_cast<uint32_t>(blocks);
 }
 
@@ -457,11 +483,12 @@ hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
   const uint32_t passes = ((a.S + 15u) / 16u + 31u) / 32u;
   // nt loads + stores: on a cold ring and batch 493 vs 552 us with plain ones
   // (a linear copy of the same bytes: 487 us; tools/rxvariants 15 cold)
+  // MODE 4: the realignment's neighbour chunks by ds_bpermute, no neighbour loads
   switch (passes) {
-    case 1: launch(kKRx, k_rx_place<1, 0, 3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 2: launch(kKRx, k_rx_place<2, 0, 3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 3: launch(kKRx, k_rx_place<3, 0, 3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 4: launch(kKRx, k_rx_place<4, 0, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 1: launch(kKRx, k_rx_place<1, 4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 2: launch(kKRx, k_rx_place<2, 4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 3: launch(kKRx, k_rx_place<3, 4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 4: launch(kKRx, k_rx_place<4, 4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
     default: launch(kKRx, k_rx_scatter, dim3(blocks), dim3(256), 0, s, a); break;
   }
   return hipGetLastError();

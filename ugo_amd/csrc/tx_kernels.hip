@@ -20,6 +20,7 @@
 // zeros).  DESIGN.md §2 states this contract.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "gf_device.hpp"
@@ -79,8 +80,8 @@ struct TxItem {
 // SL (even DN == d only): the lengths are read with scalar loads for the two
 // groups a wave can span (>= 64 chunks per group) and picked per lane, instead
 // of one broadcast vector load per packet per wave.
-template <int DN, int NT, bool SL>
-__device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x) {
+template <int DN, int NT, bool SL, bool PL = false>
+__device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x, const u32x4* padl = nullptr) {
   TxItem t{};
   const uint64_t gl = item / a.chunks;
   const uint32_t m = item - static_cast<uint32_t>(gl) * a.chunks;
@@ -129,7 +130,12 @@ __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x)
   t.live = t.o < maxsz;
   t.seq0 = static_cast<uint32_t>((uint64_t(a.first_seq) + t.g * n) % a.paws);
   if (!t.live) return t;
-  t.padc = a.pad ? load16<0>(a.pad + t.o) : V4{{0u, 0u, 0u, 0u}};
+  if constexpr (PL) {  // the block's LDS copy of the keystream
+    const u32x4 v = padl[m];
+    t.padc = V4{{v.x, v.y, v.z, v.w}};
+  } else {
+    t.padc = a.pad ? load16<0>(a.pad + t.o) : V4{{0u, 0u, 0u, 0u}};
+  }
   const uint8_t* src = a.pkts + t.g * a.d * a.slot_in + t.o;
   uint8_t* dst = a.wire + t.g * n * a.slot_out + t.o;
   // all loads first: the stores below may alias the packets as far as the
@@ -193,12 +199,19 @@ __device__ __forceinline__ bool tx_no_window(const TxArgs& a, const TxItem& t) {
 }
 
 // (10,3) / (32,8): the compile-time XOR networks of k_encode_c.
-template <int D, int P, int NT = kTxNT, bool SL = kTxSL>
+// PL: the keystream staged once per block in dynamic LDS (needs a.pad and
+// 16 * chunks bytes of dynamic LDS), instead of one 16-B global load per thread.
+template <int D, int P, int NT = kTxNT, bool SL = kTxSL, bool PL = false>
 __global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  extern __shared__ u32x4 padl[];
+  if constexpr (PL) {
+    for (uint32_t i = threadIdx.x; i < a.chunks; i += 256u) padl[i] = *reinterpret_cast<const u32x4*>(a.pad + 16u * i);
+    __syncthreads();
+  }
   if (item >= a.groups * a.chunks) return;
   V4 x[D];
-  const TxItem t = tx_data<D, NT, SL>(a, item, x);
+  const TxItem t = tx_data<D, NT, SL, PL>(a, item, x, padl);
   if (!t.live || tx_no_window(a, t)) return;
   tx_cparity<D, P, NT>(a, t, x, std::make_integer_sequence<int, P>{});
   if (t.o == 0 && a.status) a.status[t.g] = 0;
@@ -255,10 +268,24 @@ hipError_t launch_tx_assemble(int dmax, const TxArgs& a, hipStream_t s) {
     case 0: {
       // scalar lengths need a wave to span at most 2 groups: >= 64 chunks per packet
       const bool sl = kTxSL && a.chunks >= 64;
-      if (a.d == 10 && a.p == 3 && sl)
+      // with a keystream, each block stages it in LDS once (16 B per chunk;
+      // the (10,3) kernel's residency cap already allocates far more): 424 vs
+      // 439-445 us, one global load less per thread (tools/txgroup.hip,
+      // profiles/r4/txgroup_pad_lds.jsonl)
+      const uint32_t padl = 16u * a.chunks;
+      const uint32_t cap = std::max(tx_lds_cap(), padl);
+      if (a.d == 10 && a.p == 3 && a.pad && sl)
+        launch(kKTx, k_tx_c<10, 3, kTxNT, true, true>, grid, block, cap, s, a);
+      else if (a.d == 10 && a.p == 3 && a.pad)
+        launch(kKTx, k_tx_c<10, 3, kTxNT, false, true>, grid, block, cap, s, a);
+      else if (a.d == 10 && a.p == 3 && sl)
         launch(kKTx, k_tx_c<10, 3, kTxNT, true>, grid, block, tx_lds_cap(), s, a);
       else if (a.d == 10 && a.p == 3)
         launch(kKTx, k_tx_c<10, 3, kTxNT, false>, grid, block, tx_lds_cap(), s, a);
+      else if (a.d == 32 && a.p == 8 && a.pad && sl)
+        launch(kKTx, k_tx_c<32, 8, kTxNT, true, true>, grid, block, padl, s, a);
+      else if (a.d == 32 && a.p == 8 && a.pad)
+        launch(kKTx, k_tx_c<32, 8, kTxNT, false, true>, grid, block, padl, s, a);
       else if (a.d == 32 && a.p == 8 && sl)
         launch(kKTx, k_tx_c<32, 8, kTxNT, true>, grid, block, 0, s, a);
       else if (a.d == 32 && a.p == 8)
