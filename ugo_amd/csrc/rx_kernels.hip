@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 //    a packet are issued before its first store (the per-pass load -> store
 //    chain of k_rx_scatter kept one 1-KiB load in flight per wave);
 //  * lengths are clamped to the slot.
-// MODE: 4 = production: aligned loads realigned with the right neighbour's
+// (Production is k_rx_place_h below.)  MODE: 4 = aligned loads realigned with the right neighbour's
 // chunk, which lane l of a half takes from lane l+1 and lane 31 from lane 0's
 // next-pass chunk, all by one ds_bpermute (no neighbour loads; 492.7 / 490.5
 // vs 504.3 / 499.1 us in order / shuffled, profiles/r4/rxgather_bperm_*);
@@ -393,6 +393,143 @@ __global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
   }
 }
 
+// k_rx_place with the header taken from the payload's own first chunk: lane 0
+// of a half loads packet bytes [0, 16) as part of the payload anyway, so the
+// header and flag come to the other lanes by ds_bpermute instead of a separate
+// (prefetched) header load: one memory instruction less per packet pair
+// (468.6 / 489.8 vs 476.4 / 494.9 us, profiles/r4/rxgather_hdr_*).  Loading
+// the lengths 32 iterations at a time as well gains nothing measurable
+// (rxgather_lenbatch_*).  Production.
+// Every lane loads the bytes [0, min(len, S + 6)) of its packet before the
+// header is known (a packet later rejected for its flag or window is loaded
+// and dropped, like a duplicate).  Realignment as MODE 4.
+template <int NP, int NT = 3>
+__global__ __launch_bounds__(256) void k_rx_place_h(RxArgs a) {
+  if (rx_gated_off(a)) return;
+  __shared__ uint32_t bstats[5];
+  if (threadIdx.x < 5) bstats[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, hl = lane & 31u;
+  const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
+  const uint64_t nwaves = (gridDim.x * 256ull) >> 6;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  const bool chk_prev = a.prev && !(a.seen && *a.seen < a.call);
+  u32x4 K[NP];
+  uint32_t kbx = 0u, kby = 0u;  // keystream of lane 31's last-pass neighbour chunk
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const uint32_t o = 16u * (32u * q + hl);
+    K[q] = (a.pad && o + 16u <= slot) ? ld16(a.pad + o) : zero;
+    if (q == NP - 1 && a.pad && hl == 31u && o + 32u <= slot) {
+      const u32x4 B = ld16(a.pad + o + 16u);
+      kbx = B.x;
+      kby = B.y;
+    }
+  }
+  RxAccount acct;
+  const uint64_t first = 2 * wave, step = 2 * nwaves, end = a.npk;
+  const int hsrc = static_cast<int>(half * 32u) * 4;  // lane 0 of this half
+  uint64_t i = first + half;
+  uint32_t ln = i < end ? a.lens[i] : 0u;
+  for (uint64_t base = first; base < end; base += step, i += step) {
+    const bool have = i < end;
+    const uint8_t* pk = a.wire + i * a.slot;
+    const uint32_t len = have ? min(ln, slot) : 0u;
+    if (i + step < end) ln = a.lens[i + step];  // the next packet's length
+    const uint32_t lim = len >= 6u ? min(len, a.S + 6u) : 0u;  // packet bytes [0, lim) may be kept
+    u32x4 A[NP];
+    uint32_t bx = 0u, by = 0u;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      A[q] = o < lim ? ((NT & 1) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + o)) : ld16(pk + o))
+                     : zero;
+      if (q == NP - 1 && hl == 31u && o + 16u < lim) {
+        const u32x4 B = ld16(pk + o + 16u);
+        bx = B.x;
+        by = B.y;
+      }
+    }
+    const u32x4 A0 = A[0] ^ K[0];  // lane 0: packet bytes [0, 16) = the header
+    const uint32_t seqid = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(hsrc, static_cast<int>(A0.x)));
+    const uint32_t flag = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(hsrc, static_cast<int>(A0.y))) & 0xffffu;
+    uint32_t why = 0;  // 0 = accept, else stats slot (5: no packet)
+    if (!have) why = 5;
+    else if (len < 6u) why = 3;
+    else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
+    const uint32_t row = seqid % a.n;
+    const uint64_t grp = seqid / a.n;
+    if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
+    const bool acc = why == 0;
+    uint32_t claim = static_cast<uint32_t>(i);
+    if (acc && a.win) claim = a.win[(grp - a.first_group) * a.n + row];
+    uint64_t before = 0;
+    if (acc && chk_prev) before = a.prev[grp - a.first_group];
+    const uint32_t L = acc ? min(len - 6u, a.S) : 0u;  // payload bytes kept
+    if (acc && claim != static_cast<uint32_t>(i)) why = 4;  // a later copy of a claimed seqid
+    if (acc && ((before >> row) & 1ull)) why = 4;           // a copy of an earlier call's seqid
+    const bool ok = why == 0;
+    uint8_t* dst = a.shards + row * a.rstride + (grp - a.first_group) * a.gstride;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      const u32x4 Aq = A[q] ^ K[q];
+      uint32_t nx, ny;
+      if (q + 1 < NP) {  // lane l takes lane l+1's chunk, lane 31 lane 0's next-pass chunk
+        const u32x4 An = A[q + 1 < NP ? q + 1 : q] ^ K[q + 1 < NP ? q + 1 : q];
+        const uint32_t sx = hl == 0u ? An.x : Aq.x, sy = hl == 0u ? An.y : Aq.y;
+        const int src = static_cast<int>(hl == 31u ? lane - 31u : lane + 1u) * 4;
+        nx = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(sx)));
+        ny = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(sy)));
+      } else {
+        nx = from_next_lane(Aq.x);
+        ny = from_next_lane(Aq.y);
+        if (hl == 31u) {
+          nx = bx ^ kbx;
+          ny = by ^ kby;
+        }
+      }
+      if (!ok || o >= a.S) continue;
+      uint32_t w[4];
+      w[0] = __builtin_amdgcn_alignbyte(Aq.z, Aq.y, 2);  // payload bytes [o, o+16) = packet bytes [o+6, o+22)
+      w[1] = __builtin_amdgcn_alignbyte(Aq.w, Aq.z, 2);
+      w[2] = __builtin_amdgcn_alignbyte(nx, Aq.w, 2);
+      w[3] = __builtin_amdgcn_alignbyte(ny, nx, 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
+        const uint32_t b0 = o + 4u * j;
+        const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
+        w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+      }
+      const uint32_t nb = a.S - o;
+      if (nb >= 16u) {
+        const u32x4 v = {w[0], w[1], w[2], w[3]};
+        if constexpr (NT & 2)
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + o));
+        else
+          *reinterpret_cast<u32x4*>(dst + o) = v;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t lo = 4u * j;
+          if (nb >= lo + 4u) {
+            *reinterpret_cast<uint32_t*>(dst + o + lo) = w[j];
+          } else if (nb > lo) {
+            for (uint32_t t = 0; t < nb - lo; ++t) dst[o + lo + t] = static_cast<uint8_t>(w[j] >> (8u * t));
+          }
+        }
+      }
+    }
+    if (hl == 0) acct.issue(a, bstats, why, grp - a.first_group, row);
+  }
+  if (hl == 0) acct.settle(a, bstats);
+  if (a.stats) {
+    __syncthreads();
+    if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+  }
+}
+
 // First-arrival claim: one thread per packet reads its 8 header bytes (seqid,
 // flag), classifies it exactly as the place kernels do, and takes the
 // smallest index per (group, row).  ~8 B read per 1.5-KB packet.
@@ -483,12 +620,13 @@ hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
   const uint32_t passes = ((a.S + 15u) / 16u + 31u) / 32u;
   // nt loads + stores: on a cold ring and batch 493 vs 552 us with plain ones
   // (a linear copy of the same bytes: 487 us; tools/rxvariants 15 cold)
-  // MODE 4: the realignment's neighbour chunks by ds_bpermute, no neighbour loads
+  // the header from the payload's first chunk, the realignment's neighbour
+  // chunks by ds_bpermute: no header or neighbour loads
   switch (passes) {
-    case 1: launch(kKRx, k_rx_place<1, 4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 2: launch(kKRx, k_rx_place<2, 4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 3: launch(kKRx, k_rx_place<3, 4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 4: launch(kKRx, k_rx_place<4, 4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 1: launch(kKRx, k_rx_place_h<1, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 2: launch(kKRx, k_rx_place_h<2, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 3: launch(kKRx, k_rx_place_h<3, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 4: launch(kKRx, k_rx_place_h<4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
     default: launch(kKRx, k_rx_scatter, dim3(blocks), dim3(256), 0, s, a); break;
   }
   return hipGetLastError();
