@@ -155,6 +155,9 @@ int main(int argc, char** argv) {
   auto run_cl = [&](TxArgs a) {
     k_tx_c<10, 3, kTxNT, true, true><<<static_cast<uint32_t>((a.groups * a.chunks + 255) / 256), 256, tx_lds_cap()>>>(a);
   };
+  auto run_cl_cap = [&](TxArgs a, uint32_t lds) {
+    k_tx_c<10, 3, kTxNT, true, true><<<static_cast<uint32_t>((a.groups * a.chunks + 255) / 256), 256, lds>>>(a);
+  };
   auto run_g = [&](TxArgs a) { k_tx_g<10, 3><<<static_cast<uint32_t>(a.groups), 256, lds>>>(a); };
   auto run_o = [&](TxArgs a, int swz) {
     const uint32_t blocks = static_cast<uint32_t>((a.groups * 13 * a.chunks + 255) / 256);
@@ -283,6 +286,9 @@ int main(int argc, char** argv) {
   std::vector<T> ts;
   ts.push_back({"k_tx_c (round 3 production)", [&] { run_c(rot[cnt++ % 3]); }, {}});
   ts.push_back({"k_tx_c, keystream staged in LDS per block", [&] { run_cl(rot[cnt++ % 3]); }, {}});
+  ts.push_back({"k_tx_c LDS keystream, 3 blocks/CU (52 KiB LDS)", [&] { run_cl_cap(rot[cnt++ % 3], 52u * 1024u); }, {}});
+  ts.push_back({"k_tx_c LDS keystream, 4 blocks/CU (39 KiB LDS)", [&] { run_cl_cap(rot[cnt++ % 3], 39u * 1024u); }, {}});
+  ts.push_back({"k_tx_c LDS keystream, 1 block/CU (100 KiB LDS)", [&] { run_cl_cap(rot[cnt++ % 3], 100u * 1024u); }, {}});
   ts.push_back({"k_tx_c (round 3 production), again", [&] { run_c(rot[cnt++ % 3]); }, {}});
   ts.push_back({"k_tx_c, keystream staged in LDS per block, again", [&] { run_cl(rot[cnt++ % 3]); }, {}});
   // the copy reads and writes the wire buffers (G*13*1488 B each): the data
