@@ -178,7 +178,7 @@ def test_rx_assemble_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_gro
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("encrypt,S,slot", [(True, 1470, 1488), (False, 1470, 1488), (True, 3000, 3024)])
+@pytest.mark.parametrize("encrypt,S,slot", [(True, 1470, 1488), (False, 1470, 1488), (True, 2000, 2016), (True, 3000, 3024)])
 def test_rx_assemble_first_copy_wins(gpu, encrypt, S, slot):
     """Repeated seqids with DIFFERENT payloads and lengths (a replayed or
     corrupted packet with a valid header): the first copy in ring order is the
