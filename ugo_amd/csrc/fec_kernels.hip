@@ -739,6 +739,7 @@ struct SvcLds {
   uint32_t mult[256][5];                         // split tables of every coefficient
   uint32_t desc[kSvcMaxGroups + 1][kSvcDescWords];
   uint32_t t[kSvcMaxGroups + 1][4][DMAX][5];     // per slot: tables of every (output, input) product
+  u32x4 rows[DMAX][128];                         // one-group requests: the survivors' chunks
 };
 
 template <int DMAX>
@@ -782,6 +783,9 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
   svc_expand(L, ENC, a, threadIdx.x, kSvcThreads);
   uint32_t last = sa.start_seq;
   uint64_t t0 = wall_clock64();
+#ifdef UGO_SVC_TRACE
+  uint64_t tr[6] = {0, 0, 0, 0, 0, 0};
+#endif
   for (;;) {
     if (wv == 0) {
       // wave 0 polls the whole request line: lanes 0-3 one 16-B piece each
@@ -801,6 +805,9 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
         __builtin_amdgcn_s_sleep(UGO_SVC_SLEEP);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#ifdef UGO_SVC_TRACE
+      tr[0] = wall_clock64();
+#endif
       if (lane < 4u) {
         if (lane == 0 && stop) v.y = kSvcStop;
         line[lane] = v;
@@ -816,6 +823,9 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
       }
     }
     __syncthreads();
+#ifdef UGO_SVC_TRACE
+    tr[1] = wall_clock64();
+#endif
     const uint32_t* rq = reinterpret_cast<const uint32_t*>(line);
     const uint32_t sq = rq[0], op = rq[1];
     if (op != kSvcEncode && op != kSvcReconstruct) break;
@@ -839,8 +849,86 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
       __syncthreads();
     }
     const uint32_t chunks = (S + 15u) / 16u, cpad = (chunks + 63u) & ~63u;
+    // A one-group request (ugo's per-group calls: 1470-B rows, 2 slices of 64
+    // chunks) would leave 6 of the 8 waves idle while each busy wave folds
+    // every output -- the fold was half the device time (tools/svc_trace.cpp).
+    // Instead all waves load the survivors' (row, slice) pieces into LDS, then
+    // each wave folds ONE output of one slice.
+    constexpr uint32_t kWaves = kSvcThreads / 64u;
+    // (with one output the fold is short and the staging would only add its
+    // LDS round trip: 7.7 vs 7.2 us per 1-loss Reconstruct, so e >= 2 only)
+    bool one = false;
+    if (G == 1u && cpad <= 128u) {
+      const uint32_t hdr = __builtin_amdgcn_readfirstlane(L.desc[recon ? 0u : ENC][0]);
+      const uint32_t e = (hdr >> 16) & 0xffu ? 0u : (data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu));
+      one = e >= 2u;
+    }
+    if (one) {
+      const uint32_t slices = cpad / 64u;
+      const uint32_t slot = recon ? 0u : ENC;
+      const uint32_t* dw = L.desc[slot];
+      const uint32_t hdr = __builtin_amdgcn_readfirstlane(dw[0]);
+      const uint32_t e = data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);  // status 0: e >= 2 above
+      if (recon && threadIdx.x == 0) *(g_u8*)(&box->status[0]) = 0;
+      {  // block-uniform
+        // every (row, slice) piece by one wave; a wave's pieces all in flight at once
+        constexpr uint32_t kPer = (2u * DMAX + kWaves - 1u) / kWaves;
+        V4 v[kPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+          const uint32_t rs = wv + j * kWaves, k = rs / slices, sl = rs - k * slices, c = sl * 64u + lane;
+          v[j] = V4{{0u, 0u, 0u, 0u}};
+          if (rs < a.d * slices && c < chunks) {
+            const uint32_t r = (__builtin_amdgcn_readfirstlane(dw[1u + (k >> 2)]) >> (8u * (k & 3u))) & 0xffu;
+            v[j] = gload16(base + static_cast<uint64_t>(c) * 16u + static_cast<uint64_t>(r) * pitch);
+          }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) {
+          const uint32_t rs = wv + j * kWaves, k = rs / slices, sl = rs - k * slices;
+          if (rs < a.d * slices) L.rows[k][sl * 64u + lane] = u32x4{v[j].v[0], v[j].v[1], v[j].v[2], v[j].v[3]};
+        }
+        __syncthreads();
+#ifdef UGO_SVC_TRACE
+        tr[2] = wall_clock64();
+#endif
+        const uint32_t sl = wv >> 2, osel = wv & 3u;
+        if (sl < slices && osel < e) {
+          const uint32_t c = sl * 64u + lane;
+          V4 x[DMAX];
+#pragma unroll
+          for (int k = 0; k < DMAX; ++k) {
+            x[k] = V4{{0u, 0u, 0u, 0u}};
+            if (k < static_cast<int>(a.d)) {
+              const u32x4 v = L.rows[k][c];
+              x[k] = V4{{v.x, v.y, v.z, v.w}};
+            }
+          }
+          V4 y1 = V4{{0u, 0u, 0u, 0u}};
+#pragma unroll
+          for (int k = 0; k < DMAX; k += 2) {
+            if (k >= static_cast<int>(a.d)) continue;
+            uint32_t s0[4], s1[4], s2[4], r0[4], r1[4], r2[4];
+            p_sel(x[k], s0, s1, s2);
+            p_sel(x[k + 1], r0, r1, r2);
+            const uint32_t* t = L.t[slot][osel][k];
+            const uint32_t* u = L.t[slot][osel][k + 1];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              uint32_t y = xor3(y1.v[j], perm(t[1], t[0], s0[j]), perm(t[3], t[2], s1[j]));
+              y = xor3(y, perm(0u, t[4], s2[j]), perm(u[1], u[0], r0[j]));
+              y1.v[j] = xor3(y, perm(u[3], u[2], r1[j]), perm(0u, u[4], r2[j]));
+            }
+          }
+          const uint32_t orows = __builtin_amdgcn_readfirstlane(dw[(4u + a.dpad) / 4u]);
+          if (c < chunks)
+            gstore16(base + static_cast<uint64_t>(c) * 16u + static_cast<uint64_t>((orows >> (8u * osel)) & 0xffu) * pitch,
+                     y1, S - c * 16u);
+        }
+      }
+    }
     // groups wave-aligned: wave w takes 64 chunks of one group at a time
-    for (uint32_t w0 = wv * 64u; w0 < G * cpad; w0 += kSvcThreads) {
+    for (uint32_t w0 = wv * 64u; !one && w0 < G * cpad; w0 += kSvcThreads) {
       const uint32_t g = w0 / cpad;
       const uint32_t c = w0 - g * cpad + lane;
       const uint32_t slot = recon ? g : ENC;
@@ -858,6 +946,7 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
         const uint32_t r = (__builtin_amdgcn_readfirstlane(dw[1 + (k >> 2)]) >> (8 * (k & 3))) & 0xffu;
         if (k < static_cast<int>(a.d) && c < chunks) x[k] = gload16(gp + static_cast<uint64_t>(r) * pitch);
       }
+      const uint32_t orows = __builtin_amdgcn_readfirstlane(dw[(4u + a.dpad) / 4u]);
       V4 acc[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[i] = V4{{0u, 0u, 0u, 0u}};
@@ -881,7 +970,6 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
         }
       }
       if (c < chunks) {
-        const uint32_t orows = __builtin_amdgcn_readfirstlane(dw[(4u + a.dpad) / 4u]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           if (i >= static_cast<int>(e)) continue;
@@ -890,8 +978,19 @@ __global__ __launch_bounds__(kSvcThreads) void k_service(SvcArgs sa) {
         }
       }
     }
+#ifdef UGO_SVC_TRACE
+    tr[3] = wall_clock64();
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
+#ifdef UGO_SVC_TRACE
+    tr[4] = wall_clock64();
+#endif
     __syncthreads();
+#ifdef UGO_SVC_TRACE
+    tr[5] = wall_clock64();
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 6; ++k) *(volatile __attribute__((address_space(1))) uint64_t*)(&box->trace[k]) = tr[k];
+#endif
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __hip_atomic_store(&box->done, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -89,6 +89,9 @@ struct SvcBox {
   alignas(64) uint32_t done;                     // device -> host
   uint32_t alive;
   int8_t status[kSvcMaxGroups];
+#ifdef UGO_SVC_TRACE  // A/B builds only (tools/svc_trace.cpp): wall-clock ticks of a request's phases
+  alignas(64) uint64_t trace[8];
+#endif
 };
 enum : uint32_t { kSvcEncode = 1, kSvcReconstruct = 2, kSvcStop = 3 };
 struct SvcArgs {

@@ -1229,6 +1229,14 @@ int ugo_fec_service_config(ugo_fec* c, unsigned timeout_ms, unsigned grace_ms, u
 
 int ugo_fec_poisoned(const ugo_fec* c) { return c && c->poisoned ? 1 : 0; }
 
+#ifdef UGO_SVC_TRACE  // A/B builds only (tools/svc_trace.cpp): the last request's phase ticks
+int ugo_fec_svc_trace(const ugo_fec* c, uint64_t* out) {
+  if (!c || !c->svc_box || !out) return UGO_FEC_ERR_INVALID_ARG;
+  for (int k = 0; k < 6; ++k) out[k] = reinterpret_cast<volatile const uint64_t*>(c->svc_box->trace)[k];
+  return UGO_FEC_OK;
+}
+#endif
+
 int ugo_fec_encode_host(ugo_fec* c, uint8_t* shards, size_t groups, size_t S, size_t pitch) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
   if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
