@@ -210,8 +210,9 @@ int main(int argc, char** argv) {
     uint32_t grid;
   };
   std::vector<Var> vars = {
-      {"production (round 4): begin(+claim fill, fresh flag) + k_rx_place_h (8192 blocks) + gated claim/re-place", PROD, 0, 0, 0},
+      {"production (round 4): begin(+claim fill, fresh flag) + k_rx_place_h (16384 blocks) + gated claim/re-place", PROD, 0, 0, 0},
       {"round-4 second form: k_rx_place MODE 4 (ds_bpermute realignment, header load), 8192 blocks", PROD, 7, 0, 0},
+      {"production kernel, 8192 blocks", PROD, 0, 0, 8192},
       {"production (round 3): begin + place (MODE 0, 2048 blocks) + gated fill/claim/re-place", PROD_OLD, 0, 0, 2048},
       {"chunk path: begin + chunk (one output chunk per thread) + count + gated claim/re-place", CHUNK, 0, 0, 0},
       {"full-grid place: begin + zero rare + place (one packet per half-wave, npk/8 blocks) + tally + gated claim/re-place", FULL, 0, 0, 0},

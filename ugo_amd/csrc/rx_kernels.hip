@@ -599,10 +599,12 @@ hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, h
 static inline uint32_t rx_blocks(const RxArgs& a) {
   const uint64_t waves = (a.npk + 1) / 2;
   uint64_t blocks = (waves + 3) / 4;
-  // grid-stride over packet pairs; 8192 blocks (~12 packets per half-wave on
-  // the bench ring, each keeping its keystream chunks in registers) run 1-1.4%
-  // faster than 2048 (profiles/r4/rxgather_grid_*.jsonl, _bperm_*)
-  if (blocks > 8192u) blocks = 8192u;
+  // grid-stride over packet pairs; 16384 blocks (~6 packets per half-wave on
+  // the bench ring, each keeping its keystream chunks in registers): with
+  // k_rx_place_h 0.3-1.5% faster than 8192 on two boxes and 2.5% faster than
+  // 4096, 32768 no better (profiles/r4/rxgather_hgrid_*.jsonl, _g16k_*; _grid_*
+  // for the earlier form)
+  if (blocks > 16384u) blocks = 16384u;
   return static_cast<uint32_t>(blocks);
 }
 
