@@ -219,12 +219,17 @@ __global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
 
 // Any other geometry: coefficients from the encode descriptor (uniform, so
 // the coefficient words are scalar loads), masked Horner per parity row.
-template <int DMAX>
+template <int DMAX, bool PL = false>
 __global__ __launch_bounds__(256) void k_tx_var(TxArgs a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  extern __shared__ u32x4 padl[];
+  if constexpr (PL) {  // the keystream staged once per block (as k_tx_c)
+    for (uint32_t i = threadIdx.x; i < a.chunks; i += 256u) padl[i] = *reinterpret_cast<const u32x4*>(a.pad + 16u * i);
+    __syncthreads();
+  }
   if (item >= a.groups * a.chunks) return;
   V4 x[DMAX];
-  const TxItem t = tx_data<DMAX, kTxNT, false>(a, item, x);
+  const TxItem t = tx_data<DMAX, kTxNT, false, PL>(a, item, x, padl);
   if (!t.live || tx_no_window(a, t)) return;
   constexpr int NW = (DMAX + 3) / 4;
   const uint32_t cbase = 4 + a.dpad + a.epad;
@@ -294,13 +299,21 @@ hipError_t launch_tx_assemble(int dmax, const TxArgs& a, hipStream_t s) {
         return hipErrorInvalidValue;
       break;
     }
-    case 4: launch(kKTx, k_tx_var<4>, grid, block, 0, s, a); break;
-    case 8: launch(kKTx, k_tx_var<8>, grid, block, 0, s, a); break;
-    case 10: launch(kKTx, k_tx_var<10>, grid, block, 0, s, a); break;
-    case 12: launch(kKTx, k_tx_var<12>, grid, block, 0, s, a); break;
-    case 16: launch(kKTx, k_tx_var<16>, grid, block, 0, s, a); break;
-    case 24: launch(kKTx, k_tx_var<24>, grid, block, 0, s, a); break;
-    case 32: launch(kKTx, k_tx_var<32>, grid, block, 0, s, a); break;
+#define UGO_TX_VAR(DM)                                                                   \
+  case DM:                                                                               \
+    if (a.pad)                                                                           \
+      launch(kKTx, k_tx_var<DM, true>, grid, block, 16u * a.chunks, s, a);               \
+    else                                                                                 \
+      launch(kKTx, k_tx_var<DM>, grid, block, 0, s, a);                                  \
+    break;
+    UGO_TX_VAR(4)
+    UGO_TX_VAR(8)
+    UGO_TX_VAR(10)
+    UGO_TX_VAR(12)
+    UGO_TX_VAR(16)
+    UGO_TX_VAR(24)
+    UGO_TX_VAR(32)
+#undef UGO_TX_VAR
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
