@@ -1,6 +1,7 @@
 // A/B timing of jumbo (32+8)x9000 kernel variants, planar layout, 8192 groups.
 // Not product code: includes the kernel TU.  One JSON line per variant.
 #include "../ugo_amd/csrc/fec_kernels.hip"
+#include "fec_experiments.hpp"
 
 #include <algorithm>
 #include <cstdio>

@@ -12,6 +12,7 @@
 // Round-3 results: profiles/r3/qaprobe_r3m.jsonl (DESIGN_HISTORY.md §3.4 "Jumbo floor").
 // Not product code: it includes the kernel TU to instantiate the variants.
 #include "../ugo_amd/csrc/fec_kernels.hip"
+#include "fec_experiments.hpp"
 
 #include <algorithm>
 #include <cstdio>

@@ -14,6 +14,206 @@
 namespace ugo {
 namespace kern {
 
+// Loads-first form for rows of at most 32 * NP chunks (NP = 3 for ugo's
+// 1470-B payloads).  Same decomposition (half a wave per packet), but:
+//  * the keystream chunks at a lane's offsets are the same for every packet,
+//    so they are loaded once and held in registers;
+//  * the next packet's header and length are prefetched, so a packet's
+//    placement is known before its payload arrives, and all NP payload loads of
+//    a packet are issued before its first store (the per-pass load -> store
+//    chain of k_rx_scatter kept one 1-KiB load in flight per wave);
+//  * lengths are clamped to the slot.
+// (Production is k_rx_place_h in ugo_amd/csrc/rx_kernels.hip.)  MODE: 4 = aligned loads realigned with the right neighbour's
+// chunk, which lane l of a half takes from lane l+1 and lane 31 from lane 0's
+// next-pass chunk, all by one ds_bpermute (no neighbour loads; 492.7 / 490.5
+// vs 504.3 / 499.1 us in order / shuffled, profiles/r4/rxgather_bperm_*);
+// 0 = the round-3 form (DPP from lane l+1, lane 31 loads its neighbour).  A/B
+// only (tools/rxgather.hip, profiles/r4/rxgather_{attribution,unaligned}_*):
+// 1 = MODE 0 without the presence atomics (timing only, -5 us), 2 = the same
+// loads and stores without the realignment (timing only, -20 us), 3 =
+// unaligned payload loads instead of the realignment (bit-exact, +13 us).
+// NT: bit 0 nontemporal payload loads, bit 1 nontemporal stores.
+// RARE (A/B only, tools/rx_experiments.hpp full-grid path): 1 = a block adds
+// only its bad-flag / out-of-window / too-short counts to a.stats (the call's
+// scratch counters; accepted and duplicates are tallied from the presence bits
+// afterwards).  The full grid lost: 712 vs 500 us.
+template <int NP, int MODE = 0, int NT = 0, int RARE = 0>
+__global__ __launch_bounds__(256) void k_rx_place(RxArgs a) {
+  if (rx_gated_off(a)) return;
+  __shared__ uint32_t bstats[5];
+  if (threadIdx.x < 5) bstats[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, hl = lane & 31u;
+  const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
+  const uint64_t nwaves = (gridDim.x * 256ull) >> 6;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  const u32x4 K0 = a.pad ? ld16(a.pad) : zero;  // keystream over the header chunk
+  // a batch with no presence bit at call entry (the usual case: one call per
+  // batch) has nothing an earlier call placed: no per-packet snapshot lookup
+  const bool chk_prev = a.prev && !(a.seen && *a.seen < a.call);
+  u32x4 K[NP];
+  uint32_t kbx[NP], kby[NP];  // keystream of the neighbour chunk (lane 31 of a half)
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const uint32_t o = 16u * (32u * q + hl);
+    kbx[q] = kby[q] = 0u;
+    if constexpr (MODE == 3) {  // keystream at the payload's offsets, unaligned
+      K[q] = (a.pad && o + 22u <= slot) ? ldu16<false>(a.pad + 6u + o) : zero;
+      continue;
+    }
+    K[q] = (a.pad && o + 16u <= slot) ? ld16(a.pad + o) : zero;
+    if (a.pad && hl == 31u && o + 32u <= slot) {
+      const u32x4 B = ld16(a.pad + o + 16u);
+      kbx[q] = B.x;
+      kby[q] = B.y;
+    }
+  }
+  RxAccount acct;
+  // grid-stride over packet pairs
+  const uint64_t first = 2 * wave, step = 2 * nwaves, end = a.npk;
+  uint64_t i = first + half;
+  u32x4 hn = zero;
+  uint32_t ln = 0;
+  if (i < end) {
+    hn = ld16(a.wire + i * a.slot);
+    ln = a.lens[i];
+  }
+  for (uint64_t base = first; base < end; base += step, i += step) {
+    const bool have = i < end;
+    const uint8_t* pk = a.wire + i * a.slot;
+    const u32x4 h = hn ^ K0;
+    const uint32_t len = have ? min(ln, slot) : 0u;
+    const uint64_t inext = i + step;
+    if (inext < end) {  // prefetch the next packet's header and length
+      hn = ld16(a.wire + inext * a.slot);
+      ln = a.lens[inext];
+    }
+    const uint32_t seqid = h.x;
+    const uint32_t flag = h.y & 0xffffu;
+    uint32_t why = 0;  // 0 = accept, else stats slot (5: no packet)
+    if (!have) why = 5;
+    else if (len < 6u) why = 3;
+    else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
+    const uint32_t row = seqid % a.n;
+    const uint64_t grp = seqid / a.n;
+    if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
+    const bool acc = why == 0;
+    // first copy in ring order?  The claim word is loaded before the payload and
+    // only waited for at the stores (a duplicate's payload is loaded, then dropped)
+    uint32_t claim = static_cast<uint32_t>(i);
+    if (acc && a.win) claim = a.win[(grp - a.first_group) * a.n + row];
+    uint64_t before = 0;  // presence at call entry: set = an earlier call placed this seqid
+    if (acc && chk_prev) before = a.prev[grp - a.first_group];
+    const uint32_t L = acc ? min(len - 6u, a.S) : 0u;  // payload bytes kept
+    const uint32_t lim = acc ? L + 6u : 0u;            // packet bytes [0, lim) are needed
+    u32x4 A[NP];
+    uint32_t bx[NP], by[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      bx[q] = by[q] = 0u;
+      if constexpr (MODE == 3) {  // payload bytes [o, o+16) directly (host: 16*floor((S-1)/16) + 22 <= slot)
+        A[q] = o < L ? ldu16<(NT & 1) != 0>(pk + 6u + o) : zero;
+        continue;
+      }
+      A[q] = o < lim ? ((NT & 1) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + o)) : ld16(pk + o))
+                     : zero;
+      if (MODE == 4 && q + 1 < NP) continue;  // lane 31's neighbour is lane 0's next chunk
+      if (hl == 31u && o + 16u < lim) {
+        const u32x4 B = ld16(pk + o + 16u);
+        bx[q] = B.x;
+        by[q] = B.y;
+      }
+    }
+    if (acc && claim != static_cast<uint32_t>(i)) why = 4;  // a later copy of a claimed seqid
+    if (acc && ((before >> row) & 1ull)) why = 4;           // a copy of an earlier call's seqid
+    const bool ok = why == 0;
+    uint8_t* dst = a.shards + row * a.rstride + (grp - a.first_group) * a.gstride;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      const u32x4 Aq = A[q] ^ K[q];  // bytes past lim are masked below
+      // converged: neighbour's chunk (packet bytes [o+16, o+32)) by DPP
+      uint32_t nx = 0u, ny = 0u;
+      if constexpr (MODE == 4) {
+        if (q + 1 < NP) {
+          // lane l of a half takes lane l+1's chunk; lane 31 takes lane 0's
+          // chunk of the next pass (packet bytes [o+16, o+32)), which lane 0
+          // sends instead of its own: no neighbour load
+          const u32x4 An = A[q + 1 < NP ? q + 1 : q] ^ K[q + 1 < NP ? q + 1 : q];
+          const uint32_t sx = hl == 0u ? An.x : Aq.x, sy = hl == 0u ? An.y : Aq.y;
+          const int src = static_cast<int>(hl == 31u ? lane - 31u : lane + 1u) * 4;
+          nx = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(sx)));
+          ny = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(sy)));
+        } else {
+          nx = from_next_lane(Aq.x);
+          ny = from_next_lane(Aq.y);
+          if (hl == 31u) {
+            nx = bx[q] ^ kbx[q];
+            ny = by[q] ^ kby[q];
+          }
+        }
+      } else if constexpr (MODE != 3) {
+        nx = from_next_lane(Aq.x);
+        ny = from_next_lane(Aq.y);
+        if (hl == 31u) {
+          nx = bx[q] ^ kbx[q];
+          ny = by[q] ^ kby[q];
+        }
+      }
+      if (!ok || o >= a.S) continue;
+      uint32_t w[4];
+      if constexpr (MODE == 2 || MODE == 3) {
+        w[0] = Aq.x; w[1] = Aq.y; w[2] = Aq.z; w[3] = Aq.w;
+      } else {
+        // payload bytes [o, o+16) = packet bytes [o+6, o+22)
+        w[0] = __builtin_amdgcn_alignbyte(Aq.z, Aq.y, 2);
+        w[1] = __builtin_amdgcn_alignbyte(Aq.w, Aq.z, 2);
+        w[2] = __builtin_amdgcn_alignbyte(nx, Aq.w, 2);
+        w[3] = __builtin_amdgcn_alignbyte(ny, nx, 2);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
+        const uint32_t b0 = o + 4u * j;
+        const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
+        w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+      }
+      const uint32_t nb = a.S - o;
+      if (nb >= 16u) {
+        const u32x4 v = {w[0], w[1], w[2], w[3]};
+        if constexpr (NT & 2)
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + o));
+        else
+          *reinterpret_cast<u32x4*>(dst + o) = v;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t lo = 4u * j;
+          if (nb >= lo + 4u) {
+            *reinterpret_cast<uint32_t*>(dst + o + lo) = w[j];
+          } else if (nb > lo) {
+            for (uint32_t t = 0; t < nb - lo; ++t) dst[o + lo + t] = static_cast<uint8_t>(w[j] >> (8u * t));
+          }
+        }
+      }
+    }
+    if (hl == 0) {
+      if constexpr (MODE == 0 || MODE == 3 || MODE == 4)
+        acct.issue(a, bstats, why, grp - a.first_group, row);
+      else if (why < 5)
+        atomicAdd(&bstats[why], 1u);
+    }
+  }
+  if (hl == 0) acct.settle(a, bstats);
+  if (a.stats) {
+    __syncthreads();
+    const bool mine = RARE ? (threadIdx.x >= 1 && threadIdx.x <= 3) : threadIdx.x < 5;
+    if (mine && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+  }
+}
+
+
 // Chunk-path counters: (-, bad flag, out of window, too short, pieces placed)
 // x 32 shards, one 128-B line per shard (32 shards on one line serialized the
 // adds: 1740 us).

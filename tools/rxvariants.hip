@@ -6,6 +6,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/rxvariants tools/rxvariants.hip
 // Not product code: it includes the kernel TU to instantiate variants.
 #include "../ugo_amd/csrc/rx_kernels.hip"
+#include "rx_experiments.hpp"
 
 #include <algorithm>
 #include <cstdio>
