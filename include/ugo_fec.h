@@ -53,7 +53,10 @@ extern "C" {
 /* 6: the per-call service (ugo_fec_service_start / _stop). */
 /* 7: ugo_fec_service_config, ugo_fec_poisoned; rx_assemble places packets in
  *    destination order (index + gather) -- same results. */
-#define UGO_FEC_ABI_VERSION 7
+/* 8: rx_assemble writes each placed row in whole 16-B chunks: its bytes
+ *    [shard_size, round_up(shard_size, 16)) become zero; ugo_fec_lossy_groups
+ *    and ugo_fec_reconstruct_list. */
+#define UGO_FEC_ABI_VERSION 8
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
  * that ugo/fec.go logs and swallows (ugo/fec.go:60-63, 208-210, 239-241). */
@@ -167,6 +170,34 @@ int ugo_fec_reconstruct_rows(ugo_fec* ctx, const uint8_t* const* rows, const uin
                              size_t shard_size, uint8_t* out, size_t out_row_stride, size_t out_group_stride,
                              unsigned flags, int8_t* status, void* stream);
 
+/* ---- lossy-group list (the recovery ugo's input runs, ugo/fec.go:196-207) --
+ * After RX assembly most groups of a batch are complete and need no
+ * Reconstruct (input frees them, ugo/fec.go:190-195).  ugo_fec_lossy_groups
+ * writes, in ascending order, the index of every group in [0, groups) with an
+ * erased row to rebuild -- with UGO_FEC_RECONSTRUCT_DATA_ONLY, an erased DATA
+ * row (the groups input calls Reconstruct on; groups with fewer than d shards
+ * included, their status says so) -- to list[0 .. *count).  list holds
+ * `groups` entries; list, count: device (or pinned) memory; asynchronous on
+ * `stream`.  d+p <= 64.
+ * ugo_fec_reconstruct_list then runs Reconstruct (ugo/fec.go:202) on the
+ * groups list[0 .. *count) of a strided batch: entry j reads group list[j]'s
+ * rows; its output i (the i-th erased row in ascending order, erased data rows
+ * first; DATA_ONLY: data rows only) goes to
+ *     out + j*out_entry_stride + i*out_row_stride
+ * (compact: only the lossy groups' recovered shards, in list order, as input
+ * returns them), or in place into the batch when out is NULL; status[j] (int8,
+ * nullable) as ugo_fec_reconstruct.  The count is read on the device: the
+ * call launches for max_entries (<= groups) entries and entries at or past
+ * *count do nothing, so no host synchronisation is needed between the two
+ * calls.  Code d+p <= 16, 16-B aligned rows and strides (as the fast path). */
+int ugo_fec_lossy_groups(ugo_fec* ctx, const uint64_t* present, size_t groups, unsigned flags, uint32_t* list,
+                         uint32_t* count, void* stream);
+int ugo_fec_reconstruct_list(ugo_fec* ctx, const uint8_t* shards, const uint64_t* present, size_t groups,
+                             const uint32_t* list, const uint32_t* count, size_t max_entries,
+                             size_t shard_size, size_t row_stride, size_t group_stride, uint8_t* out,
+                             size_t out_row_stride, size_t out_entry_stride, unsigned flags, int8_t* status,
+                             void* stream);
+
 /* The device address of p (device memory of ctx's GPU: p itself; pinned host
  * memory: its device mapping, which on ROCm is the host address), or
  * UGO_FEC_ERR_INVALID_ARG for memory ctx's GPU cannot reach (pageable). */
@@ -243,7 +274,11 @@ int ugo_fec_check_shards(int n, const size_t* lens, int nil_ok, size_t* shard_si
  * A packet whose flag is typeData (0xf1) or typeFEC (0xf2) and whose group is
  * in [first_group, first_group + groups) is written to row seqid % (d+p) of
  * group seqid/(d+p) - first_group of the strided batch: its payload bytes
- * [0, min(len-6, shard_size)) then zeros up to shard_size; bit row of
+ * [0, min(len-6, shard_size)) then zeros up to round_up(shard_size, 16) --
+ * whole 16-B chunks, so a row's last chunk also zeroes its bytes past
+ * shard_size (each row slot, the batch's last one included, must span
+ * round_up(shard_size, 16) bytes; with 16-B strides every slot but the last
+ * does); bit row of
  * present[group] is OR-ed (zero `present` before the first call of a batch).
  * stats (device u32[5], nullable) counts accepted / bad-flag / out-of-window /
  * too-short / duplicate packets.  Then ugo_fec_reconstruct_strided recovers

@@ -571,6 +571,76 @@ def test_reconstruct_into_vs_oracle(gpu, d, p, S, pitch, opitch, shard_major, ta
         assert np.array_equal(got, exp), (d, p, S, data_only)
 
 
+@pytest.mark.parametrize("d,p,S,pitch,shard_major,G", [
+    (10, 3, 1470, 1472, True, 900),   # ugo's RX batch: k_apply_p list form, wave spans 2 list entries
+    (10, 3, 1350, 1360, False, 333),  # group-major
+    (6, 2, 77, 80, True, 257),        # rows < 64 chunks: k_apply list form
+    (12, 4, 1030, 1040, True, 100),   # p = 4
+    (10, 5, 1200, 1200, False, 64),   # p > 4 (epad 8): k_apply list form
+    (10, 3, 1470, 1472, True, 1),     # one group
+])
+def test_lossy_list_and_reconstruct_list_vs_oracle(gpu, d, p, S, pitch, shard_major, G):
+    """ugo_fec_lossy_groups lists exactly the groups with an erased (data) row,
+    ascending; ugo_fec_reconstruct_list then matches the oracle's Reconstruct
+    for list entry j: outputs compact in list order (or in place), status[j];
+    entries past the count and the input batch untouched."""
+    n = d + p
+    host = _rand(G, n, pitch, 91 + d + p + G).numpy()
+    rs_ref.c_encode(d, p, host, S=S)
+    rng = np.random.default_rng(G + d)
+    masks = np.zeros(G, np.uint64)
+    for g in range(G):
+        e = int(rng.choice([0, 0, 1, 2, p, p + 1]))  # complete, lossy and too-few-shards groups
+        m = (1 << n) - 1
+        for r in rng.choice(n, size=min(e, n), replace=False):
+            m &= ~(1 << int(r))
+        masks[g] = m
+    inp = _erase(host, masks, n)
+    enc = fec.New(d, p)
+    dm = _masks_to_dev(masks)
+    t_in = _dev(np.ascontiguousarray(inp.transpose(1, 0, 2)) if shard_major else inp)
+    for data_only in (True, False):
+        scope = ((1 << d) - 1) if data_only else ((1 << n) - 1)
+        want_list = [g for g in range(G) if (~int(masks[g])) & scope]
+        lst, cnt = enc.lossy_groups(dm, data_only=data_only)
+        k = int(cnt.item())
+        assert lst.cpu().numpy()[:k].tolist() == want_list
+        want = inp.copy()
+        rc, want_st = rs_ref.c_reconstruct(d, p, want, masks, S=S, data_only=data_only)
+        slots = min(d, p) if data_only else p
+        out = torch.full((G, slots, pitch), 0xA5, dtype=torch.uint8, device="cuda")
+        st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+        before = t_in.clone()
+        enc.reconstruct_list(t_in, dm, lst, cnt, out, shard_size=S, data_only=data_only, status=st,
+                             shard_major=shard_major)
+        torch.cuda.synchronize()
+        assert torch.equal(t_in, before), "reconstruct_list wrote its input"
+        o, s_ = out.cpu().numpy(), st.cpu().numpy()
+        exp = np.full_like(o, 0xA5)
+        for j, g in enumerate(want_list):
+            assert s_[j] == want_st[g], (j, g)
+            if want_st[g] != 0:
+                continue
+            er = [r for r in range(n) if not (int(masks[g]) >> r) & 1 and (r < d or not data_only)]
+            for i, r in enumerate(er):
+                exp[j, i, :S] = want[g, r, :S]
+        assert np.array_equal(o, exp), (d, p, S, data_only)
+        assert (s_[k:] == -1).all()
+        # in place: the erased rows of the listed groups rebuilt in the batch itself
+        t_ip = t_in.clone()
+        enc.reconstruct_list(t_ip, dm, lst, cnt, None, shard_size=S, data_only=data_only, shard_major=shard_major)
+        got = t_ip.cpu().numpy()
+        if shard_major:
+            got = got.transpose(1, 0, 2)
+        exp_ip = inp.copy()
+        for g in want_list:
+            if want_st[g] == 0:
+                for r in range(n):
+                    if not (int(masks[g]) >> r) & 1 and (r < d or not data_only):
+                        exp_ip[g, r, :S] = want[g, r, :S]
+        assert np.array_equal(got, exp_ip)
+
+
 @pytest.mark.parametrize("d,p,S,G,table_max", [
     (10, 3, 1350, 777, "16"),   # the bench's dense rows: 8 groups per pseudo-group, k_apply_p on 2-B aligned groups
     (10, 3, 1350, 777, "0"),    # same with per-group descriptors (k_prepare)

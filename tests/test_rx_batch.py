@@ -151,6 +151,29 @@ def test_rx_assemble_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_gro
                       first_group=first_group, shard_size=S, pad=pad, stats=st)
     assert np.array_equal(present.cpu().numpy().view(np.uint64), masks)
     assert st.cpu().tolist() == stats
+    raw = sh.cpu().numpy().transpose(1, 0, 2)
+    for g in range(G):
+        for r in range(n):
+            if (int(masks[g]) >> r) & 1:
+                assert not raw[g, r, S:].any(), (g, r)  # ABI 8: the last 16-B chunk written whole, zeros past S
+            else:
+                assert (raw[g, r] == 0xAB).all(), (g, r)  # rows no packet claimed stay untouched
+    # the list form (ugo_fec_lossy_groups + ugo_fec_reconstruct_list): only the lossy groups, compact outputs
+    lst, cnt = codec.lossy_groups(present, data_only=True)
+    k = int(cnt.item())
+    want_list = [g for g in range(G) if (~int(masks[g])) & ((1 << d) - 1)]
+    assert lst.cpu().numpy()[:k].tolist() == want_list
+    lout = torch.full((G, p, pitch), 0xA5, dtype=torch.uint8, device="cuda")
+    lst_st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    codec.reconstruct_list(sh, present, lst, cnt, lout, shard_size=S, data_only=True, status=lst_st)
+    lo, ls = lout.cpu().numpy(), lst_st.cpu().numpy()
+    for j, g in enumerate(want_list):
+        assert ls[j] == exp_st[g], (j, g)
+        if exp_st[g] == 0:
+            erased = [r for r in range(d) if not (int(masks[g]) >> r) & 1]
+            for i, r in enumerate(erased):
+                assert np.array_equal(lo[j, i, :S], exp[g, r]), (j, g, r)
+    assert (lo[k:] == 0xA5).all()
     status = torch.full((G,), -1, dtype=torch.int8, device="cuda")
     codec.reconstruct_batch(sh, present, shard_size=S, data_only=True, status=status, shard_major=True)
     assert np.array_equal(status.cpu().numpy(), exp_st)

@@ -332,7 +332,12 @@ def test_service_block_that_never_leaves_poisons_the_context(gpu):
                      lambda: enc.reconstruct_host(b, np.full(1, (1 << n) - 1, np.uint64), S)):
             with pytest.raises(fec.ErrHip):
                 call()
+        t0 = time.perf_counter()
         enc.close()  # leaks the mailbox and tables: the block still reads them
+        el = time.perf_counter() - t0
+        # destroy of a poisoned context must not wait for the block
+        # (every hipFree / hipHostFree / stream destroy would synchronize with it)
+        assert el < 0.5, f"destroy of a poisoned context blocked for {el:.3f} s"
         time.sleep(1.6)  # the stalled block serves, sees the stop line and leaves
         torch.cuda.synchronize()
     finally:
@@ -385,3 +390,58 @@ def test_service_block_does_not_hold_other_streams(gpu):
         fec.host_free(big.reshape(-1))
         svc.close()
         work.close()
+
+
+def test_service_more_contexts_than_hardware_queues(gpu):
+    """six contexts (one per connection) start the service and are
+    called continuously from six threads -- more than the GPU_MAX_HW_QUEUES (4)
+    high-priority queues the service streams come from.  No call times out, no
+    context is poisoned, every parity is the oracle's; at most four contexts
+    hold a resident block at once (a pool stream each), the others are served
+    on the launch path."""
+    import threading
+    d, p, S = 10, 3, 1470
+    n, pitch = d + p, 1472
+    nctx, calls = 6, 120
+    errors, served = [], []
+    ready = threading.Barrier(nctx)
+
+    def worker(seed):
+        enc, b = None, None
+        try:
+            rng = np.random.default_rng(seed)
+            enc = fec.New(d, p)
+            enc.service_config(timeout_ms=2000, grace_ms=2000)
+            b = _pinned(1, n, pitch, rng)
+            ready.wait(timeout=60)
+            enc.service_start(idle_us=1_000_000)
+            hits = 0
+            for i in range(calls):
+                b[:] = rng.integers(0, 256, b.shape, dtype=np.uint8)
+                want = b.copy()
+                rs_ref.c_encode(d, p, want, S=S)
+                hits += _timed_launches(enc, lambda: enc.encode_host(b, S)) == 0
+                if not np.array_equal(b[:, :, :S], want[:, :, :S]):
+                    errors.append((seed, i, "bytes"))
+                    return
+            if enc.poisoned:
+                errors.append((seed, "poisoned"))
+            served.append(hits >= calls // 2)  # the block's own (re)launches are timed launches too
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append((seed, repr(ex)))
+        finally:
+            if enc is not None:
+                enc.service_stop()
+                enc.close()
+            if b is not None:
+                fec.host_free(b.reshape(-1))
+
+    ts = [threading.Thread(target=worker, args=(100 + k,)) for k in range(nctx)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors
+    assert len(served) == nctx
+    assert 1 <= sum(served) <= 4, served

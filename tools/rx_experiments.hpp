@@ -6,7 +6,7 @@
 //
 //  * chunk path: k_rx_chunk (one 16-B output chunk per thread, full grid) +
 //    k_rx_count + k_rx_chunk_stats, 597-600 us against production's 523-535 us;
-//  * production's place kernel over a full grid + k_rx_tally: 712-722 us
+//  * production's place kernel over a full grid + k_rx_tally_full: 712-722 us
 //    against 500-518 (every packet reloads its lane's keystream chunks);
 //  * destination-ordered index + gather (k_rx_index, k_rx_gather), slower still.
 #pragma once
@@ -381,11 +381,11 @@ inline hipError_t launch_rx_chunk_path(RxArgs a, uint64_t* prev, uint32_t* win, 
 // Full-grid place: k_rx_place with one packet per half-wave (blocks =
 // ceil(npk / 8), the P3b shape) -- per-block stats adds would contend, so the
 // blocks add only the rare classes to the call's scratch counters rare[1..3]
-// (RARE = 1) and k_rx_tally turns the presence bits this call set into the
+// (RARE = 1) and k_rx_tally_full turns the presence bits this call set into the
 // accepted count: stats[0] += placed, stats[1..3] += rare[1..3],
 // stats[4] += npk - placed - rare (every other valid packet was a duplicate).
 // Each block adds its share of placed (wrapping uint32 arithmetic).
-__global__ __launch_bounds__(256) void k_rx_tally(const uint64_t* present, const uint64_t* prev, uint64_t groups,
+__global__ __launch_bounds__(256) void k_rx_tally_full(const uint64_t* present, const uint64_t* prev, uint64_t groups,
                                                   const uint32_t* rare, uint32_t* stats, uint64_t npk) {
   __shared__ uint32_t tot;
   if (threadIdx.x == 0) tot = 0;
@@ -437,7 +437,7 @@ inline hipError_t launch_rx_full_path(RxArgs a, uint64_t* prev, uint32_t* win, u
   if (user_stats) {
     uint64_t tb = (a.groups + 255) / 256;
     if (tb > 64u) tb = 64u;
-    k_rx_tally<<<static_cast<uint32_t>(tb ? tb : 1), 256, 0, s>>>(a.present, prev, a.groups, rare, user_stats,
+    k_rx_tally_full<<<static_cast<uint32_t>(tb ? tb : 1), 256, 0, s>>>(a.present, prev, a.groups, rare, user_stats,
                                                                a.npk);
   }
   e = launch_rx_claim(f, s);
@@ -650,6 +650,271 @@ __global__ __launch_bounds__(256) void k_rx_gather(RxArgs a, const uint32_t* par
     if (hl == 0) atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
   }
 }
+
+
+// ---------------------------------------------------------------------------
+// Round-5 full-grid forms (tools/rxgather.hip).  Both take the
+// call's 8 control words `ctl` (zeroed by k_rx_zero_rare before the kernel):
+// [0] duplicate gate, [1] pieces placed, [2..5] packets of the rare classes 1..4,
+// [6] k_rx_tally's block count.  Results (profiles/r5/rxgather_*): k_rx_slots
+// 540-630 us against production's 489-499 (its block barriers cost more than
+// the one global load per lane they save); k_rx_half ties production (486.5 /
+// 516.4 vs 489.0 / 512.9), and with whole-chunk row tails 458.7 / 499.0 vs
+// production's 466.9 / 499.1 -- but it reads whole slots whatever the packet
+// length, so a ring of short packets would read many times its bytes;
+// production keeps the length-aware loads.
+// ---------------------------------------------------------------------------
+// Slot-linear placement (round 5).  Thread t of a block owns slot chunk
+// m = t % T of packet i = P * blockIdx.x + t / T (T = slot / 16 chunks, or
+// ceil(S / 16) if that is more): the block's P * T threads read P whole slots
+// exactly as a plain nt copy reads them -- consecutive lanes on consecutive
+// 16-B chunks, one chunk per thread, a full grid (the compute-free P2 pattern's
+// shape).  What a lane needs from another lane comes through
+// LDS, behind two block barriers:
+//  * the keystream (PADLDS): staged once per block, P slots' worth of packets
+//    per 1.5-KB stage instead of one L2 reload per packet (the cost that sank
+//    the round-4 full-grid forms); PADLDS 0 loads it per thread (A/B);
+//  * the header: chunk 0's lane decrypts it, classifies the packet, ORs its
+//    presence bit and publishes (group, row, kept length);
+//  * the realignment's right neighbour: the first 8 B of chunk m + 1.
+// No per-packet counter atomics: a block adds only its rare classes to the
+// call's control words, and k_rx_tally derives the accepted count from the
+// presence bits the call set (present & ~prev) -- and raises the duplicate
+// gate when accepted + rare falls short of the packet count, i.e. when two
+// copies of one seqid were both placed (the gated claim / re-place passes then
+// keep the first copy, as for k_rx_place_h).
+struct RxHdr {
+  uint64_t gs;   // group in the batch
+  uint32_t row;  // seqid % n
+  uint32_t L;    // payload bytes kept; kRxSkip: the packet writes nothing
+};
+constexpr uint32_t kRxSkip = 0xffffffffu;
+
+template <int PADLDS>
+__global__ __launch_bounds__(1024) void k_rx_slots(RxArgs a, uint32_t T, uint32_t P, uint32_t* ctl) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t rx_smem[];
+  __shared__ uint32_t scnt[5];
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  const uint32_t Q = slot / 16u;  // chunks per slot (<= T)
+  u32x4* spad = reinterpret_cast<u32x4*>(rx_smem);                             // [Q] (PADLDS)
+  RxHdr* shdr = reinterpret_cast<RxHdr*>(rx_smem + (PADLDS ? 16u * Q : 0u));  // [P]
+  uint2* snb = reinterpret_cast<uint2*>(shdr + P);                             // [P * T]
+  const uint32_t t = threadIdx.x;
+  const uint32_t lp = t / T, m = t - lp * T;
+  const uint64_t i = uint64_t(blockIdx.x) * P + lp;
+  const bool live = i < a.npk;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const uint8_t* pk = a.wire + i * a.slot;
+  u32x4 K = zero;
+  if constexpr (PADLDS) {
+    if (a.pad)
+      for (uint32_t q = t; q < Q; q += blockDim.x) spad[q] = ld16(a.pad + 16u * q);
+  } else {
+    if (a.pad && m < Q) K = ld16(a.pad + 16u * m);
+  }
+  u32x4 A = zero;
+  if (live && m < Q) A = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + 16u * m));
+  uint32_t len = 0u;
+  if (live && m == 0u) len = min(static_cast<uint32_t>(a.lens[i]), slot);
+  if (t < 5u) scnt[t] = 0u;
+  const bool chk_prev = a.prev && !(a.seen && *a.seen < a.call);
+  __syncthreads();
+  if constexpr (PADLDS) {
+    if (a.pad && m < Q) K = spad[m];
+  }
+  A ^= K;
+  snb[t] = make_uint2(A.x, A.y);
+  if (live && m == 0u) {  // packet bytes [0, 16): the FEC header (ugo/fec.go:78-89)
+    const uint32_t seqid = A.x, flag = A.y & 0xffffu;
+    uint32_t why = 0;
+    if (len < 6u) why = 3;
+    else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
+    const uint32_t row = seqid % a.n;
+    const uint64_t grp = seqid / a.n;
+    if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
+    const uint64_t gs = grp - a.first_group;
+    if (!why && chk_prev && ((a.prev[gs] >> row) & 1ull)) why = 4;  // an earlier call placed this seqid
+    RxHdr h;
+    h.gs = gs;
+    h.row = row;
+    h.L = why ? kRxSkip : min(len - 6u, a.S);  // copy(buf, data[6:]) bounded by the row
+    shdr[lp] = h;
+    if (why == 0)
+      atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
+    else
+      atomicAdd(&scnt[why], 1u);
+  }
+  __syncthreads();
+  if (t >= 1u && t <= 4u && scnt[t]) atomicAdd(&ctl[1 + t], scnt[t]);
+  if (!live) return;
+  const RxHdr h = shdr[lp];
+  const uint32_t o = 16u * m;  // payload bytes [o, o+16) = packet bytes [o+6, o+22)
+  if (h.L == kRxSkip || o >= a.S) return;
+  const uint2 nb = m + 1u < Q ? snb[t + 1u] : make_uint2(0u, 0u);
+  uint32_t w[4];
+  w[0] = __builtin_amdgcn_alignbyte(A.z, A.y, 2);
+  w[1] = __builtin_amdgcn_alignbyte(A.w, A.z, 2);
+  w[2] = __builtin_amdgcn_alignbyte(nb.x, A.w, 2);
+  w[3] = __builtin_amdgcn_alignbyte(nb.y, nb.x, 2);
+  const uint32_t L = h.L;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
+    const uint32_t b0 = o + 4u * j;
+    const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
+    w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+  }
+  uint8_t* dst = a.shards + h.row * a.rstride + h.gs * a.gstride + o;
+  const uint32_t nbytes = a.S - o;
+  if (nbytes >= 16u) {
+    __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4*>(dst));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = 4u * j;
+      if (nbytes >= lo + 4u) {
+        *reinterpret_cast<uint32_t*>(dst + lo) = w[j];
+      } else if (nbytes > lo) {
+        for (uint32_t q = 0; q < nbytes - lo; ++q) dst[lo + q] = static_cast<uint8_t>(w[j] >> (8u * q));
+      }
+    }
+  }
+}
+
+// Full-grid half-wave placement (round 5, the P3b shape): half a wave per
+// packet, 8 packets per 256-thread block, one packet pair per wave, no loop.
+// Unlike k_rx_place_h every load a lane issues is independent of every other
+// load: the payload chunks are read whole slot (no length-dependent predicate),
+// the length and the keystream (PADMODE 0: per lane from L1/L2; 1: staged once
+// per block in LDS) alongside, so a wave has one memory round trip before its
+// stores, not a length -> payload -> header chain.  Stats and the duplicate
+// gate as k_rx_slots (ctl + k_rx_tally); the presence atomicOr returns nothing.
+// ATTR (A/B attribution only, tools/rxgather.hip; 0 in production): 1 no
+// keystream, 2 no presence atomic, 4 whole 16-B store of the tail chunk (writes
+// the row's padding), 8 no length load, 16 no realignment.
+template <int NP, int PADMODE, int ATTR = 0>
+__global__ __launch_bounds__(256) void k_rx_half(RxArgs a, uint32_t* ctl) {
+  __shared__ u32x4 spad[PADMODE ? 32 * NP + 1 : 1];
+  const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, hl = lane & 31u;
+  const uint64_t i = blockIdx.x * 8ull + (threadIdx.x >> 5);
+  const bool live = i < a.npk;
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  const uint32_t Q = slot / 16u;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const uint8_t* pk = a.wire + i * a.slot;
+  u32x4 K[NP], A[NP];
+  if constexpr (PADMODE) {
+    if (a.pad)
+      for (uint32_t q = threadIdx.x; q < Q; q += 256u) spad[q] = ld16(a.pad + 16u * q);
+  } else {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t m = 32u * q + hl;
+      K[q] = (!(ATTR & 1) && a.pad && m < Q) ? ld16(a.pad + 16u * m) : zero;
+    }
+  }
+  const uint32_t len = live ? ((ATTR & 8) ? slot - 12u : min(static_cast<uint32_t>(a.lens[i]), slot)) : 0u;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const uint32_t m = 32u * q + hl;
+    A[q] = (live && m < Q) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + 16u * m)) : zero;
+  }
+  const bool chk_prev = a.prev && !(a.seen && *a.seen < a.call);
+  if constexpr (PADMODE) {
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t m = 32u * q + hl;
+      K[q] = (a.pad && m < Q) ? spad[m] : zero;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NP; ++q) A[q] ^= K[q];
+  const int hsrc = static_cast<int>(half * 32u) * 4;  // lane 0 of this half: packet bytes [0, 16)
+  const uint32_t seqid = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(hsrc, static_cast<int>(A[0].x)));
+  const uint32_t flag = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(hsrc, static_cast<int>(A[0].y))) & 0xffffu;
+  uint32_t why = 0;
+  if (!live) why = 5;
+  else if (len < 6u) why = 3;
+  else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
+  const uint32_t row = seqid % a.n;
+  const uint64_t grp = seqid / a.n;
+  if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
+  const uint64_t gs = grp - a.first_group;
+  if (!why && chk_prev && ((a.prev[gs] >> row) & 1ull)) why = 4;  // an earlier call placed this seqid
+  if (hl == 0u) {
+    if (why == 0 && !(ATTR & 2))
+      atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
+    else if (why < 5)
+      atomicAdd(&ctl[1 + why], 1u);
+  }
+  const uint32_t L = why == 0 ? min(len - 6u, a.S) : 0u;
+  uint8_t* dst = a.shards + row * a.rstride + gs * a.gstride;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const uint32_t o = 16u * (32u * q + hl);
+    uint32_t nx, ny;
+    if (q + 1 < NP) {  // lane l takes lane l+1's chunk, lane 31 lane 0's next-pass chunk
+      const u32x4 An = A[q + 1 < NP ? q + 1 : q];
+      const uint32_t sx = hl == 0u ? An.x : A[q].x, sy = hl == 0u ? An.y : A[q].y;
+      const int src = static_cast<int>(hl == 31u ? lane - 31u : lane + 1u) * 4;
+      nx = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(sx)));
+      ny = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(sy)));
+    } else {  // lane 31's neighbour, chunk 32 * NP, lies past the slot
+      nx = from_next_lane(A[q].x);
+      ny = from_next_lane(A[q].y);
+      if (hl == 31u) nx = ny = 0u;
+    }
+    if (why != 0 || o >= a.S) continue;
+    if constexpr (ATTR & 20) {  // attribution forms (timing only)
+      uint32_t w[4];
+      if constexpr (ATTR & 16) {
+        w[0] = A[q].x; w[1] = A[q].y; w[2] = A[q].z; w[3] = A[q].w;
+      } else {
+        w[0] = __builtin_amdgcn_alignbyte(A[q].z, A[q].y, 2);
+        w[1] = __builtin_amdgcn_alignbyte(A[q].w, A[q].z, 2);
+        w[2] = __builtin_amdgcn_alignbyte(nx, A[q].w, 2);
+        w[3] = __builtin_amdgcn_alignbyte(ny, nx, 2);
+      }
+      __builtin_nontemporal_store(u32x4{w[0], w[1], w[2], w[3]}, reinterpret_cast<u32x4*>(dst + o));
+    } else {
+      rx_put<1>(dst, o, L, A[q], nx, ny);
+    }
+  }
+}
+
+// After k_rx_slots: pieces placed = popcount(present & ~prev) over the window;
+// the last block to finish adds the call's stats and sets the duplicate gate
+// ctl[0] when placed + rare < npk (two copies of a seqid were both placed).
+__global__ __launch_bounds__(256) void k_rx_tally(const uint64_t* present, const uint64_t* prev, uint64_t groups,
+                                                  uint32_t* ctl, uint32_t* stats, uint64_t npk) {
+  __shared__ uint32_t tot;
+  if (threadIdx.x == 0) tot = 0u;
+  __syncthreads();
+  uint32_t c = 0u;
+  for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < groups; g += gridDim.x * 256ull)
+    c += static_cast<uint32_t>(__popcll(present[g] & ~prev[g]));
+  if (c) atomicAdd(&tot, c);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  if (tot) atomicAdd(&ctl[1], tot);
+  __threadfence();
+  if (atomicAdd(&ctl[6], 1u) != gridDim.x - 1u) return;
+  __threadfence();
+  const uint32_t placed = atomicAdd(&ctl[1], 0u);
+  const uint32_t r1 = atomicAdd(&ctl[2], 0u), r2 = atomicAdd(&ctl[3], 0u), r3 = atomicAdd(&ctl[4], 0u),
+                 r4 = atomicAdd(&ctl[5], 0u);
+  const uint32_t np = static_cast<uint32_t>(npk);
+  if (placed + r1 + r2 + r3 + r4 != np) ctl[0] = 1u;
+  if (stats) {
+    if (placed) atomicAdd(&stats[0], placed);
+    if (r1) atomicAdd(&stats[1], r1);
+    if (r2) atomicAdd(&stats[2], r2);
+    if (r3) atomicAdd(&stats[3], r3);
+    const uint32_t dups = np - placed - r1 - r2 - r3;
+    if (dups) atomicAdd(&stats[4], dups);
+  }
+}
+
 
 }  // namespace kern
 }  // namespace ugo

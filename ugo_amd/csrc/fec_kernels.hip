@@ -180,24 +180,34 @@ __device__ __forceinline__ const uint8_t* desc_for(const Batch& a, uint64_t g) {
 }
 
 
+// List form: the launch's work items over the list entries [g0, *count).
+__device__ __forceinline__ uint32_t list_items(const Batch& a) {
+  const uint64_t cnt = *a.count;
+  if (cnt <= a.g0) return 0u;
+  return static_cast<uint32_t>(min(static_cast<uint64_t>(a.items), (cnt - a.g0) * a.chunks));
+}
+
 // One 16-byte chunk per thread over a full grid; the descriptor (presence
 // mask -> table entry, or the group's workspace entry) is read per thread from
 // L2.  Staging descriptors per tile in LDS and software-pipelining the next
 // item measured slower (fewer waves per SIMD), see DESIGN_HISTORY.md §4.
-template <int DMAX, int MODE, int NT>
+template <int DMAX, int MODE, int NT, bool LIST = false>
 __global__ __launch_bounds__(256) void k_apply(Batch a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
-  if (item >= a.items) return;
+  uint32_t items = a.items;
+  if constexpr (LIST) items = list_items(a);
+  if (item >= items) return;
   const uint32_t gl = item / a.chunks;
   const uint32_t c = item - gl * a.chunks;
-  const uint64_t g = a.g0 + gl;
-  const uint8_t* desc = desc_for<MODE>(a, g);
+  const uint64_t g = a.g0 + gl;  // output / status index (list entry in the list form)
+  const uint64_t grow = LIST ? a.list[g] : g;  // the group whose rows are read
+  const uint8_t* desc = desc_for<MODE>(a, grow);
   const uint32_t hdr = ld32(desc);
   const uint32_t st = (hdr >> 16) & 0xffu;
   if (MODE != 0 && a.status != nullptr && c == 0) a.status[g] = static_cast<int8_t>(st);
   const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
   if (st != 0 || e == 0) return;
-  uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
+  uint8_t* gp = a.base + grow * a.gstride + static_cast<uint64_t>(c) * 16u;
   constexpr int NW = (DMAX + 3) / 4;
   uint32_t rows[NW];
 #pragma unroll
@@ -446,7 +456,7 @@ __device__ __forceinline__ void p_accum(V4* acc, const V4* x, const Batch& a, co
 }
 
 template <int DMAX, int MODE, int NT, int TSEL = 1, int WPE = 1, int EMAX = 4, bool PAIR = true, int SWZ = 0,
-          int GLR = 0>
+          int GLR = 0, bool LIST = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_apply_p(Batch a) {
   // GLR > 0 (A/B only): survivors 0..GLR-1 by LDS-DMA nt.  It ties register
   // loads on a cold batch (201.0 vs 201.0 us) and in a warm loop (187.3 vs
@@ -456,19 +466,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const uint32_t bid = block_id<SWZ>();
   const uint32_t wfirst = bid * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
   const uint32_t item = bid * 256u + threadIdx.x;
-  if (wfirst >= a.items) return;
-  const uint32_t wlast = min(wfirst + 63u, a.items - 1u);
+  uint32_t items = a.items;
+  if constexpr (LIST) items = list_items(a);  // list form: entries past *count idle
+  if (wfirst >= items) return;
+  const uint32_t wlast = min(wfirst + 63u, items - 1u);
   const uint32_t gA = wfirst / a.chunks;
   const uint32_t gB = wlast / a.chunks;
-  const uint8_t* dA = desc_for<MODE>(a, a.g0 + gA);
-  const uint8_t* dB = desc_for<MODE>(a, a.g0 + gB);
+  uint64_t rA = a.g0 + gA, rB = a.g0 + gB;  // the wave's (at most) two groups whose rows it reads
+  if constexpr (LIST) {
+    rA = a.list[rA];
+    rB = a.list[rB];
+  }
+  const uint8_t* dA = desc_for<MODE>(a, rA);
+  const uint8_t* dB = desc_for<MODE>(a, rB);
   constexpr int NW = (DMAX + 3) / 4;
   const uint32_t hA = ld32(dA), hB = ld32(dB);
-  uint32_t rA[NW], rB[NW];
+  uint32_t wA[NW], wB[NW];  // survivor row words
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
-    rA[w] = ld32(dA + 4 + 4 * w);
-    rB[w] = ld32(dB + 4 + 4 * w);
+    wA[w] = ld32(dA + 4 + 4 * w);
+    wB[w] = ld32(dB + 4 + 4 * w);
   }
   const uint32_t oA = ld32(dA + 4 + a.dpad), oB = ld32(dB + 4 + a.dpad);
   // wave-uniform output count: the larger of the two groups' (a failed group
@@ -476,11 +493,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const uint32_t eA = ((hA >> 16) & 0xffu) ? 0u : (a.data_only ? ((hA >> 8) & 0xffu) : (hA & 0xffu));
   const uint32_t eB = ((hB >> 16) & 0xffu) ? 0u : (a.data_only ? ((hB >> 8) & 0xffu) : (hB & 0xffu));
   const uint32_t emax = max(eA, eB);
-  if (item >= a.items) return;
+  if (item >= items) return;
   const uint32_t gl = item / a.chunks;
   const bool inB = gl != gA;
   const uint32_t c = item - gl * a.chunks;
-  const uint64_t g = a.g0 + gl;
+  const uint64_t g = a.g0 + gl;  // output / status index (list entry in the list form)
+  const uint64_t grow = LIST ? (inB ? rB : rA) : g;
   const uint32_t hdr = inB ? hB : hA;
   const uint32_t st = (hdr >> 16) & 0xffu;
   // (the status store comes last: a vector store ahead of the table reads
@@ -493,7 +511,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   uint32_t mB;  // all-ones in group-B lanes; opaque to the optimizer (see p_tables)
   asm("v_mov_b32 %0, %1" : "=v"(mB) : "v"(inB ? ~0u : 0u));
-  uint8_t* gp = a.base + g * a.gstride + static_cast<uint64_t>(c) * 16u;
+  uint8_t* gp = a.base + grow * a.gstride + static_cast<uint64_t>(c) * 16u;
   const uint32_t nb = a.S - c * 16u;
   V4 x[DMAX];
   if constexpr (GLR > 0) {  // survivors 0..GLR-1 by LDS-DMA nt, the rest to registers (host: d == 10)
@@ -502,7 +520,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     uint32_t tok = 0;
 #pragma unroll
     for (int k = 0; k < DMAX; ++k) {
-      const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
+      const uint32_t rw = inB ? wB[k >> 2] : wA[k >> 2];
       const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
       if (k < GLR)
         lds_dma16_nt_asm(gp + static_cast<uint64_t>(r) * a.rstride, sbase + 1024u * k, tok);
@@ -514,7 +532,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int k = 0; k < DMAX; ++k) {
       if (k < static_cast<int>(a.d)) {
-        const uint32_t rw = inB ? rB[k >> 2] : rA[k >> 2];
+        const uint32_t rw = inB ? wB[k >> 2] : wA[k >> 2];
         const uint32_t r = (rw >> (8 * (k & 3))) & 0xffu;
         x[k] = load16<NT>(gp + static_cast<uint64_t>(r) * a.rstride);
       } else {
@@ -1873,6 +1891,109 @@ hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s) {
     case 2: return launch_apply_mode<2>(dmax, a, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// ------------------------------------------------------------- list form
+// Lossy-group list in two launches, no atomics, ascending group order: block b
+// of k_lossy_count counts the groups of its kLossyPerBlock that have an erased
+// row to rebuild; block b of k_lossy_write sums the counts of blocks < b (its
+// output offset), scans its own groups in order and writes their indices; the
+// last block also writes the total.
+__device__ __forceinline__ bool lossy(const uint64_t* present, uint64_t g, uint64_t nmask, uint64_t dmask) {
+  return ((~present[g]) & nmask & dmask) != 0;
+}
+
+__global__ __launch_bounds__(1024) void k_lossy_count(const uint64_t* present, uint64_t groups, uint64_t nmask,
+                                                      uint64_t dmask, uint32_t* work) {
+  __shared__ uint32_t tot;
+  if (threadIdx.x == 0) tot = 0;
+  __syncthreads();
+  const uint64_t g0 = uint64_t(blockIdx.x) * kLossyPerBlock;
+  uint32_t c = 0;
+  for (uint32_t k = threadIdx.x; k < kLossyPerBlock; k += 1024u) {
+    const uint64_t g = g0 + k;
+    if (g < groups && lossy(present, g, nmask, dmask)) ++c;
+  }
+  c = __reduce_add_sync(~0ull, c);
+  if ((threadIdx.x & 63u) == 0 && c) atomicAdd(&tot, c);
+  __syncthreads();
+  if (threadIdx.x == 0) work[blockIdx.x] = tot;
+}
+
+// Thread t scans groups g0 + 4t .. g0 + 4t + 3 (kLossyPerBlock / 1024 = 4 per
+// thread, in order); a block-wide exclusive scan of the per-thread counts
+// places them.
+__global__ __launch_bounds__(1024) void k_lossy_write(const uint64_t* present, uint64_t groups, uint64_t nmask,
+                                                      uint64_t dmask, const uint32_t* work, uint32_t* list,
+                                                      uint32_t* count) {
+  constexpr uint32_t kPer = kLossyPerBlock / 1024u;
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t base;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  // this block's offset: the counts of all earlier blocks
+  uint32_t before = 0;
+  for (uint32_t b = t; b < blockIdx.x; b += 1024u) before += work[b];
+  before = __reduce_add_sync(~0ull, before);
+  if (t == 0) base = 0;
+  __syncthreads();
+  if (lane == 0 && before) atomicAdd(&base, before);
+  const uint64_t g0 = uint64_t(blockIdx.x) * kLossyPerBlock + uint64_t(t) * kPer;
+  uint32_t bits = 0, c = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint64_t g = g0 + k;
+    if (g < groups && lossy(present, g, nmask, dmask)) {
+      bits |= 1u << k;
+      ++c;
+    }
+  }
+  // inclusive scan of c over the wave, then over the waves
+  uint32_t inc = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(inc, off, 64);
+    if (static_cast<int>(lane) >= off) inc += v;
+  }
+  if (lane == 63u) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t wbefore = 0;
+  for (uint32_t w = 0; w < wv; ++w) wbefore += wsum[w];
+  uint32_t pos = base + wbefore + inc - c;
+  for (uint32_t k = 0; k < kPer; ++k)
+    if ((bits >> k) & 1u) list[pos++] = static_cast<uint32_t>(g0 + k);
+  if (blockIdx.x == gridDim.x - 1u && t == 1023u) *count = pos;  // the last thread's end = the total
+}
+
+hipError_t launch_lossy_list(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t* list,
+                             uint32_t* count, uint32_t* work, hipStream_t s) {
+  const uint64_t blocks = (groups + kLossyPerBlock - 1) / kLossyPerBlock;
+  if (blocks == 0 || blocks > 0xffffffffull) return hipErrorInvalidValue;
+  launch(kKReconstruct, k_lossy_count, dim3(static_cast<uint32_t>(blocks)), dim3(1024), 0, s, present, groups, nmask,
+         dmask, work);
+  launch(kKReconstruct, k_lossy_write, dim3(static_cast<uint32_t>(blocks)), dim3(1024), 0, s, present, groups, nmask,
+         dmask, static_cast<const uint32_t*>(work), list, count);
+  return hipGetLastError();
+}
+
+template <int DMAX>
+static void launch_apply_list_dm(const Batch& a, hipStream_t s) {
+  const dim3 grid(blocks_for(a.items, 256)), block(256);
+  if (a.chunks >= 64 && a.epad == 4)
+    launch(kKReconstruct, k_apply_p<DMAX, 1, kApplyPNT, 1, 1, 4, true, 0, 0, true>, grid, block, 0, s, a);
+  else
+    launch(kKReconstruct, k_apply<DMAX, 1, kApplyNT, true>, grid, block, 0, s, a);
+}
+
+hipError_t launch_apply_list(int dmax, const Batch& a, hipStream_t s) {
+  switch (dmax) {
+    case 4: launch_apply_list_dm<4>(a, s); break;
+    case 8: launch_apply_list_dm<8>(a, s); break;
+    case 10: launch_apply_list_dm<10>(a, s); break;
+    case 12: launch_apply_list_dm<12>(a, s); break;
+    case 16: launch_apply_list_dm<16>(a, s); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 template <int MODE>

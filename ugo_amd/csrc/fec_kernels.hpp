@@ -34,6 +34,8 @@ struct Batch {
   uint64_t orstride;
   const uint64_t* rows;     // k_apply_rows: row r of group g at rows[g*n + r] (device addresses)
   uint32_t n;               // k_apply_rows: d + p; k_apply_pd: groups in the launch
+  const uint32_t* list;     // list form (launch_apply_list): entry j = g0 + gl reads group list[j]'s rows
+  const uint32_t* count;    //   and writes output / status j; entries at or past *count do nothing
 };
 
 struct Prep {
@@ -59,6 +61,15 @@ hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s);
 hipError_t launch_apply_bytes(int mode, const Batch& a, hipStream_t s);
 hipError_t launch_prepare(const Prep& a, uint32_t groups, hipStream_t s);
 hipError_t launch_apply_rows(int mode, const Batch& a, hipStream_t s);  // MODE 1 / 2, output batch required
+// List form of the MODE-1 reconstruct (d + p <= 16): a.items = max entries * chunks;
+// entry j reads the rows of group a.list[j] and writes output slot / status j.
+hipError_t launch_apply_list(int dmax, const Batch& a, hipStream_t s);
+// Lossy-group list: the groups of [0, groups) with an erased row to rebuild
+// (data rows only when data_only), ascending, into list[0 .. *count); `work`
+// holds ceil(groups / kLossyPerBlock) + 1 words of scratch.
+constexpr uint32_t kLossyPerBlock = 4096;
+hipError_t launch_lossy_list(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t* list,
+                             uint32_t* count, uint32_t* work, hipStream_t s);
 // Dense rows (group stride == S, no padding; k_apply_pd): MODE 1 / 2, d <= 16
 // (dmax 4..16), p <= 4, S >= kDenseMinS (a wave's 63 chunks span at most one
 // group boundary).  a.base = row 0 of group a.g0, 16-B aligned; a.items =

@@ -99,6 +99,38 @@ struct RxAccount {
   }
 };
 
+// Realigns, masks and stores one output chunk of a packet: payload bytes
+// [o, o + 16) = packet bytes [o + 6, o + 22) = bytes 6..15 of the lane's chunk
+// A and bytes 0..5 of the next one (nx, ny); bytes at or past the kept length
+// L (<= S) are zero.  Always a whole 16-B chunk: a row's last chunk carries
+// zeros past S up to round_up(S, 16) (include/ugo_fec.h).  Writing only the
+// row's S bytes left every row's last 64-B line partially written, and that
+// cost 7 % of the RX kernel's time in order, 3 % shuffled (458.7 vs 494.9 us,
+// 499.0 vs 512.4; tools/rxgather.hip, profiles/r5/rxgather_tail_*) -- while
+// one unaligned 16-B store of the row's last 16 payload bytes, which leaves
+// the padding unwritten, gained nothing (487.1 / 531.4 us): the partial line,
+// not the store count, is the cost.
+template <int NTS>
+__device__ __forceinline__ void rx_put(uint8_t* row, uint32_t o, uint32_t L, const u32x4& A, uint32_t nx,
+                                       uint32_t ny) {
+  uint32_t w[4];
+  w[0] = __builtin_amdgcn_alignbyte(A.z, A.y, 2);
+  w[1] = __builtin_amdgcn_alignbyte(A.w, A.z, 2);
+  w[2] = __builtin_amdgcn_alignbyte(nx, A.w, 2);
+  w[3] = __builtin_amdgcn_alignbyte(ny, nx, 2);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
+    const uint32_t b0 = o + 4u * j;
+    const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
+    w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+  }
+  const u32x4 v = {w[0], w[1], w[2], w[3]};
+  if constexpr (NTS)
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(row + o));
+  else
+    *reinterpret_cast<u32x4*>(row + o) = v;
+}
+
 __device__ __forceinline__ bool rx_gated_off(const RxArgs& a) { return a.gate && *a.gate == 0u; }
 
 __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
@@ -156,34 +188,7 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
         bx = B.x;
         by = B.y;
       }
-      if (ok && o < a.S) {
-        // payload bytes [o, o+16) = packet bytes [o+6, o+22)
-        uint32_t w[4];
-        w[0] = __builtin_amdgcn_alignbyte(A.z, A.y, 2);
-        w[1] = __builtin_amdgcn_alignbyte(A.w, A.z, 2);
-        w[2] = __builtin_amdgcn_alignbyte(bx, A.w, 2);
-        w[3] = __builtin_amdgcn_alignbyte(by, bx, 2);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
-          const uint32_t b0 = o + 4u * j;
-          const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
-          w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
-        }
-        const uint32_t nb = a.S - o;
-        if (nb >= 16u) {
-          *reinterpret_cast<u32x4*>(dst + o) = u32x4{w[0], w[1], w[2], w[3]};
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t lo = 4u * j;
-            if (nb >= lo + 4u) {
-              *reinterpret_cast<uint32_t*>(dst + o + lo) = w[j];
-            } else if (nb > lo) {
-              for (uint32_t t = 0; t < nb - lo; ++t) dst[o + lo + t] = static_cast<uint8_t>(w[j] >> (8u * t));
-            }
-          }
-        }
-      }
+      if (ok && o < a.S) rx_put<0>(dst, o, L, A, bx, by);  // whole chunks (rx_put)
     }
     if (hl == 0) acct.issue(a, bstats, why, gs, row);
   }
@@ -293,35 +298,7 @@ __global__ __launch_bounds__(256) void k_rx_place_h(RxArgs a) {
         }
       }
       if (!ok || o >= a.S) continue;
-      uint32_t w[4];
-      w[0] = __builtin_amdgcn_alignbyte(Aq.z, Aq.y, 2);  // payload bytes [o, o+16) = packet bytes [o+6, o+22)
-      w[1] = __builtin_amdgcn_alignbyte(Aq.w, Aq.z, 2);
-      w[2] = __builtin_amdgcn_alignbyte(nx, Aq.w, 2);
-      w[3] = __builtin_amdgcn_alignbyte(ny, nx, 2);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
-        const uint32_t b0 = o + 4u * j;
-        const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
-        w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
-      }
-      const uint32_t nb = a.S - o;
-      if (nb >= 16u) {
-        const u32x4 v = {w[0], w[1], w[2], w[3]};
-        if constexpr (NT & 2)
-          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + o));
-        else
-          *reinterpret_cast<u32x4*>(dst + o) = v;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t lo = 4u * j;
-          if (nb >= lo + 4u) {
-            *reinterpret_cast<uint32_t*>(dst + o + lo) = w[j];
-          } else if (nb > lo) {
-            for (uint32_t t = 0; t < nb - lo; ++t) dst[o + lo + t] = static_cast<uint8_t>(w[j] >> (8u * t));
-          }
-        }
-      }
+      rx_put<(NT & 2)>(dst, o, L, Aq, nx, ny);
     }
     if (hl == 0) acct.issue(a, bstats, why, grp - a.first_group, row);
   }

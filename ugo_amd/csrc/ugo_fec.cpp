@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <unordered_map>
@@ -202,17 +203,21 @@ int svc_stop(ugo_fec* c);
 void free_ctx(ugo_fec* c) {
   if (!c) return;
   DeviceGuard g(c->device);
-  // the resident block leaves before its mailbox and tables go; if it does not
-  // (poisoned), everything it reads is leaked rather than freed under it
-  const bool block_gone = svc_stop(c) == UGO_FEC_OK && !c->poisoned;
-  if (block_gone) {
-    if (c->svc_stream) (void)hipStreamDestroy(c->svc_stream);
-    if (c->svc_box) (void)hipHostFree(c->svc_box);
-    (void)hipFree(c->d_M);
-    (void)hipFree(c->d_gf);
-    (void)hipFree(c->d_encdesc);
-    (void)hipFree(c->d_table);
+  // the resident block leaves before its mailbox and tables go
+  if (c->poisoned || svc_stop(c) != UGO_FEC_OK) {
+    // poisoned: a block that never left may still read the mailbox and tables
+    // and write a caller's batch.  Every device-side release -- hipFree,
+    // hipHostFree, stream and pool destruction -- synchronizes with the device
+    // and would wait for that block (forever, if it never leaves), so all of
+    // it is leaked; only the host-side object goes.
+    delete c;
+    return;
   }
+  (void)hipHostFree(c->svc_box);
+  (void)hipFree(c->d_M);
+  (void)hipFree(c->d_gf);
+  (void)hipFree(c->d_encdesc);
+  (void)hipFree(c->d_table);
   (void)hipFree(c->d_rxseen);
   timer_release(c);
   (void)hipHostFree(c->d_zc_mask);
@@ -675,29 +680,87 @@ bool svc_eligible(const ugo_fec* c, const uint8_t* mapped, size_t groups, size_t
 // landed on the service's queue would queue every launch and copy behind the
 // resident block, i.e. wait out the idle window (tools/svc_sync_probe.cpp:
 // a 65,536-group staged host encode took 1002 ms instead of 17 with a 1-s
-// window).
+// window).  Streams of another priority come from another pool, so the
+// service runs on a high-priority stream -- but that pool is GPU_MAX_HW_QUEUES
+// queues too: a fifth high-priority stream shares a queue with one of the
+// first four, and a block resident there would hold back the other's launch
+// until the watchdog poisoned it.  So the service streams are a
+// process-wide pool per device, at most that many, each leased to ONE context
+// while its service is on (the first streams of the priority created in the
+// process, so each has its own queue); a context that finds none free serves
+// its calls on the launch path (ugo_fec_service_start still succeeds).
 #ifndef UGO_SVC_QUEUE
 #define UGO_SVC_QUEUE 2
 #endif
-hipError_t create_service_stream(ugo_fec* c) {
+hipError_t create_service_stream(int device, hipStream_t* out) {
 #if UGO_SVC_QUEUE == 1
   // a CU-masked stream is never pooled; but it is a blocking stream
   hipDeviceProp_t prop{};
-  hipError_t e = hipGetDeviceProperties(&prop, c->device);
+  hipError_t e = hipGetDeviceProperties(&prop, device);
   if (e != hipSuccess) return e;
   const int cus = std::max(prop.multiProcessorCount, 1);
   std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
   if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
-  return hipExtStreamCreateWithCUMask(&c->svc_stream, static_cast<uint32_t>(mask.size()), mask.data());
+  return hipExtStreamCreateWithCUMask(out, static_cast<uint32_t>(mask.size()), mask.data());
 #elif UGO_SVC_QUEUE == 2
-  // streams of another priority come from another queue pool
+  (void)device;
   int lo = 0, hi = 0;
   hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
   if (e != hipSuccess) return e;
-  return hipStreamCreateWithPriority(&c->svc_stream, hipStreamNonBlocking, hi);
+  return hipStreamCreateWithPriority(out, hipStreamNonBlocking, hi);
 #else
-  return hipStreamCreateWithFlags(&c->svc_stream, hipStreamNonBlocking);
+  (void)device;
+  return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
 #endif
+}
+
+struct SvcStreamPool {
+  std::mutex mu;
+  std::unordered_map<int, std::vector<hipStream_t>> idle;  // per device: created, not leased
+  std::unordered_map<int, int> created;
+};
+
+SvcStreamPool& svc_pool() {
+  static SvcStreamPool* p = new SvcStreamPool();  // process lifetime: its streams are never destroyed
+  return *p;
+}
+
+int svc_queue_cap() {
+  static const int cap = [] {
+    int q = 4;  // HIP's default GPU_MAX_HW_QUEUES
+    if (const char* env = std::getenv("GPU_MAX_HW_QUEUES"))
+      if (std::atoi(env) > 0) q = std::atoi(env);
+    return std::min(q, 32);
+  }();
+  return cap;
+}
+
+// A stream of the pool for c's service, or null when every pool stream of the
+// device is leased.  Called under the context's DeviceGuard.
+hipStream_t svc_lease(ugo_fec* c) {
+  SvcStreamPool& p = svc_pool();
+  std::lock_guard<std::mutex> lk(p.mu);
+  std::vector<hipStream_t>& idle = p.idle[c->device];
+  if (!idle.empty()) {
+    hipStream_t s = idle.back();
+    idle.pop_back();
+    return s;
+  }
+  int& made = p.created[c->device];
+  if (made >= svc_queue_cap()) return nullptr;
+  hipStream_t s = nullptr;
+  if (create_service_stream(c->device, &s) != hipSuccess) return nullptr;
+  ++made;
+  return s;
+}
+
+// Back to the pool: only once no block of c's can still be resident on it.
+void svc_release(ugo_fec* c) {
+  if (!c->svc_stream) return;
+  SvcStreamPool& p = svc_pool();
+  std::lock_guard<std::mutex> lk(p.mu);
+  p.idle[c->device].push_back(c->svc_stream);
+  c->svc_stream = nullptr;
 }
 
 // Writes one request (layout: SvcBox::line): every field, then the pieces'
@@ -751,13 +814,17 @@ int svc_retire(ugo_fec* c) {
   for (uint32_t spin = 0;; ++spin) {
     if ((spin & 255u) == 0) {
       const hipError_t q = hipStreamQuery(c->svc_stream);
-      if (q == hipSuccess) return UGO_FEC_OK;  // drained: alive is 0 or the block never ran
-      if (q != hipErrorNotReady) return UGO_FEC_OK;  // faulted: the block is dead
+      // drained (alive is 0 or the block never ran), or faulted (the block is
+      // dead): nothing of c's is left on the stream, another context may lease it
+      if (q == hipSuccess || q != hipErrorNotReady) {
+        svc_release(c);
+        return UGO_FEC_OK;
+      }
       if (std::chrono::steady_clock::now() - t0 > grace) break;
     }
     svc_relax();
   }
-  c->poisoned = true;
+  c->poisoned = true;  // the stream stays leased: the block may still be on it
   return UGO_FEC_ERR_HIP;
 }
 
@@ -1091,6 +1158,78 @@ int ugo_fec_reconstruct_into(ugo_fec* c, const uint8_t* shards, const uint64_t* 
                          static_cast<hipStream_t>(stream), O);
 }
 
+int ugo_fec_lossy_groups(ugo_fec* c, const uint64_t* present, size_t groups, unsigned flags, uint32_t* list,
+                         uint32_t* count, void* stream) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
+  if (!present || !list || !count || c->n > 64 || groups >= 0xffffffffull) return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(present) || !device_view(list) || !device_view(count)) return UGO_FEC_ERR_INVALID_ARG;
+  TimerScope ts(c);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  if (groups == 0) return hip_status(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
+  const uint64_t nmask = c->n >= 64 ? ~0ull : ((1ull << c->n) - 1);
+  const uint64_t dmask = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? ((1ull << c->d) - 1) : ~0ull;
+  const size_t blocks = (groups + ugo::kern::kLossyPerBlock - 1) / ugo::kern::kLossyPerBlock;
+  void* work = nullptr;
+  int st = scratch_alloc(c, (blocks + 1) * sizeof(uint32_t), s, &work);
+  if (st) return st;
+  st = hip_status(ugo::kern::launch_lossy_list(present, groups, nmask, dmask, list, count,
+                                               static_cast<uint32_t*>(work), s));
+  const int fr = scratch_free(c, work, s);
+  return st ? st : fr;
+}
+
+int ugo_fec_reconstruct_list(ugo_fec* c, const uint8_t* shards, const uint64_t* present, size_t groups,
+                             const uint32_t* list, const uint32_t* count, size_t max_entries, size_t S,
+                             size_t row_stride, size_t group_stride, uint8_t* out, size_t out_row_stride,
+                             size_t out_entry_stride, unsigned flags, int8_t* status, void* stream) {
+  const Layout L{row_stride, group_stride};
+  int st = check_batch(c, shards, groups, S, L);
+  if (st) return st;
+  if (groups == 0 || max_entries == 0) return UGO_FEC_OK;
+  if (!present || !list || !count || c->n > 16 || !c->d_table || max_entries > groups)
+    return UGO_FEC_ERR_INVALID_ARG;
+  if (!fast_layout(c, shards, L, S)) return UGO_FEC_ERR_INVALID_ARG;
+  const size_t oslots = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? size_t(std::min(c->d, c->p)) : size_t(c->p);
+  if (out) {
+    if (reinterpret_cast<uintptr_t>(out) % 16 || out_row_stride % 16 || out_entry_stride % 16 ||
+        !layout_disjoint(S, out_row_stride, oslots, out_entry_stride, max_entries))
+      return UGO_FEC_ERR_INVALID_ARG;
+    const size_t in_ext = extent(S, row_stride, size_t(c->n), group_stride, groups);
+    const size_t out_ext = extent(S, out_row_stride, oslots, out_entry_stride, max_entries);
+    const uintptr_t i0 = reinterpret_cast<uintptr_t>(shards), o0 = reinterpret_cast<uintptr_t>(out);
+    if (o0 < i0 + in_ext && i0 < o0 + out_ext) return UGO_FEC_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(shards) || !device_view(present) || !device_view(list) || !device_view(count) ||
+      !device_view(status) || !device_view(out))
+    return UGO_FEC_ERR_INVALID_ARG;
+  TimerScope ts(c);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  ugo::kern::Batch a = base_batch(c, const_cast<uint8_t*>(shards), S, L);
+  a.out = out;
+  a.ogstride = out_entry_stride;
+  a.orstride = out_row_stride;
+  a.present = present;
+  a.status = status;
+  a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
+  a.chunks = static_cast<uint32_t>((S + 15) / 16);
+  a.desc = c->d_table;
+  a.list = list;
+  a.count = count;
+  const size_t per = slice_groups(a.chunks, true);
+  for (size_t g0 = 0; g0 < max_entries; g0 += per) {
+    const size_t gn = std::min(per, max_entries - g0);
+    a.g0 = g0;
+    a.items = static_cast<uint32_t>(gn * a.chunks);
+    if (ugo::kern::launch_apply_list(ugo::kern::apply_dmax(c->d), a, s) != hipSuccess) return UGO_FEC_ERR_HIP;
+  }
+  return UGO_FEC_OK;
+}
+
 int ugo_fec_reconstruct(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
                         size_t pitch, unsigned flags, int8_t* status, void* stream) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
@@ -1198,7 +1337,11 @@ int ugo_fec_service_start(ugo_fec* c, unsigned idle_us) {
     c->svc_dbox = c->svc_box;
     if (!device_view(c->svc_dbox)) return UGO_FEC_ERR_HIP;
   }
-  if (!c->svc_stream && create_service_stream(c) != hipSuccess) return UGO_FEC_ERR_HIP;
+  if (!c->svc_stream) c->svc_stream = svc_lease(c);
+  if (!c->svc_stream) {  // every service stream of the device is leased: the launch path serves this context
+    c->svc_on = false;
+    return UGO_FEC_OK;
+  }
   int khz = 0;  // wall_clock64's rate (100 MHz on gfx950)
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0) khz = 100000;
   // at most 1 s resident after the last call: a process that exits without

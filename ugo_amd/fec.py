@@ -142,6 +142,8 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_tx_assemble.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp, vp]
     lib.ugo_fec_packet_decode.argtypes = [vp, vp, sz, vp, sz, vp, u, vp, vp, sz, vp, sz, vp]
     lib.ugo_fec_reconstruct_rows.argtypes = [vp, vp, vp, sz, sz, vp, sz, sz, u, vp, vp]
+    lib.ugo_fec_lossy_groups.argtypes = [vp, vp, sz, u, vp, vp, vp]
+    lib.ugo_fec_reconstruct_list.argtypes = [vp, vp, vp, sz, vp, vp, sz, sz, sz, sz, vp, sz, sz, u, vp, vp]
     lib.ugo_fec_device_address.argtypes = [vp, vp, ctypes.POINTER(vp)]
     lib.ugo_fec_timing_begin.argtypes = [vp, sz]
     lib.ugo_fec_timing_end.argtypes = [vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
@@ -288,6 +290,44 @@ class Encoder:
                                                        out.data_ptr(), ors, ogs,
                                                        RECONSTRUCT_DATA_ONLY if data_only else 0, st,
                                                        _stream_handle(stream)))
+
+    def lossy_groups(self, present, data_only: bool = True, out=None, count=None, stream=None):
+        """ugo_fec_lossy_groups: the groups of `present` (int64 CUDA [G]) with an
+        erased row to rebuild (data rows only with data_only), ascending.  Returns
+        (list, count): an int32 CUDA tensor [G] whose first *count entries are the
+        groups, and an int32 CUDA tensor [1]; nothing is synchronised."""
+        import torch
+
+        G = present.numel()
+        _require(present.is_contiguous() and present.element_size() == 8 and self.mask_words == 1)
+        lst = torch.empty(max(G, 1), dtype=torch.int32, device=present.device) if out is None else out
+        cnt = torch.empty(1, dtype=torch.int32, device=present.device) if count is None else count
+        _require(lst.numel() >= G and lst.element_size() == 4 and cnt.element_size() == 4)
+        _raise(load_library().ugo_fec_lossy_groups(self._h, present.data_ptr(), G,
+                                                   RECONSTRUCT_DATA_ONLY if data_only else 0, lst.data_ptr(),
+                                                   cnt.data_ptr(), _stream_handle(stream)))
+        return lst, cnt
+
+    def reconstruct_list(self, shards, present, lst, count, out, shard_size: Optional[int] = None,
+                         data_only: bool = True, status=None, stream=None, shard_major: bool = True,
+                         max_entries: Optional[int] = None):
+        """ugo_fec_reconstruct_list: Reconstruct the groups lst[0 .. *count) of the
+        batch; output i of list entry j goes to out[j, i] (out: contiguous uint8
+        CUDA tensor [max_entries][slots][opitch], compact in list order) or, out =
+        None, in place.  status: int8 CUDA [max_entries] (entry j's status)."""
+        G, pitch, rs, gs = self._geom(shards, shard_major)
+        _require(present.is_contiguous() and present.numel() == G and present.element_size() == 8)
+        m = G if max_entries is None else max_entries
+        S = pitch if shard_size is None else shard_size
+        ors = oes = 0
+        if out is not None:
+            _require(out.is_contiguous() and out.element_size() == 1 and out.dim() == 3 and out.shape[0] >= m)
+            ors, oes = out.shape[2], out.shape[1] * out.shape[2]
+            _require(out.shape[2] >= S)
+        _raise(load_library().ugo_fec_reconstruct_list(
+            self._h, shards.data_ptr(), present.data_ptr(), G, lst.data_ptr(), count.data_ptr(), m, S, rs, gs,
+            None if out is None else out.data_ptr(), ors, oes, RECONSTRUCT_DATA_ONLY if data_only else 0,
+            None if status is None else status.data_ptr(), _stream_handle(stream)))
 
     def reconstruct_rows(self, rows, present, out, shard_size: int, data_only=False, status=None, stream=None,
                          out_shard_major: bool = True):
