@@ -54,8 +54,8 @@ extern "C" {
 /* 7: ugo_fec_service_config, ugo_fec_poisoned; rx_assemble places packets in
  *    destination order (index + gather) -- same results. */
 /* 8: rx_assemble writes each placed row in whole 16-B chunks: its bytes
- *    [shard_size, round_up(shard_size, 16)) become zero; ugo_fec_lossy_groups
- *    and ugo_fec_reconstruct_list. */
+ *    [shard_size, round_up(shard_size, 16)) become zero; ugo_fec_lossy_groups,
+ *    ugo_fec_reconstruct_list, ugo_fec_rx_recover_host, ugo_fec_tx_assemble_host. */
 #define UGO_FEC_ABI_VERSION 8
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
@@ -332,6 +332,46 @@ int ugo_fec_tx_assemble(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, const
                         size_t groups, uint32_t first_seq, const uint8_t* pad, size_t max_len,
                         uint8_t* wire, size_t slot_out, uint16_t* wire_lens, int8_t* status,
                         void* stream);
+
+/* ---- host-memory RX and TX paths ----------------------------------------
+ * The RX path from the socket's receive buffers to the recovered packets, host
+ * memory in and out (ugo/listener.go:48 ReadFrom -> Conn.handlePacket,
+ * ugo/conn.go:387-406 -> FEC.input, ugo/fec.go:107-226): the packet ring
+ * (npackets slots of slot_stride bytes, lens[i] bytes each; host memory,
+ * pinned -- ugo_fec_host_alloc -- for full-rate DMA) is copied to the device
+ * in chunks that overlap their assembly (ugo_fec_rx_assemble semantics over
+ * the window [first_group, first_group + groups), one call per chunk, the first
+ * copy of a seqid in ring order wins), then every group with a lost data
+ * shard is recovered (ugo_fec_lossy_groups + ugo_fec_reconstruct_list,
+ * DATA_ONLY) and only its recovered shards come back:
+ *   *n_out        the number of groups with a lost data shard (as listed by
+ *                 ugo_fec_lossy_groups, fewer than d shards included);
+ *   out_groups[j] group j's index in the window (ascending), j < min(*n_out,
+ *                 max_out) -- entries past max_out are not returned;
+ *   out_status[j] (nullable) its Reconstruct status (UGO_FEC_ERR_TOO_FEW_SHARDS
+ *                 when fewer than d shards arrived: no rows then);
+ *   out + (j*min(d,p) + i)*out_row_stride: its i-th lost data shard in
+ *                 ascending row order, shard_size bytes (the `recovered` slices
+ *                 input returns, ugo/fec.go:203-207);
+ *   present_out   (host u64[groups], nullable) the presence masks after
+ *                 assembly; stats_out (host u32[5], nullable) the counts of
+ *                 ugo_fec_rx_assemble (set, not added).
+ * pad: host memory, >= slot_stride bytes, or NULL.  Synchronous.  d+p <= 16.
+ * The device batch ([d+p][groups][round_up(shard_size, 16)]) and the staging
+ * are the engine's (stream-ordered scratch). */
+int ugo_fec_rx_recover_host(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, const uint16_t* lens,
+                            size_t npackets, const uint8_t* pad, uint64_t first_group, size_t groups,
+                            size_t shard_size, uint64_t* present_out, uint32_t* stats_out, uint8_t* out,
+                            size_t out_row_stride, size_t max_out, uint32_t* out_groups, int8_t* out_status,
+                            size_t* n_out);
+
+/* ugo_fec_tx_assemble with every buffer in host memory (pinned for full-rate
+ * DMA): the groups go through the device in chunks, each chunk's data packets
+ * H2D, assembled, its wire packets, lengths and statuses D2H, chunks
+ * pipelined over three streams.  Same arguments and results; synchronous. */
+int ugo_fec_tx_assemble_host(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, const uint16_t* lens,
+                             size_t groups, uint32_t first_seq, const uint8_t* pad, size_t max_len,
+                             uint8_t* wire, size_t slot_out, uint16_t* wire_lens, int8_t* status);
 
 /* RC4 keystream (crypto/rc4 KSA + PRGA) of a key, host memory: the pad above
  * for ugo's fixed-key rc4StreamCrypto (ugo/crypto.go:14-39). */

@@ -341,6 +341,68 @@ def test_rx_assemble_first_copy_wins_across_calls(gpu, encrypt, S, slot):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("encrypt,first_group,max_out,pinned", [(True, 0, None, True), (True, 5, 40, True),
+                                                                (False, 0, None, False)])
+def test_rx_recover_host_vs_oracle(gpu, encrypt, first_group, max_out, pinned):
+    """ugo_fec_rx_recover_host: a packet ring in host memory (loss, duplicates,
+    junk, shuffled; >= 4 chunks) in, the lost data shards of every lossy group
+    out, against the oracle: placement (fec_ref decode + grouping), then
+    Reconstruct (rs_ref) of each group with a lost data shard; statuses, stats
+    and presence masks too.  max_out < the lossy count: only the first
+    max_out groups come back, the count is still the total."""
+    d, p, n, S, pitch, slot = 10, 3, 13, 1470, 1472, 1488
+    total_groups, G = 300, 256
+    pk = _packets(total_groups, 23, False)
+    rng = np.random.default_rng(31 + first_group)
+    wire = []
+    for w in pk:
+        if rng.random() < 0.12:
+            continue  # lost
+        wire.append(w)
+        if rng.random() < 0.05:
+            wire.append(w)  # duplicate
+        if rng.random() < 0.02:
+            junk = bytearray(rng.integers(0, 256, 40, dtype=np.uint8).tobytes())
+            junk[4:6] = b"\x00\x00"
+            wire.append(bytes(junk))
+    rng.shuffle(wire)
+    enc = [rc4_ref.xor_stream(KEY, w) if encrypt else w for w in wire]
+    npk = len(enc)
+    if pinned:
+        slots = fec.host_alloc(npk * slot).reshape(npk, slot)
+        lens = fec.host_alloc(npk * 2).view(np.uint16)
+    else:
+        slots, lens = np.zeros((npk, slot), np.uint8), np.zeros(npk, np.uint16)
+    slots[:] = 0
+    for i, w in enumerate(enc):
+        slots[i, :len(w)] = np.frombuffer(w, np.uint8)
+        lens[i] = len(w)
+    want, masks, stats = _expected_placement(wire, G, n, S, pitch, first_group)
+    exp = np.ascontiguousarray(want[:, :, :S])
+    rc, exp_st = rs_ref.c_reconstruct(d, p, exp, masks, data_only=True)
+    lossy = [g for g in range(G) if (~int(masks[g])) & ((1 << d) - 1)]
+    codec = fec.New(d, p)
+    pres = np.zeros(G, np.uint64)
+    nrec, gidx, st, out, got_stats = codec.rx_recover_host(
+        slots, lens, S, G, first_group=first_group, pad=rc4_ref.keystream(KEY, slot) if encrypt else None,
+        max_out=max_out, present_out=pres)
+    assert nrec == len(lossy)
+    m = len(lossy) if max_out is None else min(max_out, len(lossy))
+    assert gidx[:m].tolist() == lossy[:m]
+    assert np.array_equal(pres, masks)
+    assert got_stats.tolist() == stats
+    for j, g in enumerate(lossy[:m]):
+        assert st[j] == exp_st[g], (j, g)
+        if exp_st[g] == 0:
+            lost = [r for r in range(d) if not (int(masks[g]) >> r) & 1]
+            for i, r in enumerate(lost):
+                assert np.array_equal(out[j, i, :S], exp[g, r]), (j, g, r)
+    if pinned:
+        fec.host_free(slots.reshape(-1))
+        fec.host_free(lens.view(np.uint8))
+
+
+@pytest.mark.gpu
 def test_rx_assemble_rejects_pageable_host_memory(gpu):
     """A ring the GPU cannot reach is refused up front, not faulted on."""
     codec = fec.New(10, 3)

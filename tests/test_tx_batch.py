@@ -111,6 +111,49 @@ def test_tx_assemble_vs_sender_loop(gpu, d, p, max_len, G, key, wrap):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("d,p,max_len,G,key,pinned", [
+    (10, 3, 1476, 97, KEY, True),    # headline geometry: >= 4 chunks over the 3 streams
+    (10, 3, 1476, 5, None, False),   # pageable buffers, one group per chunk
+    (5, 3, 700, 33, KEY, True),      # descriptor kernel
+])
+def test_tx_assemble_host_vs_sender_loop(gpu, d, p, max_len, G, key, pinned):
+    """ugo_fec_tx_assemble_host (host memory in and out, chunks pipelined over
+    three streams) against the restated sender loop, statuses included."""
+    n = d + p
+    enc = fec.New(d, p)
+    pk, lens = _batch(d, G, 300 + d + G, max_len)
+    slot = (max_len + 15) // 16 * 16
+    first_seq = 13 * n
+
+    def buf(shape, dtype):
+        if not pinned:
+            return np.zeros(shape, dtype)
+        a = fec.host_alloc(int(np.prod(shape)) * np.dtype(dtype).itemsize).view(dtype).reshape(shape)
+        a[:] = 0
+        return a
+
+    host = buf((G * d, slot), np.uint8)
+    for i, b in enumerate(pk):
+        host[i, :len(b)] = np.frombuffer(b, np.uint8)
+    hl = buf((G * d,), np.uint16)
+    hl[:] = lens
+    wire, wl, st = buf((G * n, slot), np.uint8), buf((G * n,), np.uint16), buf((G,), np.int8)
+    wire[:] = 0xAB
+    st[:] = -1
+    pad = None if key is None else fec.rc4_keystream(key, slot)
+    enc.tx_assemble_host(host, hl, wire, wl, first_seq=first_seq, pad=pad, max_len=max_len, status=st)
+    ref, _ = _oracle(d, p, pk, first_seq, key)
+    for i, w in enumerate(ref):
+        assert wl[i] == len(w), f"packet {i}: length {wl[i]} vs {len(w)}"
+        assert wire[i, :len(w)].tobytes() == w, f"packet {i} (group {i // n}, row {i % n}) differs"
+    nodata = [all(int(L) == 6 for L in lens[g * d:(g + 1) * d]) for g in range(G)]
+    assert list(st) == [fec.ErrShardNoData.code if x else 0 for x in nodata]
+    if pinned:
+        for a in (host, hl, wire, wl, st):
+            fec.host_free(a.reshape(-1).view(np.uint8))
+
+
+@pytest.mark.gpu
 def test_tx_assemble_bad_length_group_and_arguments(gpu):
     d, p, n = 10, 3, 13
     enc = fec.New(d, p)

@@ -536,6 +536,13 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
   return UGO_FEC_OK;
 }
 
+int ensure_streams(ugo_fec* c) {
+  for (int i = 0; i < kStreams; ++i)
+    if (!c->streams[i] && hipStreamCreateWithFlags(&c->streams[i], hipStreamNonBlocking) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
+  return UGO_FEC_OK;
+}
+
 int ensure_stage(ugo_fec* c, size_t pitch) {
   const size_t gbytes = size_t(c->n) * pitch;
   const size_t want = std::max<size_t>(1, kStageBytes / gbytes);
@@ -964,6 +971,103 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
   return UGO_FEC_OK;
 }
 
+// rx_assemble on device views (arguments checked by the caller).
+int rx_assemble_dev(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
+                    const uint8_t* pad, uint64_t first_group, size_t groups, uint8_t* shards, size_t S,
+                    size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats, hipStream_t s) {
+  ugo::kern::RxArgs a{};
+  a.wire = wire;
+  a.lens = lens;
+  a.pad = pad;
+  a.shards = shards;
+  a.present = present;
+  a.stats = stats;
+  a.npk = npk;
+  a.slot = slot_stride;
+  a.first_group = first_group;
+  a.groups = groups;
+  a.rstride = row_stride;
+  a.gstride = group_stride;
+  a.S = static_cast<uint32_t>(S);
+  a.n = static_cast<uint32_t>(c->n);
+  // First arrival in ring order wins (ugo/fec.go:123-129), optimistically
+  // (rx_kernels.hip): place everything, flag a (group, row) taken twice, and
+  // only then -- gated on the flag, on the device -- claim and re-place.
+  // scratch: presence snapshot [groups] u64 | claim words [groups][n] u32 | dup flag
+  const uint64_t words = groups * uint64_t(c->n);
+  void* scratch = nullptr;
+  int st = scratch_alloc(c, groups * sizeof(uint64_t) + (words + 16) * sizeof(uint32_t), s, &scratch);
+  if (st) return st;
+  uint64_t* prev = static_cast<uint64_t*>(scratch);
+  uint32_t* win = reinterpret_cast<uint32_t*>(prev + groups);
+  uint32_t* dup = win + words;
+  // call entry, one launch: dup = 0, the presence snapshot -- a (group, row)
+  // an earlier call placed keeps that call's copy (ugo/fec.go:123-129 keeps the
+  // first) -- the claim words, and whether any presence bit was set at all (if
+  // none was, the place pass skips its per-packet snapshot lookups)
+  const unsigned long long call = ++c->rx_calls;
+  st = hip_status(ugo::kern::launch_rx_begin(present, prev, groups, dup, win, words, c->d_rxseen, call, s));
+  a.dup = dup;
+  a.prev = prev;
+  a.seen = c->d_rxseen;
+  a.call = call;
+  ugo::kern::RxArgs f = a;  // the gated claim and re-place of the first copies
+  f.win = win;
+  f.gate = dup;
+  f.dup = nullptr;
+  f.stats = nullptr;
+  f.fixup = 1;
+  if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
+  if (!st) st = hip_status(ugo::kern::launch_rx_claim(f, s));
+  if (!st) st = hip_status(ugo::kern::launch_rx_scatter(f, s));
+  const int fr = scratch_free(c, scratch, s);
+  return st ? st : fr;
+}
+
+
+// ugo_fec_lossy_groups on device views.
+int lossy_list_dev(ugo_fec* c, const uint64_t* present, size_t groups, unsigned flags, uint32_t* list,
+                   uint32_t* count, hipStream_t s) {
+  if (groups == 0) return hip_status(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
+  const uint64_t nmask = c->n >= 64 ? ~0ull : ((1ull << c->n) - 1);
+  const uint64_t dmask = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? ((1ull << c->d) - 1) : ~0ull;
+  const size_t blocks = (groups + ugo::kern::kLossyPerBlock - 1) / ugo::kern::kLossyPerBlock;
+  void* work = nullptr;
+  int st = scratch_alloc(c, (blocks + 1) * sizeof(uint32_t), s, &work);
+  if (st) return st;
+  st = hip_status(ugo::kern::launch_lossy_list(present, groups, nmask, dmask, list, count,
+                                               static_cast<uint32_t*>(work), s));
+  const int fr = scratch_free(c, work, s);
+  return st ? st : fr;
+}
+
+// ugo_fec_reconstruct_list on device views (arguments checked by the caller).
+int reconstruct_list_dev(ugo_fec* c, const uint8_t* shards, const uint64_t* present, const uint32_t* list,
+                         const uint32_t* count, size_t max_entries, size_t S, const Layout& L, uint8_t* out,
+                         size_t out_row_stride, size_t out_entry_stride, unsigned flags, int8_t* status,
+                         hipStream_t s) {
+  ugo::kern::Batch a = base_batch(c, const_cast<uint8_t*>(shards), S, L);
+  a.out = out;
+  a.ogstride = out_entry_stride;
+  a.orstride = out_row_stride;
+  a.present = present;
+  a.status = status;
+  a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
+  a.chunks = static_cast<uint32_t>((S + 15) / 16);
+  a.desc = c->d_table;
+  a.list = list;
+  a.count = count;
+  const size_t per = slice_groups(a.chunks, true);
+  for (size_t g0 = 0; g0 < max_entries; g0 += per) {
+    const size_t gn = std::min(per, max_entries - g0);
+    a.g0 = g0;
+    a.items = static_cast<uint32_t>(gn * a.chunks);
+    if (ugo::kern::launch_apply_list(ugo::kern::apply_dmax(c->d), a, s) != hipSuccess) return UGO_FEC_ERR_HIP;
+  }
+  return UGO_FEC_OK;
+}
+
+
 }  // namespace
 
 extern "C" {
@@ -1167,18 +1271,7 @@ int ugo_fec_lossy_groups(ugo_fec* c, const uint64_t* present, size_t groups, uns
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
   if (!device_view(present) || !device_view(list) || !device_view(count)) return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
-  const hipStream_t s = static_cast<hipStream_t>(stream);
-  if (groups == 0) return hip_status(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
-  const uint64_t nmask = c->n >= 64 ? ~0ull : ((1ull << c->n) - 1);
-  const uint64_t dmask = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? ((1ull << c->d) - 1) : ~0ull;
-  const size_t blocks = (groups + ugo::kern::kLossyPerBlock - 1) / ugo::kern::kLossyPerBlock;
-  void* work = nullptr;
-  int st = scratch_alloc(c, (blocks + 1) * sizeof(uint32_t), s, &work);
-  if (st) return st;
-  st = hip_status(ugo::kern::launch_lossy_list(present, groups, nmask, dmask, list, count,
-                                               static_cast<uint32_t*>(work), s));
-  const int fr = scratch_free(c, work, s);
-  return st ? st : fr;
+  return lossy_list_dev(c, present, groups, flags, list, count, static_cast<hipStream_t>(stream));
 }
 
 int ugo_fec_reconstruct_list(ugo_fec* c, const uint8_t* shards, const uint64_t* present, size_t groups,
@@ -1208,26 +1301,8 @@ int ugo_fec_reconstruct_list(ugo_fec* c, const uint8_t* shards, const uint64_t* 
       !device_view(status) || !device_view(out))
     return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
-  const hipStream_t s = static_cast<hipStream_t>(stream);
-  ugo::kern::Batch a = base_batch(c, const_cast<uint8_t*>(shards), S, L);
-  a.out = out;
-  a.ogstride = out_entry_stride;
-  a.orstride = out_row_stride;
-  a.present = present;
-  a.status = status;
-  a.data_only = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? 1u : 0u;
-  a.chunks = static_cast<uint32_t>((S + 15) / 16);
-  a.desc = c->d_table;
-  a.list = list;
-  a.count = count;
-  const size_t per = slice_groups(a.chunks, true);
-  for (size_t g0 = 0; g0 < max_entries; g0 += per) {
-    const size_t gn = std::min(per, max_entries - g0);
-    a.g0 = g0;
-    a.items = static_cast<uint32_t>(gn * a.chunks);
-    if (ugo::kern::launch_apply_list(ugo::kern::apply_dmax(c->d), a, s) != hipSuccess) return UGO_FEC_ERR_HIP;
-  }
-  return UGO_FEC_OK;
+  return reconstruct_list_dev(c, shards, present, list, count, max_entries, S, L, out, out_row_stride,
+                              out_entry_stride, flags, status, static_cast<hipStream_t>(stream));
 }
 
 int ugo_fec_reconstruct(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
@@ -1427,54 +1502,8 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
       !device_view(present) || !device_view(stats))
     return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
-  ugo::kern::RxArgs a{};
-  a.wire = wire;
-  a.lens = lens;
-  a.pad = pad;
-  a.shards = shards;
-  a.present = present;
-  a.stats = stats;
-  a.npk = npk;
-  a.slot = slot_stride;
-  a.first_group = first_group;
-  a.groups = groups;
-  a.rstride = row_stride;
-  a.gstride = group_stride;
-  a.S = static_cast<uint32_t>(S);
-  a.n = static_cast<uint32_t>(c->n);
-  // First arrival in ring order wins (ugo/fec.go:123-129), optimistically
-  // (rx_kernels.hip): place everything, flag a (group, row) taken twice, and
-  // only then -- gated on the flag, on the device -- claim and re-place.
-  const hipStream_t s = static_cast<hipStream_t>(stream);
-  // scratch: presence snapshot [groups] u64 | claim words [groups][n] u32 | dup flag
-  const uint64_t words = groups * uint64_t(c->n);
-  void* scratch = nullptr;
-  int st = scratch_alloc(c, groups * sizeof(uint64_t) + (words + 16) * sizeof(uint32_t), s, &scratch);
-  if (st) return st;
-  uint64_t* prev = static_cast<uint64_t*>(scratch);
-  uint32_t* win = reinterpret_cast<uint32_t*>(prev + groups);
-  uint32_t* dup = win + words;
-  // call entry, one launch: dup = 0, the presence snapshot -- a (group, row)
-  // an earlier call placed keeps that call's copy (ugo/fec.go:123-129 keeps the
-  // first) -- the claim words, and whether any presence bit was set at all (if
-  // none was, the place pass skips its per-packet snapshot lookups)
-  const unsigned long long call = ++c->rx_calls;
-  st = hip_status(ugo::kern::launch_rx_begin(present, prev, groups, dup, win, words, c->d_rxseen, call, s));
-  a.dup = dup;
-  a.prev = prev;
-  a.seen = c->d_rxseen;
-  a.call = call;
-  ugo::kern::RxArgs f = a;  // the gated claim and re-place of the first copies
-  f.win = win;
-  f.gate = dup;
-  f.dup = nullptr;
-  f.stats = nullptr;
-  f.fixup = 1;
-  if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
-  if (!st) st = hip_status(ugo::kern::launch_rx_claim(f, s));
-  if (!st) st = hip_status(ugo::kern::launch_rx_scatter(f, s));
-  const int fr = scratch_free(c, scratch, s);
-  return st ? st : fr;
+  return rx_assemble_dev(c, wire, slot_stride, lens, npk, pad, first_group, groups, shards, S, row_stride,
+                         group_stride, present, stats, static_cast<hipStream_t>(stream));
 }
 
 int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const uint16_t* lens, size_t groups,
@@ -1523,6 +1552,202 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
     const int st = hip_status(ugo::kern::launch_tx_assemble(dmax, a, static_cast<hipStream_t>(stream)));
     if (st != UGO_FEC_OK) return st;
   }
+  return UGO_FEC_OK;
+}
+
+// ---- host-memory RX and TX paths ---------------------------
+// The whole RX path from host memory to host memory: a received packet ring in
+// pinned memory (a recvmmsg batch) is copied to the device in chunks on two
+// copy streams, each chunk assembled (rx_assemble_dev, one call per chunk into
+// one batch: first copy wins across the calls) on a third stream as soon as its
+// copy lands, so copies and kernels overlap; then the lossy-group list, the
+// data-only Reconstruct of those groups into a compact output, and the D2H of
+// the recovered rows only.
+int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
+                            const uint8_t* pad, uint64_t first_group, size_t groups, size_t S, uint64_t* present_out,
+                            uint32_t* stats_out, uint8_t* out, size_t out_row_stride, size_t max_out,
+                            uint32_t* out_groups, int8_t* out_status, size_t* n_out) {
+  if (!c || !n_out) return UGO_FEC_ERR_INVALID_ARG;
+  *n_out = 0;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
+  if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
+  if (groups == 0) return UGO_FEC_OK;
+  if ((npk && (!wire || !lens)) || c->n > 16 || !c->d_table || groups >= 0xffffffffull || npk >= 0xffffffffull ||
+      slot_stride % 16 || slot_stride < 16 || S > 0xffffffffu || out_row_stride < S ||
+      (max_out && (!out || !out_groups)))
+    return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  TimerScope ts(c);
+  int st = ensure_streams(c);
+  if (st) return st;
+  const hipStream_t s0 = c->streams[0];  // assembly and recovery; copies on streams 1 and 2
+  const size_t n = size_t(c->n), pitch = round_up(S, 16), slots = size_t(std::min(c->d, c->p));
+  // packets per chunk: at most a 64-MiB stage, and at least 4 chunks so copies and assembly overlap
+  const size_t cpk = std::max<size_t>(1, std::min((npk + 3) / 4, kStageBytes / slot_stride));
+  const size_t lens_off = round_up(cpk * slot_stride, 256);
+  const size_t stage_bytes = lens_off + round_up(cpk * sizeof(uint16_t), 256);
+  const size_t mo = std::min(max_out, groups);
+  // one scratch block: batch | present | list | count, stats | status | outputs | pad | 2 ring stages
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off = round_up(off + bytes, 256); return o; };
+  const size_t o_batch = take(n * groups * pitch), o_pres = take(groups * 8), o_list = take(groups * 4),
+               o_ctl = take(64), o_stat = take(groups), o_out = take(std::max<size_t>(mo, 1) * slots * pitch),
+               o_pad = take(pad ? slot_stride : 16), o_stage = take(2 * stage_bytes);
+  uint8_t* base = nullptr;
+  st = scratch_alloc(c, off, s0, reinterpret_cast<void**>(&base));
+  if (st) return st;
+  struct Release {
+    ugo_fec* c;
+    uint8_t* p;
+    hipStream_t s;
+    ~Release() { (void)scratch_free(c, p, s); }
+  } release{c, base, s0};
+  uint8_t* batch = base + o_batch;
+  uint64_t* dpres = reinterpret_cast<uint64_t*>(base + o_pres);
+  uint32_t* dlist = reinterpret_cast<uint32_t*>(base + o_list);
+  uint32_t* dcount = reinterpret_cast<uint32_t*>(base + o_ctl);
+  uint32_t* dstats = dcount + 4;
+  int8_t* dstat = reinterpret_cast<int8_t*>(base + o_stat);
+  uint8_t* dout = base + o_out;
+  uint8_t* dpad = pad ? base + o_pad : nullptr;
+  hipEvent_t ev[4] = {};  // full[0..1]: a stage's copy landed; free[0..1]: its assembly is done
+  struct Events {
+    hipEvent_t* e;
+    ~Events() {
+      for (int i = 0; i < 4; ++i)
+        if (e[i]) (void)hipEventDestroy(e[i]);
+    }
+  } evs{ev};
+  for (int i = 0; i < 4; ++i)
+    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return UGO_FEC_ERR_HIP;
+  if (hipMemsetAsync(dpres, 0, groups * 8, s0) != hipSuccess || hipMemsetAsync(dcount, 0, 64, s0) != hipSuccess ||
+      (pad && hipMemcpyAsync(dpad, pad, slot_stride, hipMemcpyHostToDevice, s0) != hipSuccess))
+    return UGO_FEC_ERR_HIP;
+  // the copy streams start after the zeroing (their stages are this call's scratch)
+  if (hipEventRecord(ev[2], s0) != hipSuccess || hipEventRecord(ev[3], s0) != hipSuccess) return UGO_FEC_ERR_HIP;
+  for (size_t p0 = 0, k = 0; p0 < npk; p0 += cpk, ++k) {
+    const size_t m = std::min(cpk, npk - p0);
+    const int b = static_cast<int>(k & 1);
+    const hipStream_t cs = c->streams[1 + b];
+    uint8_t* sw = base + o_stage + b * stage_bytes;
+    uint16_t* sl = reinterpret_cast<uint16_t*>(sw + lens_off);
+    if (hipStreamWaitEvent(cs, ev[2 + b], 0) != hipSuccess ||
+        hipMemcpyAsync(sw, wire + p0 * slot_stride, m * slot_stride, hipMemcpyHostToDevice, cs) != hipSuccess ||
+        hipMemcpyAsync(sl, lens + p0, m * sizeof(uint16_t), hipMemcpyHostToDevice, cs) != hipSuccess ||
+        hipEventRecord(ev[b], cs) != hipSuccess || hipStreamWaitEvent(s0, ev[b], 0) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
+    st = rx_assemble_dev(c, sw, slot_stride, sl, m, dpad, first_group, groups, batch, S, groups * pitch, pitch, dpres,
+                         dstats, s0);
+    if (st) return st;
+    if (hipEventRecord(ev[2 + b], s0) != hipSuccess) return UGO_FEC_ERR_HIP;
+  }
+  st = lossy_list_dev(c, dpres, groups, UGO_FEC_RECONSTRUCT_DATA_ONLY, dlist, dcount, s0);
+  if (st) return st;
+  if (mo) {
+    st = reconstruct_list_dev(c, batch, dpres, dlist, dcount, mo, S, Layout{groups * pitch, pitch}, dout, pitch,
+                              slots * pitch, UGO_FEC_RECONSTRUCT_DATA_ONLY, dstat, s0);
+    if (st) return st;
+  }
+  uint32_t hcnt[8] = {};
+  if (hipMemcpyAsync(hcnt, dcount, 32, hipMemcpyDeviceToHost, s0) != hipSuccess || hipStreamSynchronize(s0) != hipSuccess)
+    return UGO_FEC_ERR_HIP;
+  const size_t total = hcnt[0], w = std::min<size_t>(total, mo);
+  *n_out = total;
+  hipError_t e = hipSuccess;
+  if (w) {
+    e = hipMemcpyAsync(out_groups, dlist, w * 4, hipMemcpyDeviceToHost, s0);
+    if (e == hipSuccess && out_status) e = hipMemcpyAsync(out_status, dstat, w, hipMemcpyDeviceToHost, s0);
+    if (e == hipSuccess)
+      e = hipMemcpy2DAsync(out, out_row_stride, dout, pitch, S, w * slots, hipMemcpyDeviceToHost, s0);
+  }
+  if (e == hipSuccess && present_out) e = hipMemcpyAsync(present_out, dpres, groups * 8, hipMemcpyDeviceToHost, s0);
+  if (e == hipSuccess && stats_out) e = hipMemcpyAsync(stats_out, dstats, 20, hipMemcpyDeviceToHost, s0);
+  if (e == hipSuccess) e = hipStreamSynchronize(s0);
+  return hip_status(e);
+}
+
+// The TX path from host memory to host memory: groups in chunks, each chunk's
+// data packets H2D -> tx_assemble -> wire packets D2H on one of the context's
+// three streams, chunks round-robin, so the copies in both directions and the
+// kernels of different chunks overlap.
+int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const uint16_t* lens, size_t groups,
+                             uint32_t first_seq, const uint8_t* pad, size_t max_len, uint8_t* wire, size_t slot_out,
+                             uint16_t* wire_lens, int8_t* status) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
+  if (groups == 0) return UGO_FEC_OK;
+  const uint64_t n = static_cast<uint64_t>(c->n), d = static_cast<uint64_t>(c->d);
+  const uint32_t paws = static_cast<uint32_t>((0xffffffffull / n - 1) * n);  // ugo/fec.go:58
+  const size_t need = round_up(max_len, 16);
+  if (!pkts || !lens || !wire || !wire_lens || c->d > 32 || max_len < 6 || max_len > 0xffff || slot_in % 16 ||
+      slot_out % 16 || slot_in < need || slot_out < need || first_seq % n || first_seq >= paws)
+    return UGO_FEC_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  TimerScope ts(c);
+  int st = ensure_streams(c);
+  if (st) return st;
+  const size_t per_group = d * slot_in + n * slot_out;
+  const size_t cg = std::max<size_t>(1, std::min((groups + 3) / 4, kStageBytes / per_group));  // >= 4 chunks
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off = round_up(off + bytes, 256); return o; };
+  const size_t o_in = take(cg * d * slot_in), o_lens = take(cg * d * 2), o_wire = take(cg * n * slot_out),
+               o_wl = take(cg * n * 2), o_st = take(cg), o_pad = take(pad ? need : 16);
+  uint8_t* buf[kStreams] = {};
+  struct Release {
+    ugo_fec* c;
+    uint8_t** b;
+    ~Release() {
+      for (int i = 0; i < kStreams; ++i)
+        if (b[i]) (void)scratch_free(c, b[i], c->streams[i]);
+    }
+  } release{c, buf};
+  for (int i = 0; i < kStreams; ++i) {
+    st = scratch_alloc(c, off, c->streams[i], reinterpret_cast<void**>(&buf[i]));
+    if (st) return st;
+    if (pad && hipMemcpyAsync(buf[i] + o_pad, pad, need, hipMemcpyHostToDevice, c->streams[i]) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
+  }
+  ugo::kern::TxArgs a{};
+  a.desc = c->d_encdesc;
+  a.slot_in = slot_in;
+  a.slot_out = slot_out;
+  a.paws = paws;
+  a.max_len = static_cast<uint32_t>(max_len);
+  a.chunks = static_cast<uint32_t>(need / 16);
+  a.d = static_cast<uint32_t>(c->d);
+  a.p = static_cast<uint32_t>(c->p);
+  a.dpad = c->dpad;
+  a.epad = c->epad;
+  const int dmax = ugo::kern::has_const_encode(c->d, c->p) ? 0 : ugo::kern::apply_dmax(c->d);
+  size_t k = 0;
+  for (size_t g0 = 0; g0 < groups; g0 += cg, ++k) {
+    const size_t gn = std::min(cg, groups - g0);
+    const int si = static_cast<int>(k % kStreams);
+    const hipStream_t s = c->streams[si];
+    uint8_t* b = buf[si];
+    if (hipMemcpyAsync(b + o_in, pkts + g0 * d * slot_in, gn * d * slot_in, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(b + o_lens, lens + g0 * d, gn * d * 2, hipMemcpyHostToDevice, s) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
+    a.pkts = b + o_in;
+    a.lens = reinterpret_cast<const uint16_t*>(b + o_lens);
+    a.pad = pad ? b + o_pad : nullptr;
+    a.wire = b + o_wire;
+    a.wire_lens = reinterpret_cast<uint16_t*>(b + o_wl);
+    a.status = status ? reinterpret_cast<int8_t*>(b + o_st) : nullptr;
+    a.first_seq = static_cast<uint32_t>((uint64_t(first_seq) + uint64_t(g0) * n) % paws);
+    a.g0 = 0;
+    a.groups = gn;
+    if (ugo::kern::launch_tx_assemble(dmax, a, s) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (hipMemcpyAsync(wire + g0 * n * slot_out, b + o_wire, gn * n * slot_out, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipMemcpyAsync(wire_lens + g0 * n, b + o_wl, gn * n * 2, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (status && hipMemcpyAsync(status + g0, b + o_st, gn, hipMemcpyDeviceToHost, s) != hipSuccess))
+      return UGO_FEC_ERR_HIP;
+  }
+  for (int i = 0; i < kStreams; ++i)
+    if (hipStreamSynchronize(c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
   return UGO_FEC_OK;
 }
 
