@@ -101,11 +101,12 @@ def parse(argv=None):
                          "ranks (contiguous ranges), one cold batch per rank; 0 = off")
     ap.add_argument("--c4-steps", type=int, default=10, help="timed steps of the strong leg")
     ap.add_argument("--no-host-path", action="store_true",
-                    help="skip the PCIe-inclusive host_path leg (N = 1): pinned-host encode / reconstruct of "
-                         "(10+3)x1350 x 65,536 and (32+8)x9000 x 8,192 groups")
+                    help="skip the PCIe-inclusive host_path leg (every rank, NUMA-bound): pinned-host encode / "
+                         "reconstruct of (10+3)x1350 x 65,536 and (32+8)x9000 x 8,192 groups, the host-memory RX "
+                         "and TX paths, the PCIe ceilings (and, at N = 1, the per-call leg)")
     ap.add_argument("--no-rx-tx", action="store_true",
-                    help="skip the rx_tx leg (N = 1): RX / TX assembly, data-only recovery and packet decode "
-                         "kernels with their nt-copy ceilings")
+                    help="skip the rx_tx leg (every rank): RX / TX assembly, data-only recovery and packet decode "
+                         "kernels with their ceilings")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py)")
@@ -737,6 +738,10 @@ def host_path_leg(args, dev_index, rank=0, world=1, reps=3):
                     fec.host_free(raw)
                 if enc is not None:
                     enc.close()
+        # the RX and TX paths from host memory to host memory, same binding
+        rxtx, ok_rxtx = host_rxtx_cases(args, dev_index, rank, world, reps)
+        res.update(rxtx)
+        all_ok = all_ok and ok_rxtx
     finally:
         try:
             os.sched_setaffinity(0, saved)
@@ -752,6 +757,208 @@ def host_path_leg(args, dev_index, rank=0, world=1, reps=3):
                    "= bytes crossing PCIe (encode: d padded rows in + p rows out, staged; reconstruct: d survivor "
                    "rows in + e rows out, zero-copy); bound: sum of per-GPU PCIe links and host DRAM (DESIGN.md §6)")
     return res
+
+
+def pcie_ceiling(dev, world, nbytes=1 << 30, reps=3):
+    """The per-GPU PCIe ceiling measured in this run, every rank at once (each
+    rep starts at a barrier, max over ranks): a pinned host buffer copied to
+    the device, back, and both directions at once on two streams (hipMemcpyAsync
+    DMA through torch).  GB/s are per GPU."""
+    import torch
+
+    from ugo_amd import fec
+
+    raw = [fec.host_alloc(nbytes), fec.host_alloc(nbytes)]
+    try:
+        h = [torch.from_numpy(x) for x in raw]
+        dbuf = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+        s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+        def h2d():
+            with torch.cuda.stream(s1):
+                dbuf[0].copy_(h[0], non_blocking=True)
+            s1.synchronize()
+
+        def d2h():
+            with torch.cuda.stream(s1):
+                h[0].copy_(dbuf[0], non_blocking=True)
+            s1.synchronize()
+
+        def both():
+            with torch.cuda.stream(s1):
+                dbuf[0].copy_(h[0], non_blocking=True)
+            with torch.cuda.stream(s2):
+                h[1].copy_(dbuf[1], non_blocking=True)
+            s1.synchronize()
+            s2.synchronize()
+
+        out = {}
+        for name, fn, mult in (("h2d", h2d, 1), ("d2h", d2h, 1), ("bidirectional", both, 2)):
+            fn()
+            t, _ = timed_reps(fn, reps, world)
+            out[name + "_GBps"] = round(mult * nbytes / t / 1e9, 2)
+        out["note"] = f"{nbytes >> 20} MiB pinned <-> device per copy, every rank at once, max over ranks, per GPU"
+        del dbuf
+        return out
+    finally:
+        for x in raw:
+            fec.host_free(x)
+
+
+def host_rxtx_cases(args, dev_index, rank, world, reps):
+    """The host-memory RX and TX paths (include/ugo_fec.h
+    ugo_fec_rx_recover_host / ugo_fec_tx_assemble_host), on every rank at once,
+    pinned buffers allocated after the NUMA binding:
+      * RX (ugo/listener.go:48 -> ugo/conn.go:387-406 -> ugo/fec.go:107-226): a
+        recvmmsg-shaped ring of 65,536 (10+3) groups minus 5 % uniform loss,
+        in seqid order, 1476-B RC4 packets in 1488-B slots plus uint16 lengths,
+        in; the lost data shards of every lossy group out (compact);
+      * TX (ugo/conn.go:643-685, :634): 65,536 groups of 10 full 1476-B data
+        packets in 1488-B slots in; 13 RC4 wire packets per group out.
+    Each call: 1 untimed, `reps` timed (barrier, max over ranks, median).
+    Verified against the device-resident path on the same inputs.  wire_GBps =
+    all ranks' wire bytes (RX: packets received; TX: packets sent) / time;
+    pcie_GBps = bytes crossing this GPU's link / time, beside the measured
+    per-GPU ceiling."""
+    import numpy as np
+    import torch
+
+    from ugo_amd import fec
+
+    d, p, n, S, pitch, slot, G = 10, 3, 13, 1470, 1472, 1488, 65536
+    dev = torch.device("cuda", dev_index)
+    res, ok_all = {}, True
+    st = {"err": None}
+
+    def guarded(fn):
+        def g():
+            if st["err"] is None:
+                try:
+                    fn()
+                except Exception as ex:  # noqa: BLE001
+                    st["err"] = repr(ex)[:200]
+        return g
+
+    try:
+        res["pcie_ceiling"] = pcie_ceiling(dev, world)
+    except Exception as ex:  # noqa: BLE001
+        res["pcie_ceiling"] = {"error": repr(ex)[:200]}
+    pad_b = fec.rc4_keystream(b"1234567890123456", slot)
+    pad = torch.frombuffer(bytearray(pad_b), dtype=torch.uint8).to(dev)
+    enc = fec.New(d, p, device=dev_index)
+    bufs = []
+    try:
+        # ---- RX
+        box = {}
+
+        def rx_setup():
+            gen = torch.Generator(device=dev).manual_seed(args.seed + 0x5B + 7919 * rank)
+            seq = torch.arange(G * n, device=dev, dtype=torch.int64)
+            seq = seq[torch.rand(G * n, device=dev, generator=gen) >= 0.05]
+            npk = seq.numel()
+            w = torch.randint(0, 256, (npk, slot), dtype=torch.uint8, device=dev, generator=gen)
+            hdr = torch.zeros((npk, 6), dtype=torch.uint8, device=dev)
+            for b in range(4):
+                hdr[:, b] = ((seq >> (8 * b)) & 0xFF).to(torch.uint8)
+            hdr[:, 4] = torch.where(seq % n < d, 0xF1, 0xF2).to(torch.uint8)
+            w[:, :6] = hdr ^ pad[:6]
+            ring = fec.host_alloc(npk * slot).reshape(npk, slot)
+            lens = fec.host_alloc(npk * 2).view(np.uint16)
+            out = fec.host_alloc(G * p * pitch).reshape(G, p, pitch)
+            bufs.extend([ring, lens.view(np.uint8), out])
+            torch.from_numpy(ring).copy_(w)
+            lens[:] = 1476
+            box.update(ring=ring, lens=lens, out=out, npk=npk, dring=w)
+
+        def rx_call():
+            box["r"] = enc.rx_recover_host(box["ring"], box["lens"], S, G, pad=pad_b, out=box["out"], max_out=G)
+
+        guarded(rx_setup)()
+        guarded(rx_call)()
+        t_rx, t_rx_mine = timed_reps(guarded(rx_call), reps, world)
+        ok = False
+        if st["err"] is None:
+            # reference: the device-resident path on the same ring
+            bat = torch.empty((n, G, pitch), dtype=torch.uint8, device=dev)
+            pr = torch.zeros(G, dtype=torch.int64, device=dev)
+            enc.rx_assemble(box["dring"], torch.from_numpy(box["lens"].view(np.int16)).to(dev), bat, pr,
+                            shard_size=S, pad=pad)
+            lst, cnt = enc.lossy_groups(pr, data_only=True)
+            lo = torch.empty((G, p, pitch), dtype=torch.uint8, device=dev)
+            enc.reconstruct_list(bat, pr, lst, cnt, lo, shard_size=S, data_only=True)
+            k = int(cnt.item())
+            nrec, gidx, status, out, _ = box["r"]
+            ok = nrec == k and bool(np.array_equal(gidx[:k], lst[:k].cpu().numpy().view(np.uint32)))
+            if ok:
+                pm = pr[lst[:k].long()]
+                ed = torch.zeros(k, dtype=torch.int64, device=dev)
+                for r in range(d):
+                    ed += ((pm >> r) & 1) == 0
+                ho = torch.from_numpy(out[:k]).to(dev)
+                for i in range(p):
+                    sel = ed > i
+                    ok = ok and bool(torch.equal(ho[sel, i, :S], lo[:k][sel, i, :S]))
+            del bat, pr, lo
+        ok_all = ok_all and ok
+        npk = box.get("npk", 0)
+        nrec = box["r"][0] if "r" in box else 0
+        wire_bytes = int(reduce_sum([npk * 1476], world)[0])
+        pcie = npk * (slot + 2) + nrec * p * S
+        res["rx_host"] = {
+            "groups_per_rank": G, "packets_per_rank": npk, "loss": 0.05, "rc4": True, "lossy_groups_rank0": nrec,
+            "rx_ms": round(t_rx * 1e3, 3), "wire_GBps": round(wire_bytes / t_rx / 1e9, 2),
+            "pcie_GBps_per_gpu": round(pcie / t_rx / 1e9, 2), "rank0_alone_ms": round(t_rx_mine * 1e3, 3),
+            "verify_vs_device_path": ok,
+            "path": "pinned ring -> H2D in >= 4 chunks on 2 copy streams, each chunk assembled as it lands -> "
+                    "lossy-group list -> data-only list reconstruct -> D2H of the recovered shards only"}
+        box.clear()
+        # ---- TX
+        tb = {}
+
+        def tx_setup():
+            gen = torch.Generator(device=dev).manual_seed(args.seed + 0x7C + 7919 * rank)
+            dp = torch.randint(0, 256, (G * d, slot), dtype=torch.uint8, device=dev, generator=gen)
+            pk = fec.host_alloc(G * d * slot).reshape(G * d, slot)
+            ln = fec.host_alloc(G * d * 2).view(np.uint16)
+            wire = fec.host_alloc(G * n * slot).reshape(G * n, slot)
+            wl = fec.host_alloc(G * n * 2).view(np.uint16)
+            bufs.extend([pk, ln.view(np.uint8), wire, wl.view(np.uint8)])
+            torch.from_numpy(pk).copy_(dp)
+            ln[:] = 1476
+            tb.update(pk=pk, ln=ln, wire=wire, wl=wl, dp=dp)
+
+        def tx_call():
+            enc.tx_assemble_host(tb["pk"], tb["ln"], tb["wire"], tb["wl"], pad=pad_b, max_len=1476)
+
+        guarded(tx_setup)()
+        guarded(tx_call)()
+        t_tx, t_tx_mine = timed_reps(guarded(tx_call), reps, world)
+        ok = False
+        if st["err"] is None:
+            dw = torch.empty((G * n, slot), dtype=torch.uint8, device=dev)
+            dwl = torch.empty(G * n, dtype=torch.int16, device=dev)
+            enc.tx_assemble(tb["dp"], torch.from_numpy(tb["ln"].view(np.int16)).to(dev), dw, dwl, pad=pad,
+                            max_len=1476)
+            ok = bool(torch.equal(torch.from_numpy(tb["wire"]).to(dev)[:, :1476], dw[:, :1476])) and bool(
+                np.array_equal(tb["wl"], dwl.cpu().numpy().view(np.uint16)))
+            del dw, dwl
+        ok_all = ok_all and ok
+        res["tx_host"] = {
+            "groups_per_rank": G, "packets_out_per_rank": G * n, "rc4": True, "tx_ms": round(t_tx * 1e3, 3),
+            "wire_GBps": round(world * G * n * 1476 / t_tx / 1e9, 2),
+            "pcie_GBps_per_gpu": round(G * (d + n) * slot / t_tx / 1e9, 2), "rank0_alone_ms": round(t_tx_mine * 1e3, 3),
+            "verify_vs_device_path": ok,
+            "path": "pinned data packets -> H2D -> tx_assemble -> D2H of the wire packets, >= 4 group chunks "
+                    "round-robin over 3 streams"}
+        tb.clear()
+        if st["err"]:
+            res["rxtx_error_rank0"] = st["err"]
+    finally:
+        for b in bufs:
+            fec.host_free(b)
+        enc.close()
+        torch.cuda.empty_cache()
+    return res, ok_all and st["err"] is None
 
 
 def timed_reps(call, reps, world):
@@ -950,7 +1157,29 @@ def probe_library():
     lib.ugo_probe_encode_twin.argtypes = [vp, i, sz, sz, sz, sz, i, vp, vp]
     lib.ugo_probe_nt_copy.argtypes = [vp, vp, i, sz, i, vp, vp]
     lib.ugo_probe_reconstruct_twin.argtypes = [vp, vp, i, vp, sz, sz, sz, sz, sz, sz, i, vp, vp]
+    lib.ugo_probe_recover_twin.argtypes = [vp, vp, vp, vp, vp, i, sz, sz, sz, sz, sz, sz, i, ctypes.c_uint32, i, vp,
+                                           vp]
     return lib
+
+
+def probe_recover_twin_ms(bases, outs, presents, lists, counts, G, S, pitch, rs, ors, oes, reps, stream):
+    """Average duration of the RX-path recovery's compute-free twin
+    (k_recover_twin, libugoprobe): data only, the full grid (lists None) or the
+    list form; launch r on buffer set r % n."""
+    import ctypes
+
+    import numpy as np
+
+    lib = probe_library()
+    nb = len(bases)
+    arr = lambda xs: (ctypes.c_void_p * nb)(*[x.data_ptr() for x in xs])  # noqa: E731
+    ms = np.zeros(reps, np.float32)
+    rc = lib.ugo_probe_recover_twin(arr(bases), arr(outs), arr(presents), None if lists is None else arr(lists),
+                                    None if counts is None else arr(counts), nb, G, S, pitch, rs, ors, oes, 1,
+                                    36 * 1024, reps, stream, ms.ctypes.data)
+    if rc:
+        raise RuntimeError(f"ugo_probe_recover_twin failed ({rc})")
+    return float(ms[1:].mean()) if reps > 1 else float(ms[0])
 
 
 def probe_nt_copy_ms(srcs, dsts, nbytes, reps, stream):
@@ -1025,16 +1254,21 @@ def rc4_pad(nbytes, dev):
 
 
 def rx_tx_leg(args, dev_index, reps=12):
-    """The §8f kernels on the driver's clock, N = 1, after
-    the main line (nothing here feeds `value`).  Device-resident, cold: every
-    call alternates between 2 copies of its inputs and outputs.
+    """The §8f kernels on the driver's clock, on every rank
+    (rank 0 reports its own leg plus the max over ranks of
+    each kernel time), after the main line (nothing here feeds `value`).
+    Device-resident, cold: every call alternates between 2 copies of its
+    inputs and outputs.
       * rx_assemble (ugo/conn.go:387-406 decrypt, ugo/fec.go:78-89 decode,
         :107-175 grouping / dedupe / placement): a ring of 65,536 (10+3) groups
         minus 5% uniform loss, 1476-B packets in 1488-B slots, RC4, into a
         planar [13][G][1472] batch (S = 1470); arrival in seqid order (what a
         UDP flow mostly delivers) and shuffled (worst case);
       * reconstruct_into, data only, of the lossy groups of that batch
-        (input's Reconstruct, ugo/fec.go:196-207);
+        (input's Reconstruct, ugo/fec.go:196-207), over every group, and its
+        list form (lossy_groups + reconstruct_list: only the lossy groups,
+        compact outputs), each beside its compute-free twin (the same loads
+        and stores, XOR instead of the GF products) on the same buffers;
       * tx_assemble (ugo/conn.go:643-685 sender loop + :634 encrypt): 65,536
         groups of 10 full 1476-B packets -> 13 wire packets each, RC4;
       * packet_decode (ugo/packet.go:138-177 after conn.go:387-419): 851,968
@@ -1137,6 +1371,38 @@ def rx_tx_leg(args, dev_index, reps=12):
         recoverable = (lost_data > 0) & (pop >= d)
         rec_bytes = int((recoverable * (d + lost_data)).sum()) * S
         rx_bytes = npk * (1476 + S)
+        # the list form: lossy-group list + list reconstruct, compact outputs
+        lsts = [torch.empty(G, dtype=torch.int32, device=dev) for _ in range(2)]
+        cnts = [torch.empty(1, dtype=torch.int32, device=dev) for _ in range(2)]
+        louts = [torch.empty((G, p, pitch), dtype=torch.uint8, device=dev) for _ in range(2)]
+
+        def rec_list(r):
+            i = r % 2
+            enc.lossy_groups(pres[i], data_only=True, out=lsts[i], count=cnts[i])
+            enc.reconstruct_list(bats[i], pres[i], lsts[i], cnts[i], louts[i], shard_size=S, data_only=True)
+
+        for r in range(4):
+            rx(r)
+            rec(r)
+            rec_list(r)
+        torch.cuda.synchronize()
+        # the two forms agree: entry j's slot i = group lst[j]'s output i of reconstruct_into
+        k = int(cnts[0].item())
+        lg = lsts[0][:k].long()
+        ed = torch.zeros(k, dtype=torch.int64, device=dev)
+        pm = pres[0][lg]
+        for r in range(d):
+            ed += ((pm >> r) & 1) == 0
+        ok_list = k == int((lost_data > 0).sum())
+        for i in range(p):
+            sel = ed > i
+            ok_list = ok_list and bool(torch.equal(louts[0][:k][sel, i, :S], outs[0][i, lg[sel], :S]))
+        rec_list_k = kernel_ms(rec_list, fec.KERNEL_IDS["reconstruct"], reps)
+        # ceilings: the compute-free twins of both forms on the same buffers (after the checks: wrong bytes)
+        twin_ms = probe_recover_twin_ms(bats, outs, pres, None, None, G, S, pitch, bats[0].stride(0),
+                                        outs[0].stride(0), outs[0].stride(1), reps, stream.cuda_stream)
+        ltwin_ms = probe_recover_twin_ms(bats, louts, pres, lsts, cnts, G, S, pitch, bats[0].stride(0),
+                                         louts[0].stride(1), louts[0].stride(0), reps, stream.cuda_stream)
         cb = min(rx_bytes // 2, rings[0].numel(), bats[0].numel())  # each copy stays inside both buffers
         copy_ms = probe_nt_copy_ms([rings[i].data_ptr() for i in range(2)], [bats[(i + 1) % 2].data_ptr()
                                                                             for i in range(2)],
@@ -1150,8 +1416,13 @@ def rx_tx_leg(args, dev_index, reps=12):
             "rx_frac_of_copy": round(copy_ms / rx_k, 4),
             "recover_lossy_groups": int(recoverable.sum()), "reconstruct_into_data_only_ms": round(rec_k, 4),
             "reconstruct_GBps": round(rec_bytes / (rec_k * 1e-3) / 1e9, 1), "reconstruct_frac": frac(rec_bytes, rec_k),
+            "reconstruct_twin_ms": round(twin_ms, 4), "reconstruct_frac_of_ceiling": round(twin_ms / rec_k, 4),
+            "reconstruct_list_ms": round(rec_list_k, 4), "reconstruct_list_frac": frac(rec_bytes, rec_list_k),
+            "reconstruct_list_twin_ms": round(ltwin_ms, 4),
+            "reconstruct_list_frac_of_ceiling": round(ltwin_ms / rec_list_k, 4),
+            "recovery_faster": "list" if rec_list_k < rec_k else "into", "verify_list_eq_into": ok_list,
             "stats": stats, "verify_spot_4096": ok}
-        del rings, bats, pres, outs
+        del rings, bats, pres, outs, lsts, cnts, louts
         torch.cuda.empty_cache()
 
     # ---- TX
@@ -1195,6 +1466,28 @@ def rx_tx_leg(args, dev_index, reps=12):
                    "bytes on the same cold buffers; rx_wall includes the caller's present.zero_() per call")
     enc.close()
     return out
+
+
+def rx_tx_over_ranks(mine, legs):
+    """Rank 0's rx_tx leg with, for every kernel time of it (keys ending in
+    _ms), the max over the ranks' legs (`max_over_ranks`) and each rank's
+    value (`per_rank`)."""
+    def times(d, pre=""):
+        out = {}
+        for k, v in (d or {}).items():
+            if isinstance(v, dict):
+                out.update(times(v, pre + k + "."))
+            elif k.endswith("_ms") and isinstance(v, (int, float)):
+                out[pre + k] = v
+        return out
+
+    per = [times(x) for x in legs]
+    keys = sorted(set().union(*per)) if per else []
+    res = dict(mine)
+    res["max_over_ranks"] = {k: max(t.get(k, 0.0) for t in per) for k in keys}
+    res["per_rank"] = [{k: t.get(k) for k in keys} for t in per]
+    res["ranks"] = len(legs)
+    return res
 
 
 def packet_decode_case(enc, dev, reps, kernel_ms, npk=851968):
@@ -1395,11 +1688,13 @@ def run_rank(args):
             per_call = per_call_leg(args, dev_index)
         except Exception as ex:  # noqa: BLE001
             per_call = {"error": repr(ex)[:300]}
-    if world == 1 and not args.no_rx_tx:
-        try:
+    if not args.no_rx_tx:
+        try:  # every rank (device-local work): rank 0's leg plus the max over ranks of each kernel time
             rx_tx = rx_tx_leg(args, dev_index)
         except Exception as ex:  # noqa: BLE001
             rx_tx = {"error": repr(ex)[:300]}
+        if world > 1:
+            rx_tx = rx_tx_over_ranks(rx_tx, gather_objects(rx_tx, world))
 
     if rank == 0:
         payload = G * d * S  # klauspost's convention: data bytes per call (BASELINE.md secondary column)

@@ -63,6 +63,10 @@ def main():
         placement = bench.gather_objects({"rank": rank, "numa_node": place["numa_node"], "cpus": now,
                                           "bound": bound["bound"]}, world)
         host = {"t_job": t_job, "t_mine": t_mine, "bytes": total_bytes, "placement": placement}
+    # rx_tx on every rank (bench.rx_tx_over_ranks): rank 0's leg + the max of each kernel time
+    leg = {"rx_in_order": {"rx_assemble_ms": 0.4 + rank, "stats": [1, 2]}, "tx": {"tx_assemble_ms": 0.3 - 0.1 * rank},
+           "note": "x"}
+    rxtx = bench.rx_tx_over_ranks(leg, bench.gather_objects(leg, world))
     tmax, gmax, ranks = bench.reduce_max([0.5 + rank, G, rank], world)
     covered = bench.reduce_max([g0 + G if rank == world - 1 else 0], world)[0]
     all_ok = bench.all_ranks_ok(ok, world)
@@ -70,7 +74,8 @@ def main():
     if rank == 0:
         print(json.dumps({"metric": "test", "n_gpus": world, "scaling": scaling, "total_groups": tot,
                           "tmax": tmax, "gmax": gmax, "max_rank": ranks, "covered": covered, "all_ok": all_ok,
-                          "one_bad": one_bad, "elapsed_pos": elapsed > 0, "cw_steps": cw_steps, "host": host}),
+                          "one_bad": one_bad, "elapsed_pos": elapsed > 0, "cw_steps": cw_steps, "host": host,
+                          "rx_tx": rxtx}),
               flush=True)
     else:
         print("rank %d noise on stdout" % rank, flush=True)

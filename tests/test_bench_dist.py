@@ -210,3 +210,19 @@ def test_host_path_coordination_two_ranks(tmp_path, capfd, monkeypatch):
     assert [x["rank"] for x in pl] == [0, 1]
     assert pl[0]["numa_node"] == 1 and pl[0]["cpus"] == nodes[1] and pl[0]["bound"]
     assert pl[1]["numa_node"] == 0 and pl[1]["cpus"] == nodes[0] and pl[1]["bound"]
+
+
+def test_rx_tx_over_ranks_reports_the_slowest_rank(capfd, monkeypatch):
+    """the rx_tx leg runs on every rank; rank 0's line keeps
+    its own leg and adds, for every kernel time, the max over ranks and each
+    rank's value (2 gloo ranks through bench.py's launcher)."""
+    monkeypatch.setenv("BENCH_TEST_TOTAL", "100")
+    rc = bench.launch(["--gpus", "2"], 2, script=RANK_SCRIPT, timeout=240)
+    out, err = capfd.readouterr()
+    assert rc == 0, err[-2000:]
+    r = json.loads([ln for ln in out.splitlines() if ln.strip()][0])["rx_tx"]
+    assert r["ranks"] == 2
+    assert r["rx_in_order"]["rx_assemble_ms"] == 0.4  # rank 0's own
+    assert r["max_over_ranks"]["rx_in_order.rx_assemble_ms"] == 1.4
+    assert abs(r["max_over_ranks"]["tx.tx_assemble_ms"] - 0.3) < 1e-9
+    assert [x["rx_in_order.rx_assemble_ms"] for x in r["per_rank"]] == [0.4, 1.4]

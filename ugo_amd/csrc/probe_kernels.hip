@@ -123,6 +123,65 @@ __global__ __launch_bounds__(256) void k_reconstruct_twin(RTwin a) {
   }
 }
 
+// The RX-path recovery's twin: k_apply_p's grid, the
+// wave's two groups' masks by scalar loads, survivor lists from the mask table;
+// a lane whose group has nothing to rebuild leaves before loading (as
+// production does); otherwise the first d present rows by nt loads, XOR, one
+// nt store per output.  DATA_ONLY: outputs = the erased data rows.  LIST: the
+// groups list[0 .. *count) (k_apply_p's list form), output j compact.
+struct RcTwin {
+  const uint8_t* base;
+  uint8_t* out;
+  const uint64_t* present;
+  const uint64_t* rows;
+  const uint32_t* list;
+  const uint32_t* count;
+  uint64_t rstride, gstride, orstride, ogstride;
+  uint32_t chunks, S, items, data_only;
+};
+
+__global__ __launch_bounds__(256) void k_recover_twin(RcTwin a) {
+  constexpr int D = 10, N = 13, P = 3;
+  const uint32_t wfirst = blockIdx.x * 256u + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+  const uint32_t item = blockIdx.x * 256u + threadIdx.x;
+  uint32_t items = a.items;
+  if (a.list) items = min(items, *a.count * a.chunks);
+  if (wfirst >= items) return;
+  const uint32_t wlast = min(wfirst + 63u, items - 1u);
+  const uint32_t gA = wfirst / a.chunks, gB = wlast / a.chunks;
+  const uint32_t rA = a.list ? a.list[gA] : gA, rB = a.list ? a.list[gB] : gB;
+  const uint64_t mA = a.present[rA], mB = a.present[rB];  // uniform: scalar loads
+  const uint64_t pa = a.rows[mA & ((1u << N) - 1u)], pb = a.rows[mB & ((1u << N) - 1u)];
+  if (item >= items) return;
+  const uint32_t gl = item / a.chunks, c = item - gl * a.chunks;
+  const bool inB = gl != gA;
+  const uint32_t m = static_cast<uint32_t>(inB ? mB : mA) & ((1u << N) - 1u);
+  const uint32_t lost = ~m & (a.data_only ? ((1u << D) - 1u) : ((1u << N) - 1u));
+  const uint32_t e = min(static_cast<uint32_t>(__builtin_popcount(lost)), static_cast<uint32_t>(P));
+  if (e == 0 || __builtin_popcount(m) < D) return;
+  const uint64_t pr = inB ? pb : pa;
+  const uint8_t* gp = a.base + uint64_t(inB ? rB : rA) * a.gstride + static_cast<uint64_t>(c) * 16u;
+  const uint32_t nb = a.S - c * 16u;
+  V4 x[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const uint32_t r = static_cast<uint32_t>(pr >> (4 * k)) & 15u;
+    x[k] = load16<1>(gp + static_cast<uint64_t>(r) * a.rstride);
+  }
+  V4 y = x[0];
+#pragma unroll
+  for (int k = 1; k < D; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y.v[j] ^= x[k].v[j];
+  uint8_t* op = a.out + uint64_t(gl) * a.ogstride + static_cast<uint64_t>(c) * 16u;
+#pragma unroll
+  for (int i = 0; i < P; ++i) {
+    if (i >= static_cast<int>(e)) continue;
+    y.v[0] ^= static_cast<uint32_t>(i);
+    store16<2>(op + static_cast<uint64_t>(i) * a.orstride, y, nb);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_nt_copy(const u32x4* src, u32x4* dst, uint64_t n16) {
   const uint64_t c = blockIdx.x * 256ull + threadIdx.x;
   if (c >= n16) return;
@@ -203,6 +262,46 @@ int ugo_probe_reconstruct_twin(const uint8_t* const* bases, uint8_t* const* outs
         // 36 KiB of dynamic LDS it never touches: 4 blocks (4 waves per SIMD)
         // per CU, k_apply_p<10,1,3>'s own occupancy (99 VGPRs)
         hipExtLaunchKernelGGL(k_reconstruct_twin, grid, block, 36u * 1024u, s, e0, e1, 0u, a);
+        return hipGetLastError();
+      },
+      reps, s, ms_out);
+}
+
+// reps launches of the recovery twin (k_recover_twin): launch r reads
+// bases[r % nbuf] (planar (10+3)) with masks presents[r % nbuf] and writes
+// outs[r % nbuf]: output i of entry j at j * out_entry_stride + i *
+// out_row_stride.  lists / counts: per buffer, the list form (device), or NULL
+// (every group an entry).  data_only as the reconstruct flag.
+int ugo_probe_recover_twin(const uint8_t* const* bases, uint8_t* const* outs, const uint64_t* const* presents,
+                           const uint32_t* const* lists, const uint32_t* const* counts, int nbuf, size_t groups,
+                           size_t S, size_t pitch, size_t row_stride, size_t out_row_stride, size_t out_entry_stride,
+                           int data_only, uint32_t lds_bytes, int reps, void* stream, float* ms_out) {
+  if (!bases || !outs || !presents || nbuf <= 0 || !ms_out || reps <= 0 || S == 0 || pitch < S || pitch % 16 ||
+      row_stride % 16 || out_entry_stride % 16 || out_row_stride % 16)
+    return 2;
+  const uint64_t chunks = (S + 15) / 16, items = groups * chunks;
+  if (items == 0 || items > 0xffffffffull) return 2;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  static uint64_t* rows = nullptr;  // built once per process
+  if (!rows) {
+    uint64_t h[1u << 13];
+    for (uint32_t m = 0; m < (1u << 13); ++m) {
+      uint64_t v = 0;
+      for (uint32_t r = 0, k = 0; r < 13 && k < 10; ++r)
+        if ((m >> r) & 1u) v |= static_cast<uint64_t>(r) << (4 * k++);
+      h[m] = v;
+    }
+    if (hipMalloc(&rows, sizeof(h)) != hipSuccess || hipMemcpy(rows, h, sizeof(h), hipMemcpyHostToDevice) != hipSuccess)
+      return 1;
+  }
+  const dim3 grid(static_cast<uint32_t>((items + 255) / 256)), block(256);
+  return timed(
+      [&](int r, hipEvent_t e0, hipEvent_t e1) {
+        const int b = r % nbuf;
+        RcTwin a{bases[b], outs[b], presents[b], rows, lists ? lists[b] : nullptr, counts ? counts[b] : nullptr,
+                 row_stride, pitch, out_row_stride, out_entry_stride, static_cast<uint32_t>(chunks),
+                 static_cast<uint32_t>(S), static_cast<uint32_t>(items), data_only ? 1u : 0u};
+        hipExtLaunchKernelGGL(k_recover_twin, grid, block, lds_bytes, s, e0, e1, 0u, a);
         return hipGetLastError();
       },
       reps, s, ms_out);
