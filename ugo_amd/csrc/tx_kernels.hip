@@ -80,7 +80,10 @@ struct TxItem {
 // SL (even DN == d only): the lengths are read with scalar loads for the two
 // groups a wave can span (>= 64 chunks per group) and picked per lane, instead
 // of one broadcast vector load per packet per wave.
-template <int DN, int NT, bool SL, bool PL = false>
+// ATTR (A/B and PMC attribution only, tools/txpmc.hip; 0 in production): bit 0
+// skips the wire_lens / status stores, bit 1 replaces the parity network by a
+// plain XOR of the inputs (the compute-free twin: wrong parity on purpose).
+template <int DN, int NT, bool SL, bool PL = false, int ATTR = 0>
 __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x, const u32x4* padl = nullptr) {
   TxItem t{};
   const uint64_t gl = item / a.chunks;
@@ -159,7 +162,7 @@ __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x,
       if (m == 0) {
         v.v[0] = 0u;
         v.v[1] &= 0xffff0000u;
-        a.wire_lens[t.g * n + k] = static_cast<uint16_t>(Lk);
+        if constexpr (!(ATTR & 1)) a.wire_lens[t.g * n + k] = static_cast<uint16_t>(Lk);
       }
       x[k] = v;
     } else {
@@ -169,19 +172,32 @@ __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x,
   return t;
 }
 
-template <int NT>
+template <int NT, int ATTR = 0>
 __device__ __forceinline__ void tx_parity_out(const TxArgs& a, const TxItem& t, uint32_t i, V4 y) {
   const uint32_t n = a.d + a.p;
   if (t.o == 0) put_header(y, t.seq0 + a.d + i, kTypeFEC);
   xor4(y, t.padc);
   store16<NT>(a.wire + (t.g * n + a.d + i) * a.slot_out + t.o, keep_bytes(y, t.maxsz - t.o), 16u);
-  if (t.o == 0) a.wire_lens[t.g * n + a.d + i] = static_cast<uint16_t>(t.maxsz);
+  if constexpr (!(ATTR & 1))
+    if (t.o == 0) a.wire_lens[t.g * n + a.d + i] = static_cast<uint16_t>(t.maxsz);
 }
 
-template <int D, int P, int NT, int... I>
+template <int D, int I>
+__device__ __forceinline__ V4 xor_twin(const V4* x) {  // ATTR 2: the inputs XORed, rotated by the row
+  V4 y = x[I % D];
+#pragma unroll
+  for (int k = 0; k < D; ++k)
+    if (k != I % D) xor4(y, x[k]);
+  return y;
+}
+
+template <int D, int P, int NT, int ATTR, int... I>
 __device__ __forceinline__ void tx_cparity(const TxArgs& a, const TxItem& t, const V4* x,
                                            std::integer_sequence<int, I...>) {
-  (tx_parity_out<NT>(a, t, I, cparity<D, P, I>(x)), ...);
+  if constexpr (ATTR & 2)
+    (tx_parity_out<NT, ATTR>(a, t, I, xor_twin<D, I>(x)), ...);
+  else
+    (tx_parity_out<NT, ATTR>(a, t, I, cparity<D, P, I>(x)), ...);
 }
 
 // Every data packet of the group header-only: calcECC's window [6, 6) is
@@ -201,7 +217,7 @@ __device__ __forceinline__ bool tx_no_window(const TxArgs& a, const TxItem& t) {
 // (10,3) / (32,8): the compile-time XOR networks of k_encode_c.
 // PL: the keystream staged once per block in dynamic LDS (needs a.pad and
 // 16 * chunks bytes of dynamic LDS), instead of one 16-B global load per thread.
-template <int D, int P, int NT = kTxNT, bool SL = kTxSL, bool PL = false>
+template <int D, int P, int NT = kTxNT, bool SL = kTxSL, bool PL = false, int ATTR = 0>
 __global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
   const uint32_t item = blockIdx.x * 256u + threadIdx.x;
   extern __shared__ u32x4 padl[];
@@ -211,10 +227,11 @@ __global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
   }
   if (item >= a.groups * a.chunks) return;
   V4 x[D];
-  const TxItem t = tx_data<D, NT, SL, PL>(a, item, x, padl);
+  const TxItem t = tx_data<D, NT, SL, PL, ATTR>(a, item, x, padl);
   if (!t.live || tx_no_window(a, t)) return;
-  tx_cparity<D, P, NT>(a, t, x, std::make_integer_sequence<int, P>{});
-  if (t.o == 0 && a.status) a.status[t.g] = 0;
+  tx_cparity<D, P, NT, ATTR>(a, t, x, std::make_integer_sequence<int, P>{});
+  if constexpr (!(ATTR & 1))
+    if (t.o == 0 && a.status) a.status[t.g] = 0;
 }
 
 // Any other geometry: coefficients from the encode descriptor (uniform, so
