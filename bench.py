@@ -743,10 +743,7 @@ def host_path_leg(args, dev_index, rank=0, world=1, reps=3):
         res.update(rxtx)
         all_ok = all_ok and ok_rxtx
     finally:
-        try:
-            os.sched_setaffinity(0, saved)
-        except OSError:
-            pass
+        numa.set_affinity_all_threads(saved)
     res["verify_all_ranks"] = all_ranks_ok(all_ok, world)
     me = {"rank": rank, "device": dev_index, "pci_bus_id": place["pci_bus_id"], "numa_node": place["numa_node"],
           "bound": bound.get("bound", False), "cpus": bound.get("cpus")}

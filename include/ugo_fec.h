@@ -402,9 +402,11 @@ int ugo_fec_timing_end(ugo_fec* ctx, ugo_fec_launch_time* out, size_t cap, size_
                        size_t* n_untimed);
 
 /* ---- helpers ------------------------------------------------------------- */
-/* pinned host memory; tests may set UGO_FEC_HOST_ALLOC_LIMIT=<bytes> in the
- * environment to make larger requests fail (fault injection) */
+/* pinned host memory */
 int ugo_fec_host_alloc(size_t bytes, void** out);
+/* tests only (fault injection): pinned allocations of more than `bytes` fail
+ * with UGO_FEC_ERR_HIP, as on a host out of pinnable memory; 0 = no limit */
+int ugo_fec_set_host_alloc_limit(size_t bytes);
 int ugo_fec_host_free(void* p);
 const char* ugo_fec_strerror(int status);
 int ugo_fec_abi_version(void);

@@ -181,11 +181,24 @@ def test_numa_lookup_and_binding_on_a_fake_sysfs(tmp_path):
     assert info["numa_node"] == 1 and info["node_cpus"] == nodes[1]
     assert numa.gpu_numa_node(0, sysfs=str(tmp_path), bdf="0000:ff:00.0")["numa_node"] is None
     saved = os.sched_getaffinity(0)
+    # a thread that exists before the binding (as HIP's, torch's and gloo's do) is bound too
+    import threading
+
+    go, tid = threading.Event(), []
+    t = threading.Thread(target=lambda: (tid.append(threading.get_native_id()), go.wait(30)))
+    t.start()
+    while not tid:
+        pass
     try:
         r = numa.bind_to_node(info)
         assert r["bound"] and sorted(os.sched_getaffinity(0)) == nodes[1]
+        assert r["threads"] >= 2
+        assert sorted(os.sched_getaffinity(tid[0])) == nodes[1]
     finally:
-        os.sched_setaffinity(0, saved)
+        go.set()
+        t.join()
+        numa.set_affinity_all_threads(saved)
+    assert sorted(os.sched_getaffinity(0)) == sorted(saved)
     assert not numa.bind_to_node({"node_cpus": []})["bound"]
 
 

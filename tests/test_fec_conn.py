@@ -356,7 +356,7 @@ def test_calc_ecc_random_windows(gpu, d, p, offset, width, buflen, seed):
 @pytest.mark.gpu
 def test_set_batch_allocation_failure_falls_back_to_per_call(gpu, monkeypatch):
     """a set_batch whose pinned batch cannot be allocated (fault
-    injected: UGO_FEC_HOST_ALLOC_LIMIT) fails with ErrHip and leaves the object
+    injected: ugo_fec_set_host_alloc_limit) fails with ErrHip and leaves the object
     in per-call mode -- it never keeps pointing at a freed batch.  Before and
     after, input recovers exactly what the reference restatement recovers
     (pending groups of the old batch come back first)."""
@@ -380,15 +380,18 @@ def test_set_batch_allocation_failure_falls_back_to_per_call(gpu, monkeypatch):
 
     feed(range(0, 6))  # one full batch of 4 came back, 2 pending
     assert rx_b.pending() == 2
-    monkeypatch.setenv("UGO_FEC_HOST_ALLOC_LIMIT", "4096")
     import ctypes
     lib = fec._bind_conn(fec.load_library())
-    nrec, rlen = ctypes.c_int(), ctypes.c_size_t()
-    st = lib.ugo_fecconn_set_batch_ex(rx_b._h, 8, 0, ctypes.addressof(rx_b._out), len(rx_b._out),
-                                      ctypes.byref(nrec), ctypes.byref(rlen))
+    lib.ugo_fec_set_host_alloc_limit.argtypes = [ctypes.c_size_t]
+    lib.ugo_fec_set_host_alloc_limit(4096)
+    try:
+        nrec, rlen = ctypes.c_int(), ctypes.c_size_t()
+        st = lib.ugo_fecconn_set_batch_ex(rx_b._h, 8, 0, ctypes.addressof(rx_b._out), len(rx_b._out),
+                                          ctypes.byref(nrec), ctypes.byref(rlen))
+    finally:
+        lib.ugo_fec_set_host_alloc_limit(0)
     assert st == fec.ErrHip.code
     got.extend(bytes(x) for x in rx_b._recovered(nrec, rlen) or [])  # the 2 pending groups, flushed first
-    monkeypatch.delenv("UGO_FEC_HOST_ALLOC_LIMIT")
     assert rx_b.pending() == 0
     n_before = len(got)
     feed(range(6, 12))  # per-call mode now: every lossy group comes back at once

@@ -337,7 +337,7 @@ void service_watchdog() {
   ugo_fec_host_free(g);
 }
 
-// set_batch whose pinned batch cannot be allocated (UGO_FEC_HOST_ALLOC_LIMIT):
+// set_batch whose pinned batch cannot be allocated (ugo_fec_set_host_alloc_limit):
 // ERR_HIP, per-call mode, and input keeps working
 void fec_object_alloc_failure() {
   ugo_fecconn* f = nullptr;
@@ -347,9 +347,9 @@ void fec_object_alloc_failure() {
   int nrec = 0;
   size_t rl = 0;
   EXPECT(ugo_fecconn_set_batch(f, 4, out.data(), out.size(), &nrec, &rl) == UGO_FEC_OK);
-  setenv("UGO_FEC_HOST_ALLOC_LIMIT", "4096", 1);
+  ugo_fec_set_host_alloc_limit(4096);
   EXPECT(ugo_fecconn_set_batch(f, 8, out.data(), out.size(), &nrec, &rl) == UGO_FEC_ERR_HIP);
-  unsetenv("UGO_FEC_HOST_ALLOC_LIMIT");
+  ugo_fec_set_host_alloc_limit(0);
   // one lossy group (data shard 2 lost) through input, per call now
   std::vector<std::vector<uint8_t>> grp(13, std::vector<uint8_t>(1476));
   std::vector<uint8_t*> ptr(13);

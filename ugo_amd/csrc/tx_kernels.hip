@@ -296,17 +296,22 @@ hipError_t launch_tx_assemble(int dmax, const TxArgs& a, hipStream_t s) {
       // profiles/r4/txgroup_pad_lds.jsonl)
       const uint32_t padl = 16u * a.chunks;
       const uint32_t cap = std::max(tx_lds_cap(), padl);
-      if (a.d == 10 && a.p == 3 && a.pad && sl)
+      // a block stages the whole keystream: only while that is at most one
+      // group's worth of its 256 threads (chunks <= 256, max_len <= 4096) --
+      // past that most of the stage goes unused and the lanes load
+      // their own keystream chunk instead
+      const bool pl = a.pad && a.chunks <= 256u;
+      if (a.d == 10 && a.p == 3 && pl && sl)
         launch(kKTx, k_tx_c<10, 3, kTxNT, true, true>, grid, block, cap, s, a);
-      else if (a.d == 10 && a.p == 3 && a.pad)
+      else if (a.d == 10 && a.p == 3 && pl)
         launch(kKTx, k_tx_c<10, 3, kTxNT, false, true>, grid, block, cap, s, a);
       else if (a.d == 10 && a.p == 3 && sl)
         launch(kKTx, k_tx_c<10, 3, kTxNT, true>, grid, block, tx_lds_cap(), s, a);
       else if (a.d == 10 && a.p == 3)
         launch(kKTx, k_tx_c<10, 3, kTxNT, false>, grid, block, tx_lds_cap(), s, a);
-      else if (a.d == 32 && a.p == 8 && a.pad && sl)
+      else if (a.d == 32 && a.p == 8 && pl && sl)
         launch(kKTx, k_tx_c<32, 8, kTxNT, true, true>, grid, block, padl, s, a);
-      else if (a.d == 32 && a.p == 8 && a.pad)
+      else if (a.d == 32 && a.p == 8 && pl)
         launch(kKTx, k_tx_c<32, 8, kTxNT, false, true>, grid, block, padl, s, a);
       else if (a.d == 32 && a.p == 8 && sl)
         launch(kKTx, k_tx_c<32, 8, kTxNT, true>, grid, block, 0, s, a);
@@ -318,7 +323,7 @@ hipError_t launch_tx_assemble(int dmax, const TxArgs& a, hipStream_t s) {
     }
 #define UGO_TX_VAR(DM)                                                                   \
   case DM:                                                                               \
-    if (a.pad)                                                                           \
+    if (a.pad && a.chunks <= 256u)                                                       \
       launch(kKTx, k_tx_var<DM, true>, grid, block, 16u * a.chunks, s, a);               \
     else                                                                                 \
       launch(kKTx, k_tx_var<DM>, grid, block, 0, s, a);                                  \

@@ -1839,13 +1839,23 @@ int ugo_fec_timing_end(ugo_fec* c, ugo_fec_launch_time* out, size_t cap, size_t*
   return st;
 }
 
+// Fault injection for tests (ugo_fec_set_host_alloc_limit): pinned
+// allocations larger than the limit fail, as on a host out of pinnable memory.
+// An explicit call rather than an environment variable read on the allocation
+// path (a stray variable in deployment would fail every allocation
+// silently, and getenv races a concurrent setenv).
+static std::atomic<unsigned long long> g_host_alloc_limit{0};
+
+int ugo_fec_set_host_alloc_limit(size_t bytes) {
+  g_host_alloc_limit.store(bytes, std::memory_order_relaxed);
+  return UGO_FEC_OK;
+}
+
 int ugo_fec_host_alloc(size_t bytes, void** out) {
   if (!out) return UGO_FEC_ERR_INVALID_ARG;
   *out = nullptr;
-  // fault injection for tests: UGO_FEC_HOST_ALLOC_LIMIT=<bytes> refuses larger
-  // pinned allocations (as a host out of pinnable memory would)
-  if (const char* lim = std::getenv("UGO_FEC_HOST_ALLOC_LIMIT"))
-    if (*lim && bytes > std::strtoull(lim, nullptr, 10)) return UGO_FEC_ERR_HIP;
+  const unsigned long long lim = g_host_alloc_limit.load(std::memory_order_relaxed);
+  if (lim && bytes > lim) return UGO_FEC_ERR_HIP;
   return hip_status(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
 }
 

@@ -9,9 +9,11 @@ only that socket's PCIe root and memory controllers.
 
 gpu_numa_node reads the GPU's PCI address (torch device properties, which
 come from hipDeviceGetPCIBusId) and the kernel's sysfs record of its node;
-bind_to_node restricts this process to that node's CPUs (no exec, no child)
-before the caller allocates and first-touches its pinned batches.  Every path
-takes a sysfs root, so tests drive it with a fake tree.
+bind_to_node restricts every thread of this process -- the caller's and the
+ones HIP, torch and gloo already started -- to that node's CPUs (no exec, no
+child) before the caller allocates and first-touches its pinned batches;
+threads started later inherit the mask.  Every path takes a sysfs root, so
+tests drive it with a fake tree.
 """
 from __future__ import annotations
 
@@ -74,10 +76,33 @@ def gpu_numa_node(device: int, sysfs: str = SYSFS, bdf: Optional[str] = None) ->
     return {"pci_bus_id": bdf, "numa_node": node, "node_cpus": node_cpus(node, sysfs) if node is not None else []}
 
 
-def bind_to_node(info: Dict) -> Dict:
-    """Restrict this process to the GPU's node's CPUs that it may use (the
-    affinity set it already has, intersected); returns what was done.  No-op
-    when the node is unknown or the intersection is empty."""
+def thread_ids(proc: str = "/proc") -> List[int]:
+    """The TIDs of this process's threads (Linux /proc/self/task); [0] (the
+    calling thread) where that is not readable."""
+    try:
+        return sorted(int(t) for t in os.listdir(os.path.join(proc, "self", "task")))
+    except (OSError, ValueError):
+        return [0]
+
+
+def set_affinity_all_threads(cpus, proc: str = "/proc") -> int:
+    """os.sched_setaffinity on every thread of the process: on Linux it binds
+    only the thread it names, so each TID gets the mask.  Returns
+    the number of threads bound (a thread that exits meanwhile is skipped)."""
+    bound = 0
+    for tid in thread_ids(proc):
+        try:
+            os.sched_setaffinity(tid, cpus)
+            bound += 1
+        except (OSError, ProcessLookupError):
+            continue
+    return bound
+
+
+def bind_to_node(info: Dict, proc: str = "/proc") -> Dict:
+    """Restrict every thread of this process to the GPU's node's CPUs that it
+    may use (the affinity set it already has, intersected); returns what was
+    done.  No-op when the node is unknown or the intersection is empty."""
     try:
         allowed = set(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
@@ -85,6 +110,5 @@ def bind_to_node(info: Dict) -> Dict:
     want = allowed & set(info.get("node_cpus") or [])
     if not want:
         return {"bound": False, "reason": "node unknown or none of its CPUs allowed", "cpus": len(allowed)}
-    if want != allowed:
-        os.sched_setaffinity(0, want)
-    return {"bound": True, "cpus": len(want)}
+    threads = set_affinity_all_threads(want, proc) if want != allowed else len(thread_ids(proc))
+    return {"bound": True, "cpus": len(want), "threads": threads}
