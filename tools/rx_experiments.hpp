@@ -916,5 +916,101 @@ __global__ __launch_bounds__(256) void k_rx_tally(const uint64_t* present, const
 }
 
 
+
+// ---------------------------------------------------------------------------
+// k_rx_p2 (round 5): the P2 pattern's shape -- one 16-B slot chunk per lane,
+// a full grid, consecutive lanes on consecutive chunks -- with everything
+// per-packet done on the scalar unit.  Wave w covers slot chunks [63w, 63w+64)
+// of the ring (93 per 1488-B slot): 64 < 93, so the wave touches at most two
+// packets, whose headers, lengths, classification and snapshot words it reads
+// with scalar loads; lanes 0..62 store an output chunk, lane 63 only lends its
+// chunk to lane 62's realignment (DPP), so a wave issues ONE payload load and
+// ONE store.  The keystream: per lane from L1/L2 (PADLDS 0) or staged in LDS
+// behind one block barrier that the payload loads stay in flight across
+// (PADLDS 1).  Presence / rare classes / duplicate gate as k_rx_half (ctl +
+// k_rx_tally).  Needs slot >= 1024 B (64 chunks) and S <= slot.
+typedef const __attribute__((address_space(4))) uint32_t* rx_cptr;
+
+__device__ __forceinline__ uint32_t rx_sld(const void* p) { return *(rx_cptr)(p); }
+
+struct RxPk {  // one packet's placement, wave-uniform
+  uint64_t gs;
+  uint32_t row, L, why;
+};
+
+__device__ __forceinline__ RxPk rx_classify(const RxArgs& a, uint64_t i, uint32_t k0, uint32_t k1, bool chk_prev) {
+  RxPk r{0, 0, 0, 5};
+  if (i >= a.npk) return r;
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  const uint8_t* pk = a.wire + i * a.slot;
+  const uint32_t seqid = rx_sld(pk) ^ k0;
+  const uint32_t flag = (rx_sld(pk + 4) ^ k1) & 0xffffu;
+  const uintptr_t la = reinterpret_cast<uintptr_t>(a.lens + i);
+  const uint32_t lw = rx_sld(reinterpret_cast<const void*>(la & ~uintptr_t(3)));
+  const uint32_t len = min((la & 2) ? (lw >> 16) : (lw & 0xffffu), slot);
+  uint32_t why = 0;
+  if (len < 6u) why = 3;
+  else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
+  r.row = seqid % a.n;
+  const uint64_t grp = seqid / a.n;
+  if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
+  r.gs = grp - a.first_group;
+  if (!why && chk_prev) {
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(a.prev + r.gs);
+    const uint32_t bit = r.row < 32u ? (rx_sld(pw) >> r.row) : (rx_sld(pw + 1) >> (r.row - 32u));
+    if (bit & 1u) why = 4;  // an earlier call placed this seqid
+  }
+  r.why = why;
+  r.L = why ? 0u : min(len - 6u, a.S);
+  return r;
+}
+
+template <int PADLDS>
+__global__ __launch_bounds__(256) void k_rx_p2(RxArgs a, uint32_t* ctl) {
+  __shared__ u32x4 spad[PADLDS ? 128 : 1];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t Q = static_cast<uint32_t>(a.slot / 16u);
+  const uint64_t w = uint64_t(blockIdx.x) * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t total = a.npk * Q;
+  const uint64_t c0 = 63u * w;  // the wave's first chunk (uniform)
+  const uint64_t c = c0 + lane;
+  const bool live = c < total;
+  const uint64_t i = c / Q;
+  const uint32_t m = static_cast<uint32_t>(c - i * Q);
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  u32x4 A = live ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + i * a.slot + 16u * m)) : zero;
+  u32x4 K = zero;
+  if constexpr (PADLDS) {
+    if (a.pad)
+      for (uint32_t q = threadIdx.x; q < Q; q += 256u) spad[q] = ld16(a.pad + 16u * q);
+    __syncthreads();
+    if (a.pad && live) K = spad[m];
+  } else {
+    if (a.pad && live) K = ld16(a.pad + 16u * m);
+  }
+  if (c0 >= total) return;  // wave-uniform (after the block barrier)
+  const uint32_t k0 = a.pad ? rx_sld(a.pad) : 0u, k1 = a.pad ? rx_sld(a.pad + 4) : 0u;
+  const bool chk_prev = a.prev && !(a.seen && *a.seen < a.call);
+  const uint64_t i0 = c0 / Q;
+  const RxPk p0 = rx_classify(a, i0, k0, k1, chk_prev);
+  const RxPk p1 = rx_classify(a, i0 + 1, k0, k1, chk_prev);  // the wave's second packet, if it reaches it
+  const bool second = i != i0;
+  const uint32_t why = second ? p1.why : p0.why;
+  const uint32_t row = second ? p1.row : p0.row;
+  const uint64_t gs = second ? p1.gs : p0.gs;
+  const uint32_t L = second ? p1.L : p0.L;
+  if (live && m == 0u) {  // the packet's chunk-0 lane accounts for it
+    if (why == 0)
+      atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
+    else if (why < 5)
+      atomicAdd(&ctl[1 + why], 1u);
+  }
+  A ^= K;
+  const uint32_t nx = from_next_lane(A.x), ny = from_next_lane(A.y);  // chunk m + 1 of the same packet
+  const uint32_t o = 16u * m;
+  if (lane == 63u || !live || why != 0 || o >= a.S) return;
+  rx_put<1>(a.shards + row * a.rstride + gs * a.gstride, o, L, A, nx, ny);
+}
+
 }  // namespace kern
 }  // namespace ugo

@@ -202,7 +202,7 @@ int main(int argc, char** argv) {
   uint32_t* win = reinterpret_cast<uint32_t*>(prev + G);
   uint32_t* dup = win + G * n;
 
-  enum Kind { PROD, PROD_OLD, GATHER, CHUNK, FULL, SLOTS, HALF };
+  enum Kind { PROD, PROD_OLD, GATHER, CHUNK, FULL, SLOTS, HALF, P2K };
   struct Var {
     std::string name;
     Kind kind;
@@ -212,6 +212,8 @@ int main(int argc, char** argv) {
   std::vector<Var> vars = {
       {"production (round 5): begin(+claim fill, fresh flag) + k_rx_place_h (16384 blocks, whole-chunk row tails) + gated claim/re-place", PROD, 0, 0, 0},
       {"full-grid half-wave k_rx_half (P3b shape, no length-dependent loads, whole-chunk row tails) + tally + gated claim/re-place", HALF, 0, 0, 0},
+      {"k_rx_p2: P2 shape, one chunk per lane, scalar headers, keystream per lane + tally + gated claim/re-place", P2K, 0, 0, 0},
+      {"k_rx_p2, keystream staged in LDS (one barrier)", P2K, 1, 0, 0},
       {"slot-linear k_rx_slots, keystream in LDS, P=11 (1023 threads) + tally + gated claim/re-place", SLOTS, 11, 1, 0},
       {"slot-linear k_rx_slots, keystream in LDS, P=2 (186 threads)", SLOTS, 2, 1, 0},
       {"round-4 second form: k_rx_place MODE 4 (ds_bpermute realignment, header load), 8192 blocks", PROD, 7, 0, 0},
@@ -257,7 +259,7 @@ int main(int argc, char** argv) {
         k_rx_gather<3, 1, 32><<<gr, 256, 0, s>>>(a, d_parts, ib);
       return;
     }
-    if (v.kind == SLOTS || v.kind == HALF) {  // round 5: begin -> zero ctl -> place -> tally -> gated claim / re-place
+    if (v.kind == SLOTS || v.kind == HALF || v.kind == P2K) {  // round 5: begin -> zero ctl -> place -> tally -> gated claim / re-place
       const unsigned long long call = ++call_id;
       CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, s));
       k_rx_zero_rare<<<1, 64, 0, s>>>(dup);  // ctl = dup[0..7] (ctl[0] is the duplicate gate)
@@ -266,6 +268,13 @@ int main(int argc, char** argv) {
       a.prev = prev;
       if (v.kind == HALF) {
         k_rx_half<3, 0><<<static_cast<uint32_t>((a.npk + 7) / 8), 256, 0, s>>>(a, dup);
+      } else if (v.kind == P2K) {
+        const uint64_t waves = (a.npk * (a.slot / 16) + 62) / 63;
+        const uint32_t blocks = static_cast<uint32_t>((waves + 3) / 4);
+        if (v.order)
+          k_rx_p2<1><<<blocks, 256, 0, s>>>(a, dup);
+        else
+          k_rx_p2<0><<<blocks, 256, 0, s>>>(a, dup);
       } else {
         const uint64_t Q = a.slot / 16, nq = (a.S + 15) / 16, T = Q > nq ? Q : nq;
         uint32_t P = static_cast<uint32_t>(v.order);
