@@ -965,7 +965,17 @@ __device__ __forceinline__ RxPk rx_classify(const RxArgs& a, uint64_t i, uint32_
   return r;
 }
 
-template <int PADLDS>
+// LEN 1: the lengths of the wave's two packets by scalar loads FIRST, and a
+// lane loads its chunk only if it starts inside its packet (length-aware
+// loads, as production's, at the price of a scalar round trip before them).
+__device__ __forceinline__ uint32_t rx_slen(const RxArgs& a, uint64_t i) {
+  if (i >= a.npk) return 0u;
+  const uintptr_t la = reinterpret_cast<uintptr_t>(a.lens + i);
+  const uint32_t lw = rx_sld(reinterpret_cast<const void*>(la & ~uintptr_t(3)));
+  return min((la & 2) ? (lw >> 16) : (lw & 0xffffu), static_cast<uint32_t>(a.slot));
+}
+
+template <int PADLDS, int LEN = 0>
 __global__ __launch_bounds__(256) void k_rx_p2(RxArgs a, uint32_t* ctl) {
   __shared__ u32x4 spad[PADLDS ? 128 : 1];
   const uint32_t lane = threadIdx.x & 63u;
@@ -974,10 +984,16 @@ __global__ __launch_bounds__(256) void k_rx_p2(RxArgs a, uint32_t* ctl) {
   const uint64_t total = a.npk * Q;
   const uint64_t c0 = 63u * w;  // the wave's first chunk (uniform)
   const uint64_t c = c0 + lane;
-  const bool live = c < total;
+  bool live = c < total;
   const uint64_t i = c / Q;
   const uint32_t m = static_cast<uint32_t>(c - i * Q);
   const u32x4 zero = {0u, 0u, 0u, 0u};
+  if constexpr (LEN) {  // chunk m is needed only if it starts inside the packet (the left neighbour may need it)
+    const uint64_t j0 = c0 / Q;
+    const uint32_t l0 = rx_slen(a, j0), l1 = rx_slen(a, j0 + 1);
+    const uint32_t lim = min(i != j0 ? l1 : l0, a.S + 6u);
+    live = live && 16u * m < lim;
+  }
   u32x4 A = live ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.wire + i * a.slot + 16u * m)) : zero;
   u32x4 K = zero;
   if constexpr (PADLDS) {
@@ -999,7 +1015,7 @@ __global__ __launch_bounds__(256) void k_rx_p2(RxArgs a, uint32_t* ctl) {
   const uint32_t row = second ? p1.row : p0.row;
   const uint64_t gs = second ? p1.gs : p0.gs;
   const uint32_t L = second ? p1.L : p0.L;
-  if (live && m == 0u) {  // the packet's chunk-0 lane accounts for it
+  if (c < total && m == 0u) {  // the packet's chunk-0 lane accounts for it
     if (why == 0)
       atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
     else if (why < 5)
@@ -1008,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_rx_p2(RxArgs a, uint32_t* ctl) {
   A ^= K;
   const uint32_t nx = from_next_lane(A.x), ny = from_next_lane(A.y);  // chunk m + 1 of the same packet
   const uint32_t o = 16u * m;
-  if (lane == 63u || !live || why != 0 || o >= a.S) return;
+  if (lane == 63u || c >= total || why != 0 || o >= a.S) return;
   rx_put<1>(a.shards + row * a.rstride + gs * a.gstride, o, L, A, nx, ny);
 }
 

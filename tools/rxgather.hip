@@ -214,6 +214,7 @@ int main(int argc, char** argv) {
       {"full-grid half-wave k_rx_half (P3b shape, no length-dependent loads, whole-chunk row tails) + tally + gated claim/re-place", HALF, 0, 0, 0},
       {"k_rx_p2: P2 shape, one chunk per lane, scalar headers, keystream per lane + tally + gated claim/re-place", P2K, 0, 0, 0},
       {"k_rx_p2, keystream staged in LDS (one barrier)", P2K, 1, 0, 0},
+      {"k_rx_p2, length-aware loads (lengths by scalar loads first)", P2K, 2, 0, 0},
       {"slot-linear k_rx_slots, keystream in LDS, P=11 (1023 threads) + tally + gated claim/re-place", SLOTS, 11, 1, 0},
       {"slot-linear k_rx_slots, keystream in LDS, P=2 (186 threads)", SLOTS, 2, 1, 0},
       {"round-4 second form: k_rx_place MODE 4 (ds_bpermute realignment, header load), 8192 blocks", PROD, 7, 0, 0},
@@ -271,8 +272,10 @@ int main(int argc, char** argv) {
       } else if (v.kind == P2K) {
         const uint64_t waves = (a.npk * (a.slot / 16) + 62) / 63;
         const uint32_t blocks = static_cast<uint32_t>((waves + 3) / 4);
-        if (v.order)
+        if (v.order == 1)
           k_rx_p2<1><<<blocks, 256, 0, s>>>(a, dup);
+        else if (v.order == 2)
+          k_rx_p2<0, 1><<<blocks, 256, 0, s>>>(a, dup);
         else
           k_rx_p2<0><<<blocks, 256, 0, s>>>(a, dup);
       } else {
