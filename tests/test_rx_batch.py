@@ -336,6 +336,7 @@ def test_rx_assemble_first_copy_wins_across_calls(gpu, encrypt, S, slot):
         for r in range(n):
             if (int(masks[g]) >> r) & 1:
                 assert np.array_equal(got[g, r, :S], want[g, r, :S]), (g, r)
+                assert not got[g, r, S:].any(), (g, r)  # ABI 8: whole 16-B chunks, zeros past S
             else:
                 assert (got[g, r] == 0xAB).all(), (g, r)
 
@@ -472,5 +473,6 @@ def test_rx_assemble_random_rings(gpu, d, p, S, G, first_group, loss, dup, junk,
         for r in range(n):
             if (int(masks[g]) >> r) & 1:
                 assert np.array_equal(got[g, r, :S], want[g, r, :S]), (g, r)
+                assert not got[g, r, S:].any(), (g, r)  # ABI 8: whole 16-B chunks, zeros past S
             else:
                 assert (got[g, r] == 0xAB).all(), (g, r)
