@@ -1015,7 +1015,9 @@ __global__ __launch_bounds__(256) void k_rx_p2(RxArgs a, uint32_t* ctl) {
   const uint32_t row = second ? p1.row : p0.row;
   const uint64_t gs = second ? p1.gs : p0.gs;
   const uint32_t L = second ? p1.L : p0.L;
-  if (c < total && m == 0u) {  // the packet's chunk-0 lane accounts for it
+  // the packet's chunk-0 lane accounts for it -- not lane 63, whose chunk is
+  // the next wave's lane 0 (it would count the packet twice)
+  if (lane < 63u && c < total && m == 0u) {
     if (why == 0)
       atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
     else if (why < 5)

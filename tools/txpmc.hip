@@ -94,7 +94,51 @@ int main(int argc, char** argv) {
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 2><<<grid, 256, cap>>>(a); }},
       {"compute-free twin, no wire_lens / status stores (ATTR 3)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 3><<<grid, 256, cap>>>(a); }},
+      {"XCD-contiguous blocks (ATTR 4)",
+       [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 4><<<grid, 256, cap>>>(a); }},
+      {"plain data loads (ATTR 8)",
+       [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 8><<<grid, 256, cap>>>(a); }},
+      {"XCD-contiguous blocks, plain data loads (ATTR 12)",
+       [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 12><<<grid, 256, cap>>>(a); }},
+      {"no wire_lens / status stores + k_tx_lens (ATTR 1 + lens kernel)", [&](const TxArgs& a) {
+         k_tx_c<10, 3, kTxNT, true, true, 1><<<grid, 256, cap>>>(a);
+         k_tx_lens<<<static_cast<uint32_t>((a.groups * 13 + 255) / 256), 256>>>(a);
+       }},
   };
+  {  // ATTR 1 + k_tx_lens writes the same wire, wire_lens and status as production (random lengths)
+    std::vector<uint16_t> Lr(G * d);
+    for (auto& v : Lr) v = static_cast<uint16_t>(6 + rng() % (max_len - 5));
+    for (uint64_t g = 0; g < G; g += 97) Lr[g * d + 3] = 5;  // bad
+    for (uint64_t g = 1; g < G; g += 89)
+      for (uint32_t k = 0; k < d; ++k) Lr[g * d + k] = 6;  // header-only
+    TxArgs x = rot[0], y = rot[1];
+    uint16_t* dl;
+    CK(hipMalloc(&dl, G * d * 2));
+    CK(hipMemcpy(dl, Lr.data(), G * d * 2, hipMemcpyHostToDevice));
+    x.lens = y.lens = dl;
+    y.pkts = x.pkts;
+    for (const TxArgs* t : {&x, &y}) {
+      CK(hipMemset(t->wire, 0x5c, G * n * slot));
+      CK(hipMemset(t->wire_lens, 0x77, G * n * 2));
+      CK(hipMemset(t->status, 0x33, G));
+    }
+    k_tx_c<10, 3, kTxNT, true, true, 0><<<grid, 256, cap>>>(x);
+    k_tx_c<10, 3, kTxNT, true, true, 1><<<grid, 256, cap>>>(y);
+    k_tx_lens<<<static_cast<uint32_t>((G * 13 + 255) / 256), 256>>>(y);
+    CK(hipDeviceSynchronize());
+    std::vector<uint8_t> w1(G * n * slot), w2(G * n * slot);
+    std::vector<uint16_t> l1(G * n), l2(G * n);
+    std::vector<int8_t> s1(G), s2(G);
+    CK(hipMemcpy(w1.data(), x.wire, w1.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(w2.data(), y.wire, w2.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(l1.data(), x.wire_lens, G * n * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(l2.data(), y.wire_lens, G * n * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(s1.data(), x.status, G, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(s2.data(), y.status, G, hipMemcpyDeviceToHost));
+    printf("{\"check\":\"ATTR 1 + k_tx_lens == production (wire, wire_lens, status)\",\"same\":%s}\n",
+           (w1 == w2 && l1 == l2 && s1 == s2) ? "true" : "false");
+    CK(hipFree(dl));
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

@@ -40,7 +40,9 @@ for d in sorted(glob.glob(out + "/*_*/")):
         for c, v in cs.items():
             agg[name[key]][c].append(v)
     for k, cs in agg.items():
-        short = k.split("(")[0].replace("void ugo::kern::(anonymous namespace)::", "").replace("void ugo::kern::", "")
+        import re
+        mm = re.search(r"(k_\w+)(<[^(]*>)?", k)
+        short = (mm.group(1) + (mm.group(2) or "")) if mm else k[:60]
         for c, v in cs.items():
             v = sorted(v)
             res.setdefault(slot, {}).setdefault(short, {})[c] = v[len(v) // 2]
