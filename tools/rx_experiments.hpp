@@ -791,7 +791,7 @@ __global__ __launch_bounds__(1024) void k_rx_slots(RxArgs a, uint32_t T, uint32_
 // ATTR (A/B attribution only, tools/rxgather.hip; 0 in production): 1 no
 // keystream, 2 no presence atomic, 4 whole 16-B store of the tail chunk (writes
 // the row's padding), 8 no length load, 16 no realignment.
-template <int NP, int PADMODE, int ATTR = 0>
+template <int NP, int PADMODE, int ATTR = 0, int LNT = 1>
 __global__ __launch_bounds__(256) void k_rx_half(RxArgs a, uint32_t* ctl) {
   __shared__ u32x4 spad[PADMODE ? 32 * NP + 1 : 1];
   const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, hl = lane & 31u;
@@ -816,7 +816,9 @@ __global__ __launch_bounds__(256) void k_rx_half(RxArgs a, uint32_t* ctl) {
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
     const uint32_t m = 32u * q + hl;
-    A[q] = (live && m < Q) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + 16u * m)) : zero;
+    A[q] = (live && m < Q) ? (LNT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + 16u * m))
+                                  : ld16(pk + 16u * m))
+                           : zero;
   }
   const bool chk_prev = a.prev && !(a.seen && *a.seen < a.call);
   if constexpr (PADMODE) {

@@ -212,15 +212,14 @@ int main(int argc, char** argv) {
   std::vector<Var> vars = {
       {"production (round 5): begin(+claim fill, fresh flag) + k_rx_place_h (16384 blocks, whole-chunk row tails) + gated claim/re-place", PROD, 0, 0, 0},
       {"full-grid half-wave k_rx_half (P3b shape, no length-dependent loads, whole-chunk row tails) + tally + gated claim/re-place", HALF, 0, 0, 0},
+      {"production kernel, plain payload loads (nt stores)", PROD, 30, 0, 0},
+      {"production kernel, contiguous packet runs per wave, nt loads", PROD, 31, 0, 0},
+      {"production kernel, contiguous packet runs per wave, plain payload loads", PROD, 32, 0, 0},
+      {"k_rx_half, plain payload loads", HALF, 1, 0, 0},
       {"k_rx_p2: P2 shape, one chunk per lane, scalar headers, keystream per lane + tally + gated claim/re-place", P2K, 0, 0, 0},
-      {"k_rx_p2, keystream staged in LDS (one barrier)", P2K, 1, 0, 0},
-      {"k_rx_p2, length-aware loads (lengths by scalar loads first)", P2K, 2, 0, 0},
-      {"slot-linear k_rx_slots, keystream in LDS, P=11 (1023 threads) + tally + gated claim/re-place", SLOTS, 11, 1, 0},
-      {"slot-linear k_rx_slots, keystream in LDS, P=2 (186 threads)", SLOTS, 2, 1, 0},
       {"round-4 second form: k_rx_place MODE 4 (ds_bpermute realignment, header load), 8192 blocks", PROD, 7, 0, 0},
       {"production kernel, 8192 blocks", PROD, 0, 0, 8192},
       {"production (round 3): begin + place (MODE 0, 2048 blocks) + gated fill/claim/re-place", PROD_OLD, 0, 0, 2048},
-      {"full-grid place: begin + zero rare + place (one packet per half-wave, npk/8 blocks) + tally + gated claim/re-place", FULL, 0, 0, 0},
       {"production with the place kernel's presence atomics removed (MODE 1, timing only)", PROD, 1, 0, 0},
       {"production with the place kernel's realignment removed (MODE 2, timing only)", PROD, 2, 0, 0},
   };
@@ -268,7 +267,10 @@ int main(int argc, char** argv) {
       a.call = call;
       a.prev = prev;
       if (v.kind == HALF) {
-        k_rx_half<3, 0><<<static_cast<uint32_t>((a.npk + 7) / 8), 256, 0, s>>>(a, dup);
+        if (v.order == 1)
+          k_rx_half<3, 0, 0, 0><<<static_cast<uint32_t>((a.npk + 7) / 8), 256, 0, s>>>(a, dup);
+        else
+          k_rx_half<3, 0><<<static_cast<uint32_t>((a.npk + 7) / 8), 256, 0, s>>>(a, dup);
       } else if (v.kind == P2K) {
         const uint64_t waves = (a.npk * (a.slot / 16) + 62) / 63;
         const uint32_t blocks = static_cast<uint32_t>((waves + 3) / 4);
@@ -323,7 +325,13 @@ int main(int argc, char** argv) {
         k_rx_place<3, 0, 3><<<blocks, 256, 0, s>>>(a);
       else
         k_rx_place_h<3, 3><<<blocks, 256, 0, s>>>(a);  // production
-    } else if (v.kind == PROD && v.order == 7)
+    } else if (v.kind == PROD && v.order == 30)
+      k_rx_place_h<3, 2><<<blocks, 256, 0, s>>>(a);
+    else if (v.kind == PROD && v.order == 31)
+      k_rx_place_h<3, 3, 1><<<blocks, 256, 0, s>>>(a);
+    else if (v.kind == PROD && v.order == 32)
+      k_rx_place_h<3, 2, 1><<<blocks, 256, 0, s>>>(a);
+    else if (v.kind == PROD && v.order == 7)
       k_rx_place<3, 4, 3><<<blocks, 256, 0, s>>>(a);
     else if (v.kind == PROD && v.order == 1)
       k_rx_place<3, 1, 3><<<blocks, 256, 0, s>>>(a);

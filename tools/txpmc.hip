@@ -86,7 +86,7 @@ int main(int argc, char** argv) {
     std::function<void(const TxArgs&)> go;
   };
   std::vector<V> vs = {
-      {"production k_tx_c<10,3> (ATTR 0)",
+      {"production k_tx_c<10,3> (ATTR 0; round 5: plain data loads)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 0><<<grid, 256, cap>>>(a); }},
       {"no wire_lens / status stores (ATTR 1)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 1><<<grid, 256, cap>>>(a); }},
@@ -96,9 +96,9 @@ int main(int argc, char** argv) {
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 3><<<grid, 256, cap>>>(a); }},
       {"XCD-contiguous blocks (ATTR 4)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 4><<<grid, 256, cap>>>(a); }},
-      {"plain data loads (ATTR 8)",
+      {"nontemporal data loads, the round-4 production (ATTR 8)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 8><<<grid, 256, cap>>>(a); }},
-      {"XCD-contiguous blocks, plain data loads (ATTR 12)",
+      {"XCD-contiguous blocks, nontemporal data loads (ATTR 12)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 12><<<grid, 256, cap>>>(a); }},
       {"no wire_lens / status stores + k_tx_lens (ATTR 1 + lens kernel)", [&](const TxArgs& a) {
          k_tx_c<10, 3, kTxNT, true, true, 1><<<grid, 256, cap>>>(a);

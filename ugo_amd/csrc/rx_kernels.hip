@@ -210,7 +210,10 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 // Every lane loads the bytes [0, min(len, S + 6)) of its packet before the
 // header is known (a packet later rejected for its flag or window is loaded
 // and dropped, like a duplicate).  Realignment as MODE 4.
-template <int NP, int NT = 3>
+// RUNS (A/B): 0 = grid-stride over packet pairs (wave w: pairs w, w + nwaves,
+// ...); 1 = each wave takes one contiguous run of packet pairs, so the line a
+// packet's slot shares with the next packet's is read by the same wave.
+template <int NP, int NT = 3, int RUNS = 0>
 __global__ __launch_bounds__(256) void k_rx_place_h(RxArgs a) {
   if (rx_gated_off(a)) return;
   __shared__ uint32_t bstats[5];
@@ -235,7 +238,13 @@ __global__ __launch_bounds__(256) void k_rx_place_h(RxArgs a) {
     }
   }
   RxAccount acct;
-  const uint64_t first = 2 * wave, step = 2 * nwaves, end = a.npk;
+  uint64_t first = 2 * wave, step = 2 * nwaves, end = a.npk;
+  if constexpr (RUNS) {  // wave w: packets [w * run, (w + 1) * run), run even
+    const uint64_t run = ((a.npk + nwaves - 1) / nwaves + 1) & ~1ull;
+    first = wave * run;
+    step = 2;
+    end = min(a.npk, first + run);
+  }
   const int hsrc = static_cast<int>(half * 32u) * 4;  // lane 0 of this half
   uint64_t i = first + half;
   uint32_t ln = i < end ? a.lens[i] : 0u;

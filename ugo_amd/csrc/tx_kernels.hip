@@ -64,6 +64,16 @@ __device__ __forceinline__ void put_header(V4& x, uint32_t seq, uint32_t flag) {
 // of the same accesses is 454 us cold
 constexpr int kTxNT = 3;
 constexpr bool kTxSL = true;
+// Data-packet loads: plain, not nontemporal (round 5).  A wave reads 1 KiB of
+// each of a group's 10 packets, and slots of 1488 B put those spans' ends in
+// the middle of 128-B lines that the neighbouring wave reads too: with
+// nontemporal loads such a line was gone from L2 when the second wave asked,
+// and was fetched again -- the 9 % of excess read bytes round 4 could not
+// place (2 x FETCH_SIZE 1.0896 x the algorithmic bytes; plain loads 1.0656,
+// and with XCD-contiguous blocks as well 1.0111).  Plain loads: 412.7 vs
+// 455.0 us (tools/txpmc.hip, profiles/r5/txpmc/); the XCD-contiguous deal,
+// despite its exact traffic, 451.9.
+constexpr int kTxLoadNT = 0;
 
 struct TxItem {
   uint64_t g;        // absolute group
@@ -84,7 +94,7 @@ struct TxItem {
 // skips the wire_lens / status stores, bit 1 replaces the parity network by a
 // plain XOR of the inputs (the compute-free twin: wrong parity on purpose),
 // bit 2 deals the blocks XCD-contiguously (consecutive blocks share one L2),
-// bit 3 loads the data packets with plain instead of nontemporal loads.
+// bit 3 loads the data packets nontemporally (the round-4 policy).
 template <int DN, int NT, bool SL, bool PL = false, int ATTR = 0>
 __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x, const u32x4* padl = nullptr) {
   TxItem t{};
@@ -149,7 +159,7 @@ __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x,
   for (int k = 0; k < DN; ++k) {
     x[k] = V4{{0u, 0u, 0u, 0u}};
     if (k < static_cast<int>(a.d) && t.o < Ls[k])
-      x[k] = load16<(ATTR & 8) ? 0 : 1>(src + static_cast<uint64_t>(k) * a.slot_in);
+      x[k] = load16<(ATTR & 8) ? 1 : kTxLoadNT>(src + static_cast<uint64_t>(k) * a.slot_in);
   }
 #pragma unroll
   for (int k = 0; k < DN; ++k) {
