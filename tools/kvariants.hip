@@ -533,6 +533,21 @@ int main(int argc, char** argv) {
         b.ogstride = pitch;
         b.orstride = G * pitch;
       }
+      // round 5 (LDPOL mode): load policy -- plain survivor loads with nt stores
+      vars.push_back({"LDPOL dec INTO production k_apply_p nt3 (nt loads + stores)", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"LDPOL dec INTO k_apply_p nt2 (plain loads, nt stores)", dec_bytes, [=]() {
+        hipLaunchKernelGGL((k_apply_p<10, 1, 2>), dim3(grid), dim3(256), 0, 0, rotk[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"LDPOL enc production k_encode_g<10,3,2,8,256,13>", enc_bytes, [=]() {
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[(*cnt)++ & 3]); }, {}});
+      vars.push_back({"LDPOL pair production (enc + dec INTO nt3)", enc_bytes + dec_bytes, [=]() {
+        const int r = (*cnt)++ & 3;
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[r]);
+        hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[r]); }, {}});
+      vars.push_back({"LDPOL pair enc + dec INTO nt2 (plain survivor loads)", enc_bytes + dec_bytes, [=]() {
+        const int r = (*cnt)++ & 3;
+        hipLaunchKernelGGL((k_encode_g<10, 3, 2, 8, 256, 13>), dim3(grid), dim3(256), 0, 0, rot[r]);
+        hipLaunchKernelGGL((k_apply_p<10, 1, 2>), dim3(grid), dim3(256), 0, 0, rotk[r]); }, {}});
       vars.push_back({"COLD dec INTO production k_apply_p nt3", dec_bytes, [=]() {
         hipLaunchKernelGGL((k_apply_p<10, 1, 3>), dim3(grid), dim3(256), 0, 0, rotk[(*cnt)++ & 3]); }, {}});
       vars.push_back({"COLD dec INTO k_apply_p lds-dma 10", dec_bytes, [=]() {
