@@ -3,7 +3,8 @@
 // ugo_amd/csrc/tx_kernels.hip: 1 = no wire_lens / status stores, 2 = the
 // compute-free twin: XOR instead of the network, 3 = both), each launched
 // `reps` times over 3 rotated cold input / output sets, one variant after the
-// other, so rocprofv3 --pmc passes attribute per kernel name.  argv: reps,
+// other in interleaved rounds (a cache-evicting sweep before each sample),
+// rocprofv3 --pmc passes attribute per kernel name.  argv: rounds,
 // slot (1488: ugo's packets in 16-B slots; 1536: 128-B aligned slots).
 // Timing per variant (hipEvents, median) on stdout as JSON.  Not product code.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/txpmc tools/txpmc.hip
@@ -36,6 +37,13 @@ using namespace ugo::kern;
       exit(1);                                                                   \
     }                                                                            \
   } while (0)
+
+__global__ __launch_bounds__(256) void k_flush(const u32x4* a, uint32_t* out, uint64_t n16) {
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  if (i >= n16) return;
+  const u32x4 v = a[i];
+  if ((v.x ^ v.y ^ v.z ^ v.w) == 0x9e3779b9u) out[0] = v.x;
+}
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
@@ -143,20 +151,33 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double alg = double(G) * (d + n) * max_len;
-  for (auto& v : vs) {
-    std::vector<float> t;
-    for (int r = 0; r < reps + 3; ++r) {
+  // interleaved rounds: every variant once per round, each sample after a
+  // cache-evicting sweep, 3 launches on the 3 rotated sets; medians
+  const uint64_t fl16 = (768ull << 20) / 16;
+  uint8_t* fl = nullptr;
+  CK(hipMalloc(&fl, fl16 * 16));
+  CK(hipMemset(fl, 1, fl16 * 16));
+  std::vector<std::vector<float>> t(vs.size());
+  for (int w = 0; w < 2; ++w)
+    for (auto& v : vs) v.go(rot[w % 3]);
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < reps; ++r)
+    for (size_t k = 0; k < vs.size(); ++k) {
+      k_flush<<<static_cast<uint32_t>((fl16 + 255) / 256), 256>>>(reinterpret_cast<const u32x4*>(fl),
+                                                                  reinterpret_cast<uint32_t*>(fl), fl16);
       CK(hipEventRecord(e0));
-      v.go(rot[r % 3]);
+      for (int j = 0; j < 3; ++j) vs[k].go(rot[j]);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
-      if (r >= 3) t.push_back(ms * 1000.f);
+      t[k].push_back(ms * 1000.f / 3.f);
     }
-    std::sort(t.begin(), t.end());
-    printf("{\"variant\":\"%s\",\"slot\":%u,\"median_us\":%.2f,\"frac\":%.4f}\n", v.name.c_str(), slot,
-           t[t.size() / 2], alg / (t[t.size() / 2] * 1e-6) / 8e12);
+  for (size_t k = 0; k < vs.size(); ++k) {
+    std::sort(t[k].begin(), t[k].end());
+    const double med = t[k][t[k].size() / 2];
+    printf("{\"variant\":\"%s\",\"slot\":%u,\"median_us\":%.2f,\"min_us\":%.2f,\"frac\":%.4f}\n",
+           vs[k].name.c_str(), slot, med, t[k][0], alg / (med * 1e-6) / 8e12);
   }
   CK(hipGetLastError());
   return 0;

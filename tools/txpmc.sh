@@ -13,11 +13,11 @@ if grep -q "TCC_EA0_RDREQ_32B" "$OUT/avail.txt" && grep -q "TCC_EA0_RDREQ\b\|TCC
   EXTRA="TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_sum"
 fi
 for slot in 1488 1536; do
-  timeout -k 10 90 tools/txpmc 20 $slot > "$OUT/time_$slot.jsonl" 2> "$OUT/time_$slot.err" || { echo "txpmc $slot failed"; exit 1; }
+  timeout -k 10 90 tools/txpmc 15 $slot > "$OUT/time_$slot.jsonl" 2> "$OUT/time_$slot.err" || { echo "txpmc $slot failed"; exit 1; }
   for ctr in FETCH_SIZE WRITE_SIZE "$EXTRA"; do
     [ -n "$ctr" ] || continue
     tag=$(echo $ctr | cut -d' ' -f1)
-    timeout -s KILL 90 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/${slot}_$tag" -o run -- tools/txpmc 20 $slot \
+    timeout -s KILL 90 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/${slot}_$tag" -o run -- tools/txpmc 15 $slot \
       > "$OUT/${slot}_$tag.log" 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "pmc $slot $tag rc=$rc"; tail -3 "$OUT/${slot}_$tag.log"; exit $rc; }
   done
