@@ -24,6 +24,35 @@ LaunchTimer*& current_timer() {
   static thread_local LaunchTimer* t = nullptr;
   return t;
 }
+
+// wire_lens and status of a TX batch in a pass of their own: one thread per
+// wire packet, consecutive threads on consecutive lengths, so a wave writes
+// whole 64-B lines of the length array.  (A/B: k_tx_c ATTR 1 + this kernel
+// against k_tx_c, whose chunk-0 lanes store each group's 13 lengths and its
+// status one by one.)  Results as tx_data / tx_parity_out:
+// bad group -> status ERR_SHARD_SIZE, every length 0; header-only group ->
+// ERR_SHARD_NO_DATA, data lengths kept, parity lengths 0; else 0, data lengths,
+// parity lengths = the group's longest data packet.
+__global__ __launch_bounds__(256) void k_tx_lens(TxArgs a) {
+  const uint32_t n = a.d + a.p;
+  const uint64_t t = blockIdx.x * 256ull + threadIdx.x;
+  if (t >= a.groups * n) return;
+  const uint64_t gl = t / n;
+  const uint32_t r = static_cast<uint32_t>(t - gl * n);
+  const uint64_t g = a.g0 + gl;
+  const uint16_t* L = a.lens + g * a.d;
+  bool bad = false;
+  uint32_t maxsz = 0, mine = 0;
+  for (uint32_t k = 0; k < a.d; ++k) {
+    const uint32_t Lk = L[k];
+    bad |= Lk < kFecHeader || Lk > a.max_len;
+    maxsz = max(maxsz, Lk);
+    if (k == r) mine = Lk;
+  }
+  const bool nodata = maxsz <= kFecHeader;
+  a.wire_lens[g * n + r] = static_cast<uint16_t>(bad ? 0u : (r < a.d ? mine : (nodata ? 0u : maxsz)));
+  if (r == 0 && a.status) a.status[g] = bad ? kBadLength : (nodata ? kNoData : 0);
+}
 }  // namespace kern
 }  // namespace ugo
 
@@ -104,6 +133,10 @@ int main(int argc, char** argv) {
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 3><<<grid, 256, cap>>>(a); }},
       {"XCD-contiguous blocks (ATTR 4)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 4><<<grid, 256, cap>>>(a); }},
+      {"runs of 4 blocks per XCD (ATTR 16)",
+       [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 16><<<grid, 256, cap>>>(a); }},
+      {"runs of 8 blocks per XCD (ATTR 32)",
+       [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 32><<<grid, 256, cap>>>(a); }},
       {"nontemporal data loads, the round-4 production (ATTR 8)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 8><<<grid, 256, cap>>>(a); }},
       {"XCD-contiguous blocks, nontemporal data loads (ATTR 12)",

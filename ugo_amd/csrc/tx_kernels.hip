@@ -94,7 +94,9 @@ struct TxItem {
 // skips the wire_lens / status stores, bit 1 replaces the parity network by a
 // plain XOR of the inputs (the compute-free twin: wrong parity on purpose),
 // bit 2 deals the blocks XCD-contiguously (consecutive blocks share one L2),
-// bit 3 loads the data packets nontemporally (the round-4 policy).
+// bit 3 loads the data packets nontemporally (the round-4 policy), bit 4 / 5
+// deal runs of 4 / 8 consecutive blocks to one XCD within windows of 32 / 64
+// blocks (neighbours share an L2, the XCDs stay on nearby addresses).
 template <int DN, int NT, bool SL, bool PL = false, int ATTR = 0>
 __device__ __forceinline__ TxItem tx_data(const TxArgs& a, uint32_t item, V4* x, const u32x4* padl = nullptr) {
   TxItem t{};
@@ -230,9 +232,17 @@ __device__ __forceinline__ bool tx_no_window(const TxArgs& a, const TxItem& t) {
 // (10,3) / (32,8): the compile-time XOR networks of k_encode_c.
 // PL: the keystream staged once per block in dynamic LDS (needs a.pad and
 // 16 * chunks bytes of dynamic LDS), instead of one 16-B global load per thread.
+template <int RUN>
+__device__ __forceinline__ uint32_t block_run() {  // hardware block b on XCD b % 8 -> runs of RUN logical blocks
+  const uint32_t b = blockIdx.x, W = 8u * RUN;
+  if (b >= gridDim.x / W * W) return b;
+  return (b / W) * W + (b & 7u) * RUN + (b >> 3) % RUN;
+}
+
 template <int D, int P, int NT = kTxNT, bool SL = kTxSL, bool PL = false, int ATTR = 0>
 __global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
-  const uint32_t item = block_id<(ATTR & 4) ? 1 : 0>() * 256u + threadIdx.x;
+  const uint32_t bid = (ATTR & 16) ? block_run<4>() : (ATTR & 32) ? block_run<8>() : block_id<(ATTR & 4) ? 1 : 0>();
+  const uint32_t item = bid * 256u + threadIdx.x;
   extern __shared__ u32x4 padl[];
   if constexpr (PL) {
     for (uint32_t i = threadIdx.x; i < a.chunks; i += 256u) padl[i] = *reinterpret_cast<const u32x4*>(a.pad + 16u * i);
@@ -245,35 +255,6 @@ __global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
   tx_cparity<D, P, NT, ATTR>(a, t, x, std::make_integer_sequence<int, P>{});
   if constexpr (!(ATTR & 1))
     if (t.o == 0 && a.status) a.status[t.g] = 0;
-}
-
-// wire_lens and status of a TX batch in a pass of their own: one thread per
-// wire packet, consecutive threads on consecutive lengths, so a wave writes
-// whole 64-B lines of the length array.  (A/B: k_tx_c ATTR 1 + this kernel
-// against k_tx_c, whose chunk-0 lanes store each group's 13 lengths and its
-// status one by one, tools/txpmc.hip.)  Results as tx_data / tx_parity_out:
-// bad group -> status ERR_SHARD_SIZE, every length 0; header-only group ->
-// ERR_SHARD_NO_DATA, data lengths kept, parity lengths 0; else 0, data lengths,
-// parity lengths = the group's longest data packet.
-__global__ __launch_bounds__(256) void k_tx_lens(TxArgs a) {
-  const uint32_t n = a.d + a.p;
-  const uint64_t t = blockIdx.x * 256ull + threadIdx.x;
-  if (t >= a.groups * n) return;
-  const uint64_t gl = t / n;
-  const uint32_t r = static_cast<uint32_t>(t - gl * n);
-  const uint64_t g = a.g0 + gl;
-  const uint16_t* L = a.lens + g * a.d;
-  bool bad = false;
-  uint32_t maxsz = 0, mine = 0;
-  for (uint32_t k = 0; k < a.d; ++k) {
-    const uint32_t Lk = L[k];
-    bad |= Lk < kFecHeader || Lk > a.max_len;
-    maxsz = max(maxsz, Lk);
-    if (k == r) mine = Lk;
-  }
-  const bool nodata = maxsz <= kFecHeader;
-  a.wire_lens[g * n + r] = static_cast<uint16_t>(bad ? 0u : (r < a.d ? mine : (nodata ? 0u : maxsz)));
-  if (r == 0 && a.status) a.status[g] = bad ? kBadLength : (nodata ? kNoData : 0);
 }
 
 // Any other geometry: coefficients from the encode descriptor (uniform, so
