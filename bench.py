@@ -861,7 +861,7 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             w[:, :6] = hdr ^ pad[:6]
             ring = fec.host_alloc(npk * slot).reshape(npk, slot)
             lens = fec.host_alloc(npk * 2).view(np.uint16)
-            out = fec.host_alloc(G * p * pitch).reshape(G, p, pitch)
+            out = fec.host_alloc(G * p * pitch).reshape(G * p, pitch)
             bufs.extend([ring, lens.view(np.uint8), out])
             torch.from_numpy(ring).copy_(w)
             lens[:] = 1476
@@ -884,17 +884,17 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             lo = torch.empty((G, p, pitch), dtype=torch.uint8, device=dev)
             enc.reconstruct_list(bat, pr, lst, cnt, lo, shard_size=S, data_only=True)
             k = int(cnt.item())
-            nrec, gidx, status, out, _ = box["r"]
-            ok = nrec == k and bool(np.array_equal(gidx[:k], lst[:k].cpu().numpy().view(np.uint32)))
-            if ok:
-                pm = pr[lst[:k].long()]
-                ed = torch.zeros(k, dtype=torch.int64, device=dev)
-                for r in range(d):
-                    ed += ((pm >> r) & 1) == 0
-                ho = torch.from_numpy(out[:k]).to(dev)
-                for i in range(p):
-                    sel = ed > i
-                    ok = ok and bool(torch.equal(ho[sel, i, :S], lo[:k][sel, i, :S]))
+            nrec, index, out, _ = box["r"]
+            # ugo's `recovered` order: entries ascending, each entry's lost data rows ascending
+            pm = pr[lst[:k].long()]
+            ed, okg = lost_and_recoverable(pm, d, n)
+            lost = (((pm[:, None] >> torch.arange(d, device=dev)) & 1) == 0) & okg[:, None]
+            jj, rr = torch.nonzero(lost, as_tuple=True)
+            want_index = lst[:k].long()[jj] * n + rr
+            want_rows = lo[:k][(torch.arange(p, device=dev)[None, :] < ed[:, None]) & okg[:, None]]
+            ok = nrec == int(jj.numel()) and bool(np.array_equal(index[:nrec].astype(np.int64),
+                                                                  want_index.cpu().numpy()))
+            ok = ok and bool(torch.equal(torch.from_numpy(out[:nrec, :S]).to(dev), want_rows[:, :S]))
             del bat, pr, lo
         ok_all = ok_all and ok
         # the zero-copy alternative: rx_assemble reads the pinned ring over PCIe itself (no DMA
@@ -915,8 +915,8 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             enc.rx_assemble(ring_t, lens_t, zc["zb"], zc["zp"], shard_size=S, pad=zc["pad"])
             enc.lossy_groups(zc["zp"], data_only=True, out=zc["zl"], count=zc["zc"])
             enc.reconstruct_list(zc["zb"], zc["zp"], zc["zl"], zc["zc"], zc["zo"], shard_size=S, data_only=True)
-            k = int(zc["zc"].item())
-            torch.from_numpy(box["out"][:k]).copy_(zc["zo"][:k])
+            k = int(zc["zc"].item())  # entry form: k entries x p row slots cross PCIe
+            torch.from_numpy(box["out"][:k * p]).copy_(zc["zo"][:k].reshape(k * p, pitch))
             torch.cuda.synchronize(dev)
 
         t_zc = None
@@ -927,16 +927,19 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
         npk = box.get("npk", 0)
         nrec = box["r"][0] if "r" in box else 0
         wire_bytes = int(reduce_sum([npk * 1476], world)[0])
-        pcie = npk * (slot + 2) + nrec * p * S
+        pcie = npk * (slot + 2) + nrec * S
         res["rx_host"] = {
-            "groups_per_rank": G, "packets_per_rank": npk, "loss": 0.05, "rc4": True, "lossy_groups_rank0": nrec,
+            "groups_per_rank": G, "packets_per_rank": npk, "loss": 0.05, "rc4": True, "recovered_shards_rank0": nrec,
             "rx_ms": round(t_rx * 1e3, 3), "wire_GBps": round(wire_bytes / t_rx / 1e9, 2),
             "pcie_GBps_per_gpu": round(pcie / t_rx / 1e9, 2), "rank0_alone_ms": round(t_rx_mine * 1e3, 3),
             "zero_copy_ring_ms": None if t_zc is None else round(t_zc * 1e3, 3),
+            "zero_copy_note": "rx_assemble reading the pinned ring in place, then the public lossy list + "
+                              "entry-form list reconstruct, D2H of every entry's p row slots",
             "zero_copy_wire_GBps": None if t_zc is None else round(wire_bytes / t_zc / 1e9, 2),
             "verify_vs_device_path": ok,
             "path": "pinned ring -> H2D in >= 4 chunks on 2 copy streams, each chunk assembled as it lands -> "
-                    "lossy-group list -> data-only list reconstruct -> D2H of the recovered shards only"}
+                    "lossy-group list with row offsets -> data-only list reconstruct, row-compact -> D2H of "
+                    "the recovered shards only (ugo's `recovered` order)"}
         box.clear()
         # ---- TX
         tb = {}
@@ -1279,6 +1282,20 @@ def rc4_pad(nbytes, dev):
     return torch.frombuffer(bytearray(fec.rc4_keystream(b"1234567890123456", nbytes)), dtype=torch.uint8).to(dev)
 
 
+def lost_and_recoverable(pm, d, n):
+    """Per presence mask: erased data rows, and whether >= d of the n rows are present."""
+    import torch
+
+    ed = torch.zeros(pm.shape, dtype=torch.int64, device=pm.device)
+    have = torch.zeros(pm.shape, dtype=torch.int64, device=pm.device)
+    for r in range(n):
+        bit = (pm >> r) & 1
+        have += bit
+        if r < d:
+            ed += bit == 0
+    return ed, have >= d
+
+
 def rx_tx_leg(args, dev_index, reps=12):
     """The §8f kernels on the driver's clock, on every rank
     (rank 0 reports its own leg plus the max over ranks of
@@ -1415,13 +1432,10 @@ def rx_tx_leg(args, dev_index, reps=12):
         # the two forms agree: entry j's slot i = group lst[j]'s output i of reconstruct_into
         k = int(cnts[0].item())
         lg = lsts[0][:k].long()
-        ed = torch.zeros(k, dtype=torch.int64, device=dev)
-        pm = pres[0][lg]
-        for r in range(d):
-            ed += ((pm >> r) & 1) == 0
+        ed, okg = lost_and_recoverable(pres[0][lg], d, n)
         ok_list = k == int((lost_data > 0).sum())
         for i in range(p):
-            sel = ed > i
+            sel = (ed > i) & okg  # groups below d shards: no output in either form
             ok_list = ok_list and bool(torch.equal(louts[0][:k][sel, i, :S], outs[0][i, lg[sel], :S]))
         rec_list_k = kernel_ms(rec_list, fec.KERNEL_IDS["reconstruct"], reps)
         # ceilings: the compute-free twins of both forms on the same buffers (after the checks: wrong bytes)

@@ -343,27 +343,26 @@ int ugo_fec_tx_assemble(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, const
  * the window [first_group, first_group + groups), one call per chunk, the first
  * copy of a seqid in ring order wins), then every group with a lost data
  * shard is recovered (ugo_fec_lossy_groups + ugo_fec_reconstruct_list,
- * DATA_ONLY) and only its recovered shards come back:
- *   *n_out        the number of groups with a lost data shard (as listed by
- *                 ugo_fec_lossy_groups, fewer than d shards included);
- *   out_groups[j] group j's index in the window (ascending), j < min(*n_out,
- *                 max_out) -- entries past max_out are not returned;
- *   out_status[j] (nullable) its Reconstruct status (UGO_FEC_ERR_TOO_FEW_SHARDS
- *                 when fewer than d shards arrived: no rows then);
- *   out + (j*min(d,p) + i)*out_row_stride: its i-th lost data shard in
- *                 ascending row order, shard_size bytes (the `recovered` slices
- *                 input returns, ugo/fec.go:203-207);
+ * DATA_ONLY) and only the recovered shards come back, row-compact, in the
+ * order ugo's input appends them to `recovered` (ugo/fec.go:203-207: groups
+ * ascending, each group's lost data rows ascending; a group with fewer than d
+ * shards recovers nothing, as there):
+ *   *n_out        the number of recovered data shards;
+ *   out + r*out_row_stride: recovered shard r, shard_size bytes, for
+ *                 r < min(*n_out, max_out) -- shards past max_out are not
+ *                 returned (max_out = 0: no recovery; *n_out still counts them);
+ *   out_index[r]  its place: (window group) * (d+p) + row, i.e. its seqid
+ *                 minus first_group * (d+p);
  *   present_out   (host u64[groups], nullable) the presence masks after
  *                 assembly; stats_out (host u32[5], nullable) the counts of
  *                 ugo_fec_rx_assemble (set, not added).
- * pad: host memory, >= slot_stride bytes, or NULL.  Synchronous.  d+p <= 16.
- * The device batch ([d+p][groups][round_up(shard_size, 16)]) and the staging
+ * pad: host memory, >= slot_stride bytes, or NULL.  Synchronous.  d+p <= 16,
+ * groups*(d+p) < 2^32.  The device batch ([d+p][groups][round_up(shard_size, 16)]) and the staging
  * are the engine's (stream-ordered scratch). */
 int ugo_fec_rx_recover_host(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, const uint16_t* lens,
                             size_t npackets, const uint8_t* pad, uint64_t first_group, size_t groups,
                             size_t shard_size, uint64_t* present_out, uint32_t* stats_out, uint8_t* out,
-                            size_t out_row_stride, size_t max_out, uint32_t* out_groups, int8_t* out_status,
-                            size_t* n_out);
+                            size_t out_row_stride, size_t max_out, uint32_t* out_index, size_t* n_out);
 
 /* ugo_fec_tx_assemble with every buffer in host memory (pinned for full-rate
  * DMA): the groups go through the device in chunks, each chunk's data packets

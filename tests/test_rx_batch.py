@@ -346,11 +346,11 @@ def test_rx_assemble_first_copy_wins_across_calls(gpu, encrypt, S, slot):
                                                                 (False, 0, None, False)])
 def test_rx_recover_host_vs_oracle(gpu, encrypt, first_group, max_out, pinned):
     """ugo_fec_rx_recover_host: a packet ring in host memory (loss, duplicates,
-    junk, shuffled; >= 4 chunks) in, the lost data shards of every lossy group
-    out, against the oracle: placement (fec_ref decode + grouping), then
-    Reconstruct (rs_ref) of each group with a lost data shard; statuses, stats
-    and presence masks too.  max_out < the lossy count: only the first
-    max_out groups come back, the count is still the total."""
+    junk, shuffled; >= 4 chunks) in, the recovered data shards out, row-compact
+    in ugo's `recovered` order, against the oracle: placement (fec_ref decode +
+    grouping), then Reconstruct (rs_ref) of each group with a lost data shard;
+    stats and presence masks too.  max_out < the recovered count: only the
+    first max_out shards come back, the count is still the total."""
     d, p, n, S, pitch, slot = 10, 3, 13, 1470, 1472, 1488
     total_groups, G = 300, 256
     pk = _packets(total_groups, 23, False)
@@ -382,22 +382,22 @@ def test_rx_recover_host_vs_oracle(gpu, encrypt, first_group, max_out, pinned):
     exp = np.ascontiguousarray(want[:, :, :S])
     rc, exp_st = rs_ref.c_reconstruct(d, p, exp, masks, data_only=True)
     lossy = [g for g in range(G) if (~int(masks[g])) & ((1 << d) - 1)]
+    # ugo's `recovered` (ugo/fec.go:203-207): every lost data shard of each group that Reconstruct
+    # rebuilds, groups ascending, rows ascending; a group below d shards recovers nothing
+    rec = [(g, r) for g in range(G) if exp_st[g] == 0 for r in range(d) if not (int(masks[g]) >> r) & 1]
+    assert any(exp_st[g] != 0 for g in lossy), "the case should hold an unrecoverable lossy group"
     codec = fec.New(d, p)
     pres = np.zeros(G, np.uint64)
-    nrec, gidx, st, out, got_stats = codec.rx_recover_host(
+    nrec, index, out, got_stats = codec.rx_recover_host(
         slots, lens, S, G, first_group=first_group, pad=rc4_ref.keystream(KEY, slot) if encrypt else None,
         max_out=max_out, present_out=pres)
-    assert nrec == len(lossy)
-    m = len(lossy) if max_out is None else min(max_out, len(lossy))
-    assert gidx[:m].tolist() == lossy[:m]
+    assert nrec == len(rec)
+    m = len(rec) if max_out is None else min(max_out, len(rec))
+    assert index[:m].tolist() == [g * n + r for g, r in rec[:m]]
     assert np.array_equal(pres, masks)
     assert got_stats.tolist() == stats
-    for j, g in enumerate(lossy[:m]):
-        assert st[j] == exp_st[g], (j, g)
-        if exp_st[g] == 0:
-            lost = [r for r in range(d) if not (int(masks[g]) >> r) & 1]
-            for i, r in enumerate(lost):
-                assert np.array_equal(out[j, i, :S], exp[g, r]), (j, g, r)
+    for j, (g, r) in enumerate(rec[:m]):
+        assert np.array_equal(out[j, :S], exp[g, r]), (j, g, r)
     if pinned:
         fec.host_free(slots.reshape(-1))
         fec.host_free(lens.view(np.uint8))

@@ -86,6 +86,17 @@ __device__ __forceinline__ uint8_t* out_row(const Batch& a, uint8_t* gp, uint64_
                : gp + static_cast<uint64_t>(r) * a.rstride;
 }
 
+// List forms: entry g's output i at out + oent + i*orstride, where oent is
+// the entry's offset -- row-compact (a.rowoff) or entry-strided.
+__device__ __forceinline__ uint64_t list_out_off(const Batch& a, uint64_t g) {
+  return a.rowoff ? static_cast<uint64_t>(a.rowoff[g]) * a.orstride : g * a.ogstride;
+}
+
+__device__ __forceinline__ uint8_t* out_row_at(const Batch& a, uint8_t* gp, uint64_t oent, uint32_t off, uint32_t r,
+                                              uint32_t i) {
+  return a.out ? a.out + oent + static_cast<uint64_t>(i) * a.orstride + off : gp + static_cast<uint64_t>(r) * a.rstride;
+}
+
 template <int D, int NT>
 __device__ __forceinline__ void load_rows(V4* x, const uint8_t* gp, uint64_t rstride) {
 #pragma unroll
@@ -208,6 +219,7 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
   const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
   if (st != 0 || e == 0) return;
   uint8_t* gp = a.base + grow * a.gstride + static_cast<uint64_t>(c) * 16u;
+  const uint64_t oent = LIST ? list_out_off(a, g) : g * a.ogstride;
   constexpr int NW = (DMAX + 3) / 4;
   uint32_t rows[NW];
 #pragma unroll
@@ -230,7 +242,8 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
 #pragma unroll
     for (int w = 0; w < NW; ++w) cw[w] = ld32(coef + i * a.dpad + 4 * w);
     const V4 y = horner_var<DMAX>(x, cw);
-    store16<NT>(out_row(a, gp, g, c * 16u, orow[i], i), y, nb);
+    store16<NT>(out_row_at(a, gp, oent, c * 16u, orow[i], i), y, nb);
+    if (LIST && a.rowid && c == 0) a.rowid[a.rowoff[g] + i] = static_cast<uint32_t>(grow * a.n + orow[i]);
   }
 }
 
@@ -512,6 +525,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t mB;  // all-ones in group-B lanes; opaque to the optimizer (see p_tables)
   asm("v_mov_b32 %0, %1" : "=v"(mB) : "v"(inB ? ~0u : 0u));
   uint8_t* gp = a.base + grow * a.gstride + static_cast<uint64_t>(c) * 16u;
+  const uint64_t oent = LIST ? list_out_off(a, g) : g * a.ogstride;
   const uint32_t nb = a.S - c * 16u;
   V4 x[DMAX];
   if constexpr (GLR > 0) {  // survivors 0..GLR-1 by LDS-DMA nt, the rest to registers (host: d == 10)
@@ -550,7 +564,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (int i = 0; i < EMAX; ++i) {
     if (i >= static_cast<int>(e)) continue;
     const uint32_t r = (orows >> (8 * i)) & 0xffu;
-    store16<NT>(out_row(a, gp, g, c * 16u, r, i), acc[i], nb);
+    store16<NT>(out_row_at(a, gp, oent, c * 16u, r, i), acc[i], nb);
+    if (LIST && a.rowid && c == 0) a.rowid[a.rowoff[g] + i] = static_cast<uint32_t>(grow * a.n + r);
   }
   if (wst) a.status[g] = 0;
 }
@@ -1894,84 +1909,124 @@ hipError_t launch_apply(int mode, int dmax, const Batch& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------- list form
-// Lossy-group list in two launches, no atomics, ascending group order: block b
-// of k_lossy_count counts the groups of its kLossyPerBlock that have an erased
-// row to rebuild; block b of k_lossy_write sums the counts of blocks < b (its
-// output offset), scans its own groups in order and writes their indices; the
-// last block also writes the total.
-__device__ __forceinline__ bool lossy(const uint64_t* present, uint64_t g, uint64_t nmask, uint64_t dmask) {
-  return ((~present[g]) & nmask & dmask) != 0;
+// Lossy-group list in two launches, ascending group order, no global atomics:
+// block b of k_lossy_count counts the groups of its kLossyPerBlock that have an
+// erased row to rebuild, and the rows they rebuild; block b of k_lossy_write
+// sums both counts over the blocks < b (its output offsets), scans its own
+// groups in order and writes their indices (and row offsets); the last block
+// also writes the totals.
+__device__ __forceinline__ uint32_t lossy_rows(uint64_t m, uint64_t nmask, uint64_t dmask, uint32_t d,
+                                               bool& lossy) {
+  const uint64_t lost = ~m & nmask & dmask;
+  lossy = lost != 0;
+  return static_cast<uint32_t>(__popcll(m & nmask)) >= d ? static_cast<uint32_t>(__popcll(lost)) : 0u;
 }
 
 __global__ __launch_bounds__(1024) void k_lossy_count(const uint64_t* present, uint64_t groups, uint64_t nmask,
-                                                      uint64_t dmask, uint32_t* work) {
-  __shared__ uint32_t tot;
-  if (threadIdx.x == 0) tot = 0;
+                                                      uint64_t dmask, uint32_t d, uint32_t* work) {
+  __shared__ uint32_t tot[2];
+  if (threadIdx.x < 2) tot[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t g0 = uint64_t(blockIdx.x) * kLossyPerBlock;
-  uint32_t c = 0;
+  uint32_t c = 0, r = 0;
   for (uint32_t k = threadIdx.x; k < kLossyPerBlock; k += 1024u) {
     const uint64_t g = g0 + k;
-    if (g < groups && lossy(present, g, nmask, dmask)) ++c;
+    if (g >= groups) break;
+    bool l;
+    const uint32_t rows = lossy_rows(present[g], nmask, dmask, d, l);
+    c += l;
+    r += rows;
   }
   c = __reduce_add_sync(~0ull, c);
-  if ((threadIdx.x & 63u) == 0 && c) atomicAdd(&tot, c);
+  r = __reduce_add_sync(~0ull, r);
+  if ((threadIdx.x & 63u) == 0) {
+    if (c) atomicAdd(&tot[0], c);
+    if (r) atomicAdd(&tot[1], r);
+  }
   __syncthreads();
-  if (threadIdx.x == 0) work[blockIdx.x] = tot;
+  if (threadIdx.x < 2) work[2 * blockIdx.x + threadIdx.x] = tot[threadIdx.x];
+}
+
+// inclusive scan over a 64-lane wave
+__device__ __forceinline__ uint32_t wave_inclusive(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(v, off, 64);
+    if (static_cast<int>(lane) >= off) v += u;
+  }
+  return v;
 }
 
 // Thread t scans groups g0 + 4t .. g0 + 4t + 3 (kLossyPerBlock / 1024 = 4 per
-// thread, in order); a block-wide exclusive scan of the per-thread counts
-// places them.
+// thread, in order); block-wide exclusive scans of the per-thread counts place
+// them.
 __global__ __launch_bounds__(1024) void k_lossy_write(const uint64_t* present, uint64_t groups, uint64_t nmask,
-                                                      uint64_t dmask, const uint32_t* work, uint32_t* list,
-                                                      uint32_t* count) {
+                                                      uint64_t dmask, uint32_t d, const uint32_t* work,
+                                                      uint32_t* list, uint32_t* count, uint32_t* rowoff,
+                                                      uint32_t* rows_total) {
   constexpr uint32_t kPer = kLossyPerBlock / 1024u;
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t base;
+  __shared__ uint32_t wsum[2][16];
+  __shared__ uint32_t base[2];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  // this block's offset: the counts of all earlier blocks
-  uint32_t before = 0;
-  for (uint32_t b = t; b < blockIdx.x; b += 1024u) before += work[b];
+  // this block's offsets: the counts of all earlier blocks
+  uint32_t before = 0, rbefore = 0;
+  for (uint32_t b = t; b < blockIdx.x; b += 1024u) {
+    before += work[2 * b];
+    rbefore += work[2 * b + 1];
+  }
   before = __reduce_add_sync(~0ull, before);
-  if (t == 0) base = 0;
+  rbefore = __reduce_add_sync(~0ull, rbefore);
+  if (t < 2) base[t] = 0;
   __syncthreads();
-  if (lane == 0 && before) atomicAdd(&base, before);
+  if (lane == 0) {
+    if (before) atomicAdd(&base[0], before);
+    if (rbefore) atomicAdd(&base[1], rbefore);
+  }
   const uint64_t g0 = uint64_t(blockIdx.x) * kLossyPerBlock + uint64_t(t) * kPer;
-  uint32_t bits = 0, c = 0;
+  uint32_t bits = 0, c = 0, r = 0, rk[kPer];
 #pragma unroll
   for (uint32_t k = 0; k < kPer; ++k) {
     const uint64_t g = g0 + k;
-    if (g < groups && lossy(present, g, nmask, dmask)) {
-      bits |= 1u << k;
-      ++c;
-    }
+    bool l = false;
+    rk[k] = g < groups ? lossy_rows(present[g], nmask, dmask, d, l) : 0u;
+    bits |= static_cast<uint32_t>(l) << k;
+    c += l;
+    r += rk[k];
   }
-  // inclusive scan of c over the wave, then over the waves
-  uint32_t inc = c;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t v = __shfl_up(inc, off, 64);
-    if (static_cast<int>(lane) >= off) inc += v;
+  const uint32_t inc = wave_inclusive(c, lane), rinc = wave_inclusive(r, lane);
+  if (lane == 63u) {
+    wsum[0][wv] = inc;
+    wsum[1][wv] = rinc;
   }
-  if (lane == 63u) wsum[wv] = inc;
   __syncthreads();
-  uint32_t wbefore = 0;
-  for (uint32_t w = 0; w < wv; ++w) wbefore += wsum[w];
-  uint32_t pos = base + wbefore + inc - c;
+  uint32_t wbefore = 0, wrbefore = 0;
+  for (uint32_t w = 0; w < wv; ++w) {
+    wbefore += wsum[0][w];
+    wrbefore += wsum[1][w];
+  }
+  uint32_t pos = base[0] + wbefore + inc - c, rpos = base[1] + wrbefore + rinc - r;
   for (uint32_t k = 0; k < kPer; ++k)
-    if ((bits >> k) & 1u) list[pos++] = static_cast<uint32_t>(g0 + k);
-  if (blockIdx.x == gridDim.x - 1u && t == 1023u) *count = pos;  // the last thread's end = the total
+    if ((bits >> k) & 1u) {
+      list[pos] = static_cast<uint32_t>(g0 + k);
+      if (rowoff) rowoff[pos] = rpos;
+      ++pos;
+      rpos += rk[k];
+    }
+  if (blockIdx.x == gridDim.x - 1u && t == 1023u) {  // the last thread's ends = the totals
+    *count = pos;
+    if (rows_total) *rows_total = rpos;
+  }
 }
 
-hipError_t launch_lossy_list(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t* list,
-                             uint32_t* count, uint32_t* work, hipStream_t s) {
+hipError_t launch_lossy_list(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t d,
+                             uint32_t* list, uint32_t* count, uint32_t* rowoff, uint32_t* rows, uint32_t* work,
+                             hipStream_t s) {
   const uint64_t blocks = (groups + kLossyPerBlock - 1) / kLossyPerBlock;
   if (blocks == 0 || blocks > 0xffffffffull) return hipErrorInvalidValue;
   launch(kKReconstruct, k_lossy_count, dim3(static_cast<uint32_t>(blocks)), dim3(1024), 0, s, present, groups, nmask,
-         dmask, work);
+         dmask, d, work);
   launch(kKReconstruct, k_lossy_write, dim3(static_cast<uint32_t>(blocks)), dim3(1024), 0, s, present, groups, nmask,
-         dmask, static_cast<const uint32_t*>(work), list, count);
+         dmask, d, static_cast<const uint32_t*>(work), list, count, rowoff, rows);
   return hipGetLastError();
 }
 

@@ -36,6 +36,9 @@ struct Batch {
   uint32_t n;               // k_apply_rows: d + p; k_apply_pd: groups in the launch
   const uint32_t* list;     // list form (launch_apply_list): entry j = g0 + gl reads group list[j]'s rows
   const uint32_t* count;    //   and writes output / status j; entries at or past *count do nothing
+  const uint32_t* rowoff;   // list form, nullable: entry j's output i is row rowoff[j] + i of out (row-compact,
+  uint32_t* rowid;          //   out + row*orstride), and rowid[rowoff[j] + i] = list[j]*n + its erased row
+                            //   (nullable; needs rowoff; n = d + p)
 };
 
 struct Prep {
@@ -66,10 +69,14 @@ hipError_t launch_apply_rows(int mode, const Batch& a, hipStream_t s);  // MODE 
 hipError_t launch_apply_list(int dmax, const Batch& a, hipStream_t s);
 // Lossy-group list: the groups of [0, groups) with an erased row to rebuild
 // (data rows only when data_only), ascending, into list[0 .. *count); `work`
-// holds ceil(groups / kLossyPerBlock) + 1 words of scratch.
+// holds 2 * ceil(groups / kLossyPerBlock) words of scratch.  rowoff (nullable):
+// rowoff[j] = the rows to rebuild in entries before j, counting only groups
+// with >= d present rows (the others rebuild nothing), and *rows (nullable)
+// their total: the row-compact output offsets of launch_apply_list.
 constexpr uint32_t kLossyPerBlock = 4096;
-hipError_t launch_lossy_list(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t* list,
-                             uint32_t* count, uint32_t* work, hipStream_t s);
+hipError_t launch_lossy_list(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t d,
+                             uint32_t* list, uint32_t* count, uint32_t* rowoff, uint32_t* rows, uint32_t* work,
+                             hipStream_t s);
 // Dense rows (group stride == S, no padding; k_apply_pd): MODE 1 / 2, d <= 16
 // (dmax 4..16), p <= 4, S >= kDenseMinS (a wave's 63 chunks span at most one
 // group boundary).  a.base = row 0 of group a.g0, 16-B aligned; a.items =

@@ -35,6 +35,11 @@ namespace {
 
 constexpr int kStreams = 3;
 constexpr size_t kStageBytes = size_t(64) << 20;  // per host-path staging buffer
+// RX ring stages in flight: with two, both stages' copies ran at once and the
+// next pair waited for the first stage's assembly -- the link idled ~0.15 ms
+// per 2.4-ms pair (profiles/r5/host_rx_trace); with four a copy stream always
+// has its next stage free.
+constexpr int kRxStages = 4;
 constexpr size_t kZeroCopyEncodeBytes = size_t(4) << 20;  // pinned encode batches up to this run zero-copy
 constexpr uint32_t kMaxItems = 0x7fffffffu;
 
@@ -1027,16 +1032,19 @@ int rx_assemble_dev(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const u
 
 // ugo_fec_lossy_groups on device views.
 int lossy_list_dev(ugo_fec* c, const uint64_t* present, size_t groups, unsigned flags, uint32_t* list,
-                   uint32_t* count, hipStream_t s) {
-  if (groups == 0) return hip_status(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
+                   uint32_t* count, hipStream_t s, uint32_t* rowoff = nullptr, uint32_t* rows = nullptr) {
+  if (groups == 0) {
+    if (rows && hipMemsetAsync(rows, 0, sizeof(uint32_t), s) != hipSuccess) return UGO_FEC_ERR_HIP;
+    return hip_status(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
+  }
   const uint64_t nmask = c->n >= 64 ? ~0ull : ((1ull << c->n) - 1);
   const uint64_t dmask = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? ((1ull << c->d) - 1) : ~0ull;
   const size_t blocks = (groups + ugo::kern::kLossyPerBlock - 1) / ugo::kern::kLossyPerBlock;
   void* work = nullptr;
-  int st = scratch_alloc(c, (blocks + 1) * sizeof(uint32_t), s, &work);
+  int st = scratch_alloc(c, 2 * blocks * sizeof(uint32_t), s, &work);
   if (st) return st;
-  st = hip_status(ugo::kern::launch_lossy_list(present, groups, nmask, dmask, list, count,
-                                               static_cast<uint32_t*>(work), s));
+  st = hip_status(ugo::kern::launch_lossy_list(present, groups, nmask, dmask, static_cast<uint32_t>(c->d), list,
+                                               count, rowoff, rows, static_cast<uint32_t*>(work), s));
   const int fr = scratch_free(c, work, s);
   return st ? st : fr;
 }
@@ -1045,8 +1053,11 @@ int lossy_list_dev(ugo_fec* c, const uint64_t* present, size_t groups, unsigned 
 int reconstruct_list_dev(ugo_fec* c, const uint8_t* shards, const uint64_t* present, const uint32_t* list,
                          const uint32_t* count, size_t max_entries, size_t S, const Layout& L, uint8_t* out,
                          size_t out_row_stride, size_t out_entry_stride, unsigned flags, int8_t* status,
-                         hipStream_t s) {
+                         hipStream_t s, const uint32_t* rowoff = nullptr, uint32_t* rowid = nullptr) {
   ugo::kern::Batch a = base_batch(c, const_cast<uint8_t*>(shards), S, L);
+  a.rowoff = rowoff;  // row-compact outputs (rx_recover_host)
+  a.rowid = rowid;
+  a.n = static_cast<uint32_t>(c->n);
   a.out = out;
   a.ogstride = out_entry_stride;
   a.orstride = out_row_stride;
@@ -1561,20 +1572,20 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
 // copy streams, each chunk assembled (rx_assemble_dev, one call per chunk into
 // one batch: first copy wins across the calls) on a third stream as soon as its
 // copy lands, so copies and kernels overlap; then the lossy-group list, the
-// data-only Reconstruct of those groups into a compact output, and the D2H of
-// the recovered rows only.
+// data-only Reconstruct of those groups into a row-compact output (the
+// `recovered` list of ugo/fec.go:203-207), and the D2H of those rows only.
 int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
                             const uint8_t* pad, uint64_t first_group, size_t groups, size_t S, uint64_t* present_out,
                             uint32_t* stats_out, uint8_t* out, size_t out_row_stride, size_t max_out,
-                            uint32_t* out_groups, int8_t* out_status, size_t* n_out) {
+                            uint32_t* out_index, size_t* n_out) {
   if (!c || !n_out) return UGO_FEC_ERR_INVALID_ARG;
   *n_out = 0;
   if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
   if (groups == 0) return UGO_FEC_OK;
-  if ((npk && (!wire || !lens)) || c->n > 16 || !c->d_table || groups >= 0xffffffffull || npk >= 0xffffffffull ||
+  if ((npk && (!wire || !lens)) || c->n > 16 || !c->d_table || groups * size_t(c->n) >= 0xffffffffull || npk >= 0xffffffffull ||
       slot_stride % 16 || slot_stride < 16 || S > 0xffffffffu || out_row_stride < S ||
-      (max_out && (!out || !out_groups)))
+      (max_out && (!out || !out_index)))
     return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
@@ -1585,15 +1596,16 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   const size_t n = size_t(c->n), pitch = round_up(S, 16), slots = size_t(std::min(c->d, c->p));
   // packets per chunk: at most a 64-MiB stage, and at least 4 chunks so copies and assembly overlap
   const size_t cpk = std::max<size_t>(1, std::min((npk + 3) / 4, kStageBytes / slot_stride));
-  const size_t lens_off = round_up(cpk * slot_stride, 256);
-  const size_t stage_bytes = lens_off + round_up(cpk * sizeof(uint16_t), 256);
-  const size_t mo = std::min(max_out, groups);
-  // one scratch block: batch | present | list | count, stats | status | outputs | pad | 2 ring stages
+  const size_t stage_bytes = round_up(cpk * slot_stride, 256);
+  // every recovered row fits: a recoverable group rebuilds at most min(d, p) data rows
+  const size_t max_rows = max_out ? groups * slots : 1;
+  // one scratch block: batch | present | list | row offsets | counts, stats | row ids | rows | pad | lens | ring stages
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off = round_up(off + bytes, 256); return o; };
   const size_t o_batch = take(n * groups * pitch), o_pres = take(groups * 8), o_list = take(groups * 4),
-               o_ctl = take(64), o_stat = take(groups), o_out = take(std::max<size_t>(mo, 1) * slots * pitch),
-               o_pad = take(pad ? slot_stride : 16), o_stage = take(2 * stage_bytes);
+               o_roff = take(groups * 4), o_ctl = take(64), o_rid = take(max_rows * 4), o_out = take(max_rows * pitch),
+               o_pad = take(pad ? slot_stride : 16), o_lens = take(std::max<size_t>(npk, 1) * 2),
+               o_stage = take(kRxStages * stage_bytes);
   uint8_t* base = nullptr;
   st = scratch_alloc(c, off, s0, reinterpret_cast<void**>(&base));
   if (st) return st;
@@ -1606,60 +1618,76 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   uint8_t* batch = base + o_batch;
   uint64_t* dpres = reinterpret_cast<uint64_t*>(base + o_pres);
   uint32_t* dlist = reinterpret_cast<uint32_t*>(base + o_list);
-  uint32_t* dcount = reinterpret_cast<uint32_t*>(base + o_ctl);
+  uint32_t* droff = reinterpret_cast<uint32_t*>(base + o_roff);
+  uint32_t* dcount = reinterpret_cast<uint32_t*>(base + o_ctl);  // [0] lossy groups, [1] recovered rows
   uint32_t* dstats = dcount + 4;
-  int8_t* dstat = reinterpret_cast<int8_t*>(base + o_stat);
+  uint32_t* drid = reinterpret_cast<uint32_t*>(base + o_rid);
   uint8_t* dout = base + o_out;
   uint8_t* dpad = pad ? base + o_pad : nullptr;
-  hipEvent_t ev[4] = {};  // full[0..1]: a stage's copy landed; free[0..1]: its assembly is done
+  uint16_t* dlens = reinterpret_cast<uint16_t*>(base + o_lens);
+  // ev[b]: stage b's copy landed; ev[kRxStages + b]: its assembly is done (the stage is free)
+  hipEvent_t ev[2 * kRxStages] = {};
   struct Events {
     hipEvent_t* e;
     ~Events() {
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 2 * kRxStages; ++i)
         if (e[i]) (void)hipEventDestroy(e[i]);
     }
   } evs{ev};
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2 * kRxStages; ++i)
     if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return UGO_FEC_ERR_HIP;
   if (hipMemsetAsync(dpres, 0, groups * 8, s0) != hipSuccess || hipMemsetAsync(dcount, 0, 64, s0) != hipSuccess ||
       (pad && hipMemcpyAsync(dpad, pad, slot_stride, hipMemcpyHostToDevice, s0) != hipSuccess))
     return UGO_FEC_ERR_HIP;
   // the copy streams start after the zeroing (their stages are this call's scratch)
-  if (hipEventRecord(ev[2], s0) != hipSuccess || hipEventRecord(ev[3], s0) != hipSuccess) return UGO_FEC_ERR_HIP;
-  for (size_t p0 = 0, k = 0; p0 < npk; p0 += cpk, ++k) {
-    const size_t m = std::min(cpk, npk - p0);
-    const int b = static_cast<int>(k & 1);
-    const hipStream_t cs = c->streams[1 + b];
-    uint8_t* sw = base + o_stage + b * stage_bytes;
-    uint16_t* sl = reinterpret_cast<uint16_t*>(sw + lens_off);
-    if (hipStreamWaitEvent(cs, ev[2 + b], 0) != hipSuccess ||
-        hipMemcpyAsync(sw, wire + p0 * slot_stride, m * slot_stride, hipMemcpyHostToDevice, cs) != hipSuccess ||
-        hipMemcpyAsync(sl, lens + p0, m * sizeof(uint16_t), hipMemcpyHostToDevice, cs) != hipSuccess ||
-        hipEventRecord(ev[b], cs) != hipSuccess || hipStreamWaitEvent(s0, ev[b], 0) != hipSuccess)
-      return UGO_FEC_ERR_HIP;
-    st = rx_assemble_dev(c, sw, slot_stride, sl, m, dpad, first_group, groups, batch, S, groups * pitch, pitch, dpres,
-                         dstats, s0);
+  for (int b = 0; b < kRxStages; ++b)
+    if (hipEventRecord(ev[kRxStages + b], s0) != hipSuccess) return UGO_FEC_ERR_HIP;
+  // all the lengths in one copy ahead of the first stage (a small copy between two ring copies on a
+  // stream cost a ~0.1-ms gap per chunk: profiles/r5/host_rx_trace)
+  if (npk && (hipStreamWaitEvent(c->streams[1], ev[kRxStages], 0) != hipSuccess ||
+              hipMemcpyAsync(dlens, lens, npk * sizeof(uint16_t), hipMemcpyHostToDevice, c->streams[1]) != hipSuccess))
+    return UGO_FEC_ERR_HIP;
+  // copies run up to kRxStages - 1 chunks ahead of the assembly in enqueue order too, so a host
+  // thread held up between two chunks does not leave the link idle
+  const size_t nchunks = (npk + cpk - 1) / cpk;
+  size_t next = 0;
+  for (size_t k = 0; k < nchunks; ++k) {
+    for (; next < nchunks && next < k + kRxStages; ++next) {
+      const int b = static_cast<int>(next % kRxStages);
+      const hipStream_t cs = c->streams[1 + (next & 1)];
+      const size_t p0 = next * cpk, m = std::min(cpk, npk - p0);
+      if (hipStreamWaitEvent(cs, ev[kRxStages + b], 0) != hipSuccess ||
+          hipMemcpyAsync(base + o_stage + b * stage_bytes, wire + p0 * slot_stride, m * slot_stride,
+                         hipMemcpyHostToDevice, cs) != hipSuccess ||
+          hipEventRecord(ev[b], cs) != hipSuccess)
+        return UGO_FEC_ERR_HIP;
+    }
+    const int b = static_cast<int>(k % kRxStages);
+    const size_t p0 = k * cpk, m = std::min(cpk, npk - p0);
+    if (hipStreamWaitEvent(s0, ev[b], 0) != hipSuccess) return UGO_FEC_ERR_HIP;
+    // (chunk 0's wait covers the lengths' copy, earlier on the same stream; later chunks follow it on s0)
+    st = rx_assemble_dev(c, base + o_stage + b * stage_bytes, slot_stride, dlens + p0, m, dpad, first_group, groups,
+                         batch, S, groups * pitch, pitch, dpres, dstats, s0);
     if (st) return st;
-    if (hipEventRecord(ev[2 + b], s0) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (hipEventRecord(ev[kRxStages + b], s0) != hipSuccess) return UGO_FEC_ERR_HIP;
   }
-  st = lossy_list_dev(c, dpres, groups, UGO_FEC_RECONSTRUCT_DATA_ONLY, dlist, dcount, s0);
+  // the lossy groups and, per entry, where its rows start in the row-compact output
+  st = lossy_list_dev(c, dpres, groups, UGO_FEC_RECONSTRUCT_DATA_ONLY, dlist, dcount, s0, droff, dcount + 1);
   if (st) return st;
-  if (mo) {
-    st = reconstruct_list_dev(c, batch, dpres, dlist, dcount, mo, S, Layout{groups * pitch, pitch}, dout, pitch,
-                              slots * pitch, UGO_FEC_RECONSTRUCT_DATA_ONLY, dstat, s0);
+  if (max_out) {
+    st = reconstruct_list_dev(c, batch, dpres, dlist, dcount, groups, S, Layout{groups * pitch, pitch}, dout, pitch,
+                              0, UGO_FEC_RECONSTRUCT_DATA_ONLY, nullptr, s0, droff, drid);
     if (st) return st;
   }
   uint32_t hcnt[8] = {};
   if (hipMemcpyAsync(hcnt, dcount, 32, hipMemcpyDeviceToHost, s0) != hipSuccess || hipStreamSynchronize(s0) != hipSuccess)
     return UGO_FEC_ERR_HIP;
-  const size_t total = hcnt[0], w = std::min<size_t>(total, mo);
+  const size_t total = hcnt[1], w = std::min<size_t>(total, max_out);
   *n_out = total;
   hipError_t e = hipSuccess;
-  if (w) {
-    e = hipMemcpyAsync(out_groups, dlist, w * 4, hipMemcpyDeviceToHost, s0);
-    if (e == hipSuccess && out_status) e = hipMemcpyAsync(out_status, dstat, w, hipMemcpyDeviceToHost, s0);
-    if (e == hipSuccess)
-      e = hipMemcpy2DAsync(out, out_row_stride, dout, pitch, S, w * slots, hipMemcpyDeviceToHost, s0);
+  if (w) {  // only the recovered rows cross PCIe: w rows of S bytes
+    e = hipMemcpyAsync(out_index, drid, w * 4, hipMemcpyDeviceToHost, s0);
+    if (e == hipSuccess) e = hipMemcpy2DAsync(out, out_row_stride, dout, pitch, S, w, hipMemcpyDeviceToHost, s0);
   }
   if (e == hipSuccess && present_out) e = hipMemcpyAsync(present_out, dpres, groups * 8, hipMemcpyDeviceToHost, s0);
   if (e == hipSuccess && stats_out) e = hipMemcpyAsync(stats_out, dstats, 20, hipMemcpyDeviceToHost, s0);

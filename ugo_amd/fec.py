@@ -144,7 +144,7 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_reconstruct_rows.argtypes = [vp, vp, vp, sz, sz, vp, sz, sz, u, vp, vp]
     lib.ugo_fec_lossy_groups.argtypes = [vp, vp, sz, u, vp, vp, vp]
     lib.ugo_fec_rx_recover_host.argtypes = [vp, vp, sz, vp, sz, vp, ctypes.c_uint64, sz, sz, vp, vp, vp, sz, sz, vp,
-                                            vp, ctypes.POINTER(sz)]
+                                            ctypes.POINTER(sz)]
     lib.ugo_fec_tx_assemble_host.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp]
     lib.ugo_fec_reconstruct_list.argtypes = [vp, vp, vp, sz, vp, vp, sz, sz, sz, sz, vp, sz, sz, u, vp, vp]
     lib.ugo_fec_device_address.argtypes = [vp, vp, ctypes.POINTER(vp)]
@@ -337,28 +337,25 @@ class Encoder:
                         max_out: Optional[int] = None, present_out: Optional[np.ndarray] = None):
         """ugo_fec_rx_recover_host: the RX path host memory to host memory.  wire =
         uint8 [npk, slot] (pinned for DMA rates), lens = uint16 [npk].  Returns
-        (n, groups_idx, status, out, stats): n lossy groups; for the first
-        min(n, max_out) of them their window index, status and their lost data
-        shards in out[j, i] (out: uint8 [max_out, min(d, p), row] with row >=
-        shard_size, allocated if None)."""
+        (n, index, out, stats): n recovered data shards, the first
+        min(n, max_out) of them row-compact in out[r, :shard_size] (out: uint8
+        [max_out, row] with row >= shard_size, allocated if None) in ugo's
+        `recovered` order, index[r] = window group * (d+p) + row."""
         npk, slot = wire.shape
         _require(wire.flags.c_contiguous and lens.flags.c_contiguous and lens.size == npk and lens.itemsize == 2)
-        slots = min(self.DataShards, self.ParityShards)
-        m = groups if max_out is None else max_out
+        m = groups * min(self.DataShards, self.ParityShards) if max_out is None else max_out
         if out is None:
-            out = np.zeros((max(m, 1), slots, (shard_size + 15) // 16 * 16), np.uint8)
-        _require(out.flags.c_contiguous and out.shape[0] >= m and out.shape[1] == slots and out.shape[2] >= shard_size)
-        gidx = np.zeros(max(m, 1), np.uint32)
-        status = np.zeros(max(m, 1), np.int8)
+            out = np.zeros((max(m, 1), (shard_size + 15) // 16 * 16), np.uint8)
+        _require(out.ndim == 2 and out.flags.c_contiguous and out.shape[0] >= m and out.shape[1] >= shard_size)
+        index = np.zeros(max(m, 1), np.uint32)
         stats = np.zeros(5, np.uint32)
         padb = None if pad is None else np.frombuffer(bytes(pad), np.uint8)
         n_out = ctypes.c_size_t(0)
         _raise(load_library().ugo_fec_rx_recover_host(
             self._h, wire.ctypes.data, slot, lens.ctypes.data, npk, None if padb is None else padb.ctypes.data,
             first_group, groups, shard_size, None if present_out is None else present_out.ctypes.data,
-            stats.ctypes.data, out.ctypes.data, out.shape[2], m, gidx.ctypes.data, status.ctypes.data,
-            ctypes.byref(n_out)))
-        return n_out.value, gidx, status, out, stats
+            stats.ctypes.data, out.ctypes.data, out.shape[1], m, index.ctypes.data, ctypes.byref(n_out)))
+        return n_out.value, index, out, stats
 
     def tx_assemble_host(self, pkts: np.ndarray, lens: np.ndarray, wire: np.ndarray, wire_lens: np.ndarray,
                          first_seq: int = 0, pad: Optional[bytes] = None, max_len: int = 1476,
