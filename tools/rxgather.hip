@@ -219,10 +219,18 @@ int main(int argc, char** argv) {
       {"k_rx_p2: P2 shape, one chunk per lane, scalar headers, keystream per lane + tally + gated claim/re-place", P2K, 0, 0, 0},
       {"round-4 second form: k_rx_place MODE 4 (ds_bpermute realignment, header load), 8192 blocks", PROD, 7, 0, 0},
       {"production kernel, 8192 blocks", PROD, 0, 0, 8192},
+      {"production, gated claim / re-place on 1024 blocks", PROD, 40, 0, 0},
+      {"production, claim words filled by a gated pass (not by begin), gated passes on 1024 blocks", PROD, 41, 0, 0},
       {"production (round 3): begin + place (MODE 0, 2048 blocks) + gated fill/claim/re-place", PROD_OLD, 0, 0, 2048},
       {"production with the place kernel's presence atomics removed (MODE 1, timing only)", PROD, 1, 0, 0},
       {"production with the place kernel's realignment removed (MODE 2, timing only)", PROD, 2, 0, 0},
   };
+  if (const char* only = getenv("RXG_ONLY")) {  // the production form plus the variants whose name holds `only`
+    std::vector<Var> keep = {vars[0]};
+    for (size_t k = 1; k < vars.size(); ++k)
+      if (vars[k].name.find(only) != std::string::npos) keep.push_back(vars[k]);
+    vars = keep;
+  }
   uint32_t* d_cnt;
   CK(hipMalloc(&d_cnt, kRxCntWords * 4));
   unsigned long long* d_seen;
@@ -311,7 +319,10 @@ int main(int argc, char** argv) {
     }
     if (v.kind == PROD) {
       const unsigned long long call = ++call_id;
-      CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, s));
+      if (v.order == 41)
+        CK(launch_rx_begin(a.present, prev, a.groups, dup, nullptr, 0, d_seen, call, s));
+      else
+        CK(launch_rx_begin(a.present, prev, a.groups, dup, win, a.groups * n, d_seen, call, s));
       a.seen = d_seen;
       a.call = call;
     } else {
@@ -320,6 +331,19 @@ int main(int argc, char** argv) {
     a.dup = dup;
     a.prev = prev;
     const uint32_t blocks = v.grid ? v.grid : rx_blocks(a);
+    if (v.kind == PROD && (v.order == 40 || v.order == 41)) {
+      k_rx_place_h<3, 3><<<blocks, 256, 0, s>>>(a);
+      if (v.order == 41) CK(launch_rx_fill(win, a.groups * n, dup, s));
+      RxArgs f = a;
+      f.win = win;
+      f.gate = dup;
+      f.dup = nullptr;
+      f.stats = nullptr;
+      f.fixup = 1;
+      k_rx_claim<<<1024, 256, 0, s>>>(f);
+      k_rx_place_h<3, 3><<<1024, 256, 0, s>>>(f);
+      return;
+    }
     if (v.kind == PROD && (v.order == 0 || v.order == 5)) {
       if (v.order == 5)
         k_rx_place<3, 0, 3><<<blocks, 256, 0, s>>>(a);
