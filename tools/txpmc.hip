@@ -133,6 +133,10 @@ int main(int argc, char** argv) {
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 3><<<grid, 256, cap>>>(a); }},
       {"XCD-contiguous blocks (ATTR 4)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 4><<<grid, 256, cap>>>(a); }},
+      {"resident grid: 512 blocks (2 per CU) striding, no residency LDS (ATTR 64)",
+       [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 64><<<512, 256, 16u * a.chunks>>>(a); }},
+      {"resident grid: 768 blocks (3 per CU) striding, no residency LDS (ATTR 64)",
+       [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 64><<<768, 256, 16u * a.chunks>>>(a); }},
       {"runs of 4 blocks per XCD (ATTR 16)",
        [&](const TxArgs& a) { k_tx_c<10, 3, kTxNT, true, true, 16><<<grid, 256, cap>>>(a); }},
       {"runs of 8 blocks per XCD (ATTR 32)",
@@ -177,6 +181,17 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(s1.data(), x.status, G, hipMemcpyDeviceToHost));
     CK(hipMemcpy(s2.data(), y.status, G, hipMemcpyDeviceToHost));
     printf("{\"check\":\"ATTR 1 + k_tx_lens == production (wire, wire_lens, status)\",\"same\":%s}\n",
+           (w1 == w2 && l1 == l2 && s1 == s2) ? "true" : "false");
+    // the resident striding grid (ATTR 64) against production
+    CK(hipMemset(y.wire, 0x5c, G * n * slot));
+    CK(hipMemset(y.wire_lens, 0x77, G * n * 2));
+    CK(hipMemset(y.status, 0x33, G));
+    k_tx_c<10, 3, kTxNT, true, true, 64><<<512, 256, 16u * y.chunks>>>(y);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(w2.data(), y.wire, w2.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(l2.data(), y.wire_lens, G * n * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(s2.data(), y.status, G, hipMemcpyDeviceToHost));
+    printf("{\"check\":\"resident 512-block grid (ATTR 64) == production (wire, wire_lens, status)\",\"same\":%s}\n",
            (w1 == w2 && l1 == l2 && s1 == s2) ? "true" : "false");
     CK(hipFree(dl));
   }

@@ -239,22 +239,35 @@ __device__ __forceinline__ uint32_t block_run() {  // hardware block b on XCD b 
   return (b / W) * W + (b & 7u) * RUN + (b >> 3) % RUN;
 }
 
-template <int D, int P, int NT = kTxNT, bool SL = kTxSL, bool PL = false, int ATTR = 0>
-__global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
-  const uint32_t bid = (ATTR & 16) ? block_run<4>() : (ATTR & 32) ? block_run<8>() : block_id<(ATTR & 4) ? 1 : 0>();
-  const uint32_t item = bid * 256u + threadIdx.x;
-  extern __shared__ u32x4 padl[];
-  if constexpr (PL) {
-    for (uint32_t i = threadIdx.x; i < a.chunks; i += 256u) padl[i] = *reinterpret_cast<const u32x4*>(a.pad + 16u * i);
-    __syncthreads();
-  }
-  if (item >= a.groups * a.chunks) return;
+template <int D, int P, int NT, bool SL, bool PL, int ATTR>
+__device__ __forceinline__ void tx_c_item(const TxArgs& a, uint32_t item, const u32x4* padl) {
   V4 x[D];
   const TxItem t = tx_data<D, NT, SL, PL, ATTR>(a, item, x, padl);
   if (!t.live || tx_no_window(a, t)) return;
   tx_cparity<D, P, NT, ATTR>(a, t, x, std::make_integer_sequence<int, P>{});
   if constexpr (!(ATTR & 1))
     if (t.o == 0 && a.status) a.status[t.g] = 0;
+}
+
+// ATTR bit 6 (A/B only): a resident grid (2 blocks per CU) striding over the
+// items instead of the full grid with its residency held by unused LDS.
+template <int D, int P, int NT = kTxNT, bool SL = kTxSL, bool PL = false, int ATTR = 0>
+__global__ __launch_bounds__(256) void k_tx_c(TxArgs a) {
+  const uint32_t bid = (ATTR & 16) ? block_run<4>() : (ATTR & 32) ? block_run<8>() : block_id<(ATTR & 4) ? 1 : 0>();
+  extern __shared__ u32x4 padl[];
+  if constexpr (PL) {
+    for (uint32_t i = threadIdx.x; i < a.chunks; i += 256u) padl[i] = *reinterpret_cast<const u32x4*>(a.pad + 16u * i);
+    __syncthreads();
+  }
+  const uint32_t total = a.groups * a.chunks;
+  if constexpr (ATTR & 64) {
+    for (uint32_t base = bid * 256u; base < total; base += gridDim.x * 256u)
+      if (base + threadIdx.x < total) tx_c_item<D, P, NT, SL, PL, ATTR>(a, base + threadIdx.x, padl);
+  } else {
+    const uint32_t item = bid * 256u + threadIdx.x;
+    if (item >= total) return;
+    tx_c_item<D, P, NT, SL, PL, ATTR>(a, item, padl);
+  }
 }
 
 // Any other geometry: coefficients from the encode descriptor (uniform, so
