@@ -739,7 +739,7 @@ def host_path_leg(args, dev_index, rank=0, world=1, reps=3):
                 if enc is not None:
                     enc.close()
         # the RX and TX paths from host memory to host memory, same binding
-        rxtx, ok_rxtx = host_rxtx_cases(args, dev_index, rank, world, reps)
+        rxtx, ok_rxtx = host_rxtx_cases(args, dev_index, rank, world, max(reps, 5))
         res.update(rxtx)
         all_ok = all_ok and ok_rxtx
     finally:
@@ -760,14 +760,14 @@ def pcie_ceiling(dev, world, nbytes=1 << 30, reps=3):
     """The per-GPU PCIe ceiling measured in this run, every rank at once (each
     rep starts at a barrier, max over ranks): a pinned host buffer copied to
     the device, back, and both directions at once on two streams (hipMemcpyAsync
-    DMA through torch).  GB/s are per GPU."""
+    DMA through torch).  GB/s are per GPU.  The host buffers are torch's own
+    pinned tensors: torch treats a tensor over other pinned memory as pageable
+    and synchronises after each copy, which serialised the two directions
+    (round 5's first lines read 57.6 GB/s "both at once")."""
     import torch
 
-    from ugo_amd import fec
-
-    raw = [fec.host_alloc(nbytes), fec.host_alloc(nbytes)]
+    h = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
     try:
-        h = [torch.from_numpy(x) for x in raw]
         dbuf = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
         s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
 
@@ -798,8 +798,7 @@ def pcie_ceiling(dev, world, nbytes=1 << 30, reps=3):
         del dbuf
         return out
     finally:
-        for x in raw:
-            fec.host_free(x)
+        del h
 
 
 def host_rxtx_cases(args, dev_index, rank, world, reps):
@@ -872,7 +871,8 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
 
         guarded(rx_setup)()
         guarded(rx_call)()
-        t_rx, t_rx_mine = timed_reps(guarded(rx_call), reps, world)
+        rx_reps = []
+        t_rx, t_rx_mine = timed_reps(guarded(rx_call), reps, world, rx_reps)
         ok = False
         if st["err"] is None:
             # reference: the device-resident path on the same ring
@@ -932,6 +932,7 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             "groups_per_rank": G, "packets_per_rank": npk, "loss": 0.05, "rc4": True, "recovered_shards_rank0": nrec,
             "rx_ms": round(t_rx * 1e3, 3), "wire_GBps": round(wire_bytes / t_rx / 1e9, 2),
             "pcie_GBps_per_gpu": round(pcie / t_rx / 1e9, 2), "rank0_alone_ms": round(t_rx_mine * 1e3, 3),
+            "rep_ms": [round(t * 1e3, 2) for t in rx_reps],
             "zero_copy_ring_ms": None if t_zc is None else round(t_zc * 1e3, 3),
             "zero_copy_note": "rx_assemble reading the pinned ring in place, then the public lossy list + "
                               "entry-form list reconstruct, D2H of every entry's p row slots",
@@ -961,7 +962,8 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
 
         guarded(tx_setup)()
         guarded(tx_call)()
-        t_tx, t_tx_mine = timed_reps(guarded(tx_call), reps, world)
+        tx_reps = []
+        t_tx, t_tx_mine = timed_reps(guarded(tx_call), reps, world, tx_reps)
         ok = False
         if st["err"] is None:
             dw = torch.empty((G * n, slot), dtype=torch.uint8, device=dev)
@@ -976,6 +978,7 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             "groups_per_rank": G, "packets_out_per_rank": G * n, "rc4": True, "tx_ms": round(t_tx * 1e3, 3),
             "wire_GBps": round(world * G * n * 1476 / t_tx / 1e9, 2),
             "pcie_GBps_per_gpu": round(G * (d + n) * slot / t_tx / 1e9, 2), "rank0_alone_ms": round(t_tx_mine * 1e3, 3),
+            "rep_ms": [round(t * 1e3, 2) for t in tx_reps],
             "verify_vs_device_path": ok,
             "path": "pinned data packets -> H2D -> tx_assemble -> D2H of the wire packets, >= 4 group chunks "
                     "round-robin over 3 streams"}
@@ -990,10 +993,11 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
     return res, ok_all and st["err"] is None
 
 
-def timed_reps(call, reps, world):
+def timed_reps(call, reps, world, all_out=None):
     """`reps` calls, each started by a barrier over the ranks and timed on each
     rank; returns (median over reps of the max over ranks, this rank's own
-    median): the job's time for one call when all ranks run it at once."""
+    median): the job's time for one call when all ranks run it at once.
+    all_out (a list): receives the max-over-ranks time of every rep."""
     ts = []
     for _ in range(reps):
         barrier(world)
@@ -1001,7 +1005,10 @@ def timed_reps(call, reps, world):
         call()
         ts.append(time.perf_counter() - t0)
     mine = sorted(ts)[len(ts) // 2]
-    return sorted(reduce_max(ts, world))[len(ts) // 2], mine
+    mx = reduce_max(ts, world)
+    if all_out is not None:
+        all_out.extend(mx)
+    return sorted(mx)[len(ts) // 2], mine
 
 
 def gather_objects(obj, world):

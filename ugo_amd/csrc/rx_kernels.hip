@@ -105,11 +105,11 @@ struct RxAccount {
 // L (<= S) are zero.  Always a whole 16-B chunk: a row's last chunk carries
 // zeros past S up to round_up(S, 16) (include/ugo_fec.h).  Writing only the
 // row's S bytes left every row's last 64-B line partially written, and that
-// cost 7 % of the RX kernel's time in order, 3 % shuffled (458.7 vs 494.9 us,
-// 499.0 vs 512.4; tools/rxgather.hip, profiles/r5/rxgather_tail_*) -- while
-// one unaligned 16-B store of the row's last 16 payload bytes, which leaves
-// the padding unwritten, gained nothing (487.1 / 531.4 us): the partial line,
-// not the store count, is the cost.
+// cost 6 % of the RX call's time in order, 3 % shuffled (466.9 vs 494.9 us,
+// 499.1 vs 512.4; tools/rxgather.hip, profiles/r5/rxgather/r5_rxtail4_*) --
+// while one unaligned 16-B store of the row's last 16 payload bytes, which
+// leaves the padding unwritten, gained nothing (498.2 / 529.3 us): the partial
+// line, not the store count, is the cost.
 template <int NTS>
 __device__ __forceinline__ void rx_put(uint8_t* row, uint32_t o, uint32_t L, const u32x4& A, uint32_t nx,
                                        uint32_t ny) {

@@ -71,8 +71,10 @@ constexpr bool kTxSL = true;
 // and was fetched again -- the 9 % of excess read bytes round 4 could not
 // place (2 x FETCH_SIZE 1.0896 x the algorithmic bytes; plain loads 1.0656,
 // and with XCD-contiguous blocks as well 1.0111).  Plain loads: 412.7 vs
-// 455.0 us (tools/txpmc.hip, profiles/r5/txpmc/); the XCD-contiguous deal,
-// despite its exact traffic, 451.9.
+// 455.0 us back to back, 413.0 vs 425.7 in interleaved cold rounds
+// (tools/txpmc.hip, profiles/r5/txpmc_a/, txpmc_b/); the XCD-contiguous deal,
+// despite its exact traffic, 451.9 / 452.0, and runs of 4 or 8 blocks per XCD
+// (reads 0.96 / 0.955 of production's) 427.6 / 429.9 (txpmc_c/).
 constexpr int kTxLoadNT = 0;
 
 struct TxItem {

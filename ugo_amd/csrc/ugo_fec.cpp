@@ -1717,11 +1717,25 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
   int st = ensure_streams(c);
   if (st) return st;
   const size_t per_group = d * slot_in + n * slot_out;
+  // Outputs staged through device memory and copied back by DMA, which runs
+  // concurrently with the next chunks' input copies: 30.7-30.9 ms for 65,536
+  // (10+3) groups (72.7 GB/s over PCIe in both directions together), against
+  // 37.0-37.5 ms with the kernel writing pinned outputs through their device
+  // mapping (A/B build -DUGO_TX_HOST_ZERO_COPY_OUT, tools/host_txrx_ab.py,
+  // profiles/r5/host_txrx_ab.jsonl).
+  uint8_t* zwire = wire;
+  uint16_t* zlens = wire_lens;
+  int8_t* zstatus = status;
+#ifdef UGO_TX_HOST_ZERO_COPY_OUT
+  const bool zc = device_view(zwire) && device_view(zlens) && device_view(zstatus);
+#else
+  const bool zc = false;
+#endif
   const size_t cg = std::max<size_t>(1, std::min((groups + 3) / 4, kStageBytes / per_group));  // >= 4 chunks
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off = round_up(off + bytes, 256); return o; };
-  const size_t o_in = take(cg * d * slot_in), o_lens = take(cg * d * 2), o_wire = take(cg * n * slot_out),
-               o_wl = take(cg * n * 2), o_st = take(cg), o_pad = take(pad ? need : 16);
+  const size_t o_in = take(cg * d * slot_in), o_lens = take(cg * d * 2), o_wire = take(zc ? 16 : cg * n * slot_out),
+               o_wl = take(zc ? 16 : cg * n * 2), o_st = take(zc ? 16 : cg), o_pad = take(pad ? need : 16);
   uint8_t* buf[kStreams] = {};
   struct Release {
     ugo_fec* c;
@@ -1761,13 +1775,14 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
     a.pkts = b + o_in;
     a.lens = reinterpret_cast<const uint16_t*>(b + o_lens);
     a.pad = pad ? b + o_pad : nullptr;
-    a.wire = b + o_wire;
-    a.wire_lens = reinterpret_cast<uint16_t*>(b + o_wl);
-    a.status = status ? reinterpret_cast<int8_t*>(b + o_st) : nullptr;
+    a.wire = zc ? zwire + g0 * n * slot_out : b + o_wire;
+    a.wire_lens = zc ? zlens + g0 * n : reinterpret_cast<uint16_t*>(b + o_wl);
+    a.status = !status ? nullptr : zc ? zstatus + g0 : reinterpret_cast<int8_t*>(b + o_st);
     a.first_seq = static_cast<uint32_t>((uint64_t(first_seq) + uint64_t(g0) * n) % paws);
     a.g0 = 0;
     a.groups = gn;
     if (ugo::kern::launch_tx_assemble(dmax, a, s) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (zc) continue;
     if (hipMemcpyAsync(wire + g0 * n * slot_out, b + o_wire, gn * n * slot_out, hipMemcpyDeviceToHost, s) !=
             hipSuccess ||
         hipMemcpyAsync(wire_lens + g0 * n, b + o_wl, gn * n * 2, hipMemcpyDeviceToHost, s) != hipSuccess ||
