@@ -2005,6 +2005,7 @@ __global__ __launch_bounds__(1024) void k_lossy_write(const uint64_t* present, u
     wrbefore += wsum[1][w];
   }
   uint32_t pos = base[0] + wbefore + inc - c, rpos = base[1] + wrbefore + rinc - r;
+#pragma unroll
   for (uint32_t k = 0; k < kPer; ++k)
     if ((bits >> k) & 1u) {
       list[pos] = static_cast<uint32_t>(g0 + k);
