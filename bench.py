@@ -756,49 +756,43 @@ def host_path_leg(args, dev_index, rank=0, world=1, reps=3):
     return res
 
 
-def pcie_ceiling(dev, world, nbytes=1 << 30, reps=3):
+def pcie_ceiling(dev, world, nbytes=1 << 30, reps=5):
     """The per-GPU PCIe ceiling measured in this run, every rank at once (each
-    rep starts at a barrier, max over ranks): a pinned host buffer copied to
-    the device, back, and both directions at once on two streams (hipMemcpyAsync
-    DMA through torch).  GB/s are per GPU.  The host buffers are torch's own
-    pinned tensors: torch treats a tensor over other pinned memory as pageable
-    and synchronises after each copy, which serialised the two directions
-    (round 5's first lines read 57.6 GB/s "both at once")."""
+    rep starts at a barrier, max over ranks): a 1-GiB pinned host buffer
+    (ugo_fec_host_alloc) copied to the device, back, and both directions at once
+    on two streams, with the copy calls the host paths use (hipMemcpyAsync,
+    libugoprobe's ugo_probe_pcie).  GB/s are per GPU; "bidirectional" counts
+    both directions' bytes.  (Round 5's first lines timed torch copies of
+    tensors over this memory, which torch takes for pageable and synchronises
+    after each copy: the two directions never overlapped, 57.6 GB/s.)"""
+    import ctypes
+
+    import numpy as np
     import torch
 
-    h = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    from ugo_amd import fec
+
+    raw = [fec.host_alloc(nbytes), fec.host_alloc(nbytes)]
     try:
         dbuf = [torch.empty(nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-        s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-
-        def h2d():
-            with torch.cuda.stream(s1):
-                dbuf[0].copy_(h[0], non_blocking=True)
-            s1.synchronize()
-
-        def d2h():
-            with torch.cuda.stream(s1):
-                h[0].copy_(dbuf[0], non_blocking=True)
-            s1.synchronize()
-
-        def both():
-            with torch.cuda.stream(s1):
-                dbuf[0].copy_(h[0], non_blocking=True)
-            with torch.cuda.stream(s2):
-                h[1].copy_(dbuf[1], non_blocking=True)
-            s1.synchronize()
-            s2.synchronize()
-
-        out = {}
-        for name, fn, mult in (("h2d", h2d, 1), ("d2h", d2h, 1), ("bidirectional", both, 2)):
-            fn()
-            t, _ = timed_reps(fn, reps, world)
-            out[name + "_GBps"] = round(mult * nbytes / t / 1e9, 2)
-        out["note"] = f"{nbytes >> 20} MiB pinned <-> device per copy, every rank at once, max over ranks, per GPU"
+        lib = probe_library()
+        ms = np.zeros(3, np.float32)
+        barrier(world)
+        rc = lib.ugo_probe_pcie(raw[0].ctypes.data, raw[1].ctypes.data, dbuf[0].data_ptr(), dbuf[1].data_ptr(),
+                                nbytes, reps, ms.ctypes.data)  # medians over reps
+        if rc != 0:
+            raise RuntimeError(f"ugo_probe_pcie: {rc}")
+        tmax = reduce_max([float(x) for x in ms], world)
+        out = {"h2d_GBps": round(nbytes / (tmax[0] * 1e-3) / 1e9, 2),
+               "d2h_GBps": round(nbytes / (tmax[1] * 1e-3) / 1e9, 2),
+               "bidirectional_GBps": round(2 * nbytes / (tmax[2] * 1e-3) / 1e9, 2),
+               "note": f"{nbytes >> 20} MiB pinned <-> device per copy (hipMemcpyAsync, one stream per direction), "
+                       "every rank at once, max over ranks, per GPU"}
         del dbuf
         return out
     finally:
-        del h
+        for x in raw:
+            fec.host_free(x)
 
 
 def host_rxtx_cases(args, dev_index, rank, world, reps):
@@ -980,8 +974,8 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             "pcie_GBps_per_gpu": round(G * (d + n) * slot / t_tx / 1e9, 2), "rank0_alone_ms": round(t_tx_mine * 1e3, 3),
             "rep_ms": [round(t * 1e3, 2) for t in tx_reps],
             "verify_vs_device_path": ok,
-            "path": "pinned data packets -> H2D -> tx_assemble -> D2H of the wire packets, >= 4 group chunks "
-                    "round-robin over 3 streams"}
+            "path": "pinned data packets -> H2D -> tx_assemble -> D2H of the wire packets, group chunks through "
+                    "4 device stages, one stream per role (H2D / kernel / D2H) joined by events"}
         tb.clear()
         if st["err"]:
             res["rxtx_error_rank0"] = st["err"]
@@ -1195,6 +1189,7 @@ def probe_library():
     lib.ugo_probe_reconstruct_twin.argtypes = [vp, vp, i, vp, sz, sz, sz, sz, sz, sz, i, vp, vp]
     lib.ugo_probe_recover_twin.argtypes = [vp, vp, vp, vp, vp, i, sz, sz, sz, sz, sz, sz, i, ctypes.c_uint32, i, vp,
                                            vp]
+    lib.ugo_probe_pcie.argtypes = [vp, vp, vp, vp, sz, i, vp]
     return lib
 
 
@@ -1720,15 +1715,19 @@ def run_rank(args):
     # 3. Secondary legs, after the main line's measurement (nothing in them
     #    feeds `value`): BASELINE configs[3] strong over the ranks, and at N = 1
     #    the PCIe-inclusive host path (configs[4] among it).
+    #    The host path runs before the 74-GB configs[3] batch is allocated: after
+    #    that allocation (freed, cache emptied) the host TX leg's H2D and D2H
+    #    copies stopped overlapping for the rest of the process (39 vs 31 ms,
+    #    profiles/r5/host_tx_leg_order.txt).
     batches = outs = shards = view = None
     torch.cuda.empty_cache()
-    strong = strong_leg(args, enc, rank, world, dev, stream) if args.c4_total_groups > 0 else None
     host = None
     if not args.no_host_path:
         try:  # every rank at once, NUMA-local (a secondary leg: failures are reported, never lose the line)
             host = host_path_leg(args, dev_index, rank, world)
         except Exception as ex:  # noqa: BLE001
             host = {"error": repr(ex)[:300]}
+    strong = strong_leg(args, enc, rank, world, dev, stream) if args.c4_total_groups > 0 else None
     per_call = rx_tx = None
     if world == 1 and not args.no_host_path:
         try:

@@ -25,16 +25,37 @@ def main():
     label = sys.argv[1] if len(sys.argv) > 1 else "?"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
     placement = None
-    if len(sys.argv) > 3 and sys.argv[3] == "bind":  # as bench.py's host_path: every thread on the GPU's node
+    if "bind" in sys.argv[3:]:  # as bench.py's host_path: every thread on the GPU's node
         from ugo_amd import numa
 
         placement = numa.bind_to_node(numa.gpu_numa_node(0))
-    d, p, S, G, slot = 10, 3, 1350, 65536, 1488
+    d, p, S, slot = 10, 3, 1350, 1488
+    G = int(os.environ.get("HAB_GROUPS", "65536"))
     n = d + p
     dev = torch.device("cuda:0")
     enc = fec.Encoder(d, p, device=0)
     gen = torch.Generator(device=dev).manual_seed(11)
     padb = fec.rc4_keystream(b"1234567890123456", slot)
+    if "rxfirst" in sys.argv[3:]:  # as bench.py: the host RX case first, on the same context
+        seq = torch.arange(G * n, device=dev, dtype=torch.int64)
+        seq = seq[torch.rand(G * n, device=dev, generator=gen) >= 0.05]
+        npk = seq.numel()
+        w = torch.randint(0, 256, (npk, slot), dtype=torch.uint8, device=dev, generator=gen)
+        hdr = torch.zeros((npk, 6), dtype=torch.uint8, device=dev)
+        for b in range(4):
+            hdr[:, b] = ((seq >> (8 * b)) & 0xFF).to(torch.uint8)
+        hdr[:, 4] = torch.where(seq % n < d, 0xF1, 0xF2).to(torch.uint8)
+        w[:, :6] = hdr ^ torch.frombuffer(bytearray(padb[:6]), dtype=torch.uint8).to(dev)
+        ring = fec.host_alloc(npk * slot).reshape(npk, slot)
+        rl = fec.host_alloc(npk * 2).view(np.uint16)
+        out = fec.host_alloc(G * p * 1360).reshape(G * p, 1360)
+        torch.from_numpy(ring).copy_(w)
+        rl[:] = 1476
+        del w
+        for _ in range(4):
+            enc.rx_recover_host(ring, rl, S, G, pad=padb, out=out, max_out=G)
+        for b in (ring, rl.view(np.uint8), out):
+            fec.host_free(b)
     pk = fec.host_alloc(G * d * slot).reshape(G * d, slot)
     ln = fec.host_alloc(G * d * 2).view(np.uint16)
     wire = fec.host_alloc(G * n * slot).reshape(G * n, slot)
@@ -50,7 +71,7 @@ def main():
     for b in (pk, ln.view(np.uint8), wire, wl.view(np.uint8)):
         fec.host_free(b)
     tx_ms = sorted(tx)[len(tx) // 2]
-    print(json.dumps({"label": label, "placement": placement, "tx_ms": round(tx_ms, 3),
+    print(json.dumps({"label": label, "groups": G, "placement": placement, "tx_ms": round(tx_ms, 3),
                       "tx_pcie_GBps": round(G * (d + n) * slot / tx_ms / 1e6, 2), "tx_all_ms": [round(t, 2) for t in tx],
                       "tx_digest": digest}))
 

@@ -23,6 +23,10 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
 #include <cstddef>
 #include <cstdint>
 
@@ -323,6 +327,39 @@ int ugo_probe_nt_copy(const uint8_t* const* srcs, uint8_t* const* dsts, int nbuf
         return hipGetLastError();
       },
       reps, s, ms_out);
+}
+
+// The PCIe ceiling with the copy calls the host paths use (hipMemcpyAsync of
+// pinned host <-> device, one stream per direction): ms_out[0] = one H2D of
+// `bytes`, [1] one D2H, [2] both at once on two streams (wall time from the
+// first enqueue to both done), medians over reps.  hipHostMalloc'd host
+// buffers; the streams are the probe's own non-blocking ones.
+int ugo_probe_pcie(uint8_t* host_a, uint8_t* host_b, uint8_t* dev_a, uint8_t* dev_b, size_t bytes, int reps,
+                   float* ms_out) {
+  if (!host_a || !host_b || !dev_a || !dev_b || !ms_out || reps <= 0 || bytes == 0) return 2;
+  hipStream_t s1 = nullptr, s2 = nullptr;
+  if (hipStreamCreateWithFlags(&s1, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&s2, hipStreamNonBlocking) != hipSuccess)
+    return 1;
+  int rc = 0;
+  for (int mode = 0; mode < 3 && !rc; ++mode) {
+    std::vector<double> t;
+    for (int r = 0; r <= reps && !rc; ++r) {  // rep 0 warms up
+      const auto t0 = std::chrono::steady_clock::now();
+      if (mode != 1 && hipMemcpyAsync(dev_a, host_a, bytes, hipMemcpyHostToDevice, s1) != hipSuccess) rc = 1;
+      if (mode != 0 && hipMemcpyAsync(host_b, dev_b, bytes, hipMemcpyDeviceToHost, mode == 2 ? s2 : s1) != hipSuccess)
+        rc = 1;
+      if (hipStreamSynchronize(s1) != hipSuccess || hipStreamSynchronize(s2) != hipSuccess) rc = 1;
+      if (r) t.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    if (!rc) {
+      std::sort(t.begin(), t.end());
+      ms_out[mode] = static_cast<float>(t[t.size() / 2]);
+    }
+  }
+  (void)hipStreamDestroy(s1);
+  (void)hipStreamDestroy(s2);
+  return rc;
 }
 
 }  // extern "C"

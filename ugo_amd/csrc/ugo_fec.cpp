@@ -1594,8 +1594,9 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   if (st) return st;
   const hipStream_t s0 = c->streams[0];  // assembly and recovery; copies on streams 1 and 2
   const size_t n = size_t(c->n), pitch = round_up(S, 16), slots = size_t(std::min(c->d, c->p));
-  // packets per chunk: at most a 64-MiB stage, and at least 4 chunks so copies and assembly overlap
-  const size_t cpk = std::max<size_t>(1, std::min((npk + 3) / 4, kStageBytes / slot_stride));
+  // packets per chunk: at most a 64-MiB stage, at least 4 chunks so copies and assembly overlap, and
+  // at most 32 chunks (the chunks grow with the ring past that: see kTxMaxChunks)
+  const size_t cpk = std::max<size_t>({size_t(1), (npk + 31) / 32, std::min((npk + 3) / 4, kStageBytes / slot_stride)});
   const size_t stage_bytes = round_up(cpk * slot_stride, 256);
   // every recovered row fits: a recoverable group rebuilds at most min(d, p) data rows
   const size_t max_rows = max_out ? groups * slots : 1;
@@ -1695,10 +1696,35 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   return hip_status(e);
 }
 
-// The TX path from host memory to host memory: groups in chunks, each chunk's
-// data packets H2D -> tx_assemble -> wire packets D2H on one of the context's
-// three streams, chunks round-robin, so the copies in both directions and the
-// kernels of different chunks overlap.
+// The TX path from host memory to host memory: groups in chunks through
+// kTxStages device stages, one stream per role -- the data packets' H2D on
+// streams[1], tx_assemble on streams[0], the wire packets' D2H on streams[2] --
+// joined by events, so each copy engine streams its direction without waiting
+// for the other; the lengths go in with one copy ahead of the first chunk and
+// the wire lengths and statuses come back with one copy after the last (a
+// small copy between two large ones costs the engine ~0.1 ms,
+// profiles/r5/host_rx_trace).  Round 5's first form (H2D -> kernel -> D2H per
+// chunk on three round-robin streams, a stream's next input behind its
+// previous output) took 30.6 ms for 65,536 (10+3) groups; the kernel writing
+// pinned outputs through their device mapping instead of the D2H copies took
+// 37.0-37.5 ms against 30.7-30.9 (tools/host_txrx_ab.py,
+// profiles/r5/host_txrx_ab.jsonl).
+#ifndef UGO_TX_STAGES
+#define UGO_TX_STAGES 4
+#endif
+constexpr int kTxStages = UGO_TX_STAGES;
+#ifndef UGO_TX_CHUNK_MIB
+#define UGO_TX_CHUNK_MIB 64
+#endif
+constexpr size_t kTxChunkBytes = size_t(UGO_TX_CHUNK_MIB) << 20;  // a stage's input + output bytes at most
+// At most kTxMaxChunks chunks per call: the chunks grow with the batch past
+// that.  Calls of more chunks ran 2-4x slower, with everything enqueued at once
+// (64-MiB chunks at 65,536 / 131,072 / 262,144 groups: 26.7 / 52-130 / 210 ms;
+// 32-MiB chunks at 65,536: 48-54 ms), and bounding the enqueue from the host
+// (waiting for chunk k - 16 or k - 8 before enqueueing chunk k) was slower
+// still (42 / 122 / 249 ms) -- profiles/r5/host_tx_chunk_ab*.jsonl.
+constexpr size_t kTxMaxChunks = 32;
+
 int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const uint16_t* lens, size_t groups,
                              uint32_t first_seq, const uint8_t* pad, size_t max_len, uint8_t* wire, size_t slot_out,
                              uint16_t* wire_lens, int8_t* status) {
@@ -1716,41 +1742,47 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
   TimerScope ts(c);
   int st = ensure_streams(c);
   if (st) return st;
+  const hipStream_t sk = c->streams[0], sin = c->streams[1], sout = c->streams[2];
   const size_t per_group = d * slot_in + n * slot_out;
-  // Outputs staged through device memory and copied back by DMA, which runs
-  // concurrently with the next chunks' input copies: 30.7-30.9 ms for 65,536
-  // (10+3) groups (72.7 GB/s over PCIe in both directions together), against
-  // 37.0-37.5 ms with the kernel writing pinned outputs through their device
-  // mapping (A/B build -DUGO_TX_HOST_ZERO_COPY_OUT, tools/host_txrx_ab.py,
-  // profiles/r5/host_txrx_ab.jsonl).
-  uint8_t* zwire = wire;
-  uint16_t* zlens = wire_lens;
-  int8_t* zstatus = status;
-#ifdef UGO_TX_HOST_ZERO_COPY_OUT
-  const bool zc = device_view(zwire) && device_view(zlens) && device_view(zstatus);
-#else
-  const bool zc = false;
-#endif
-  const size_t cg = std::max<size_t>(1, std::min((groups + 3) / 4, kStageBytes / per_group));  // >= 4 chunks
+  // groups per chunk: a stage of at most kTxChunkBytes, at least 8 chunks so the two directions
+  // overlap, at most kTxMaxChunks
+  const size_t cg = std::max<size_t>({size_t(1), (groups + kTxMaxChunks - 1) / kTxMaxChunks,
+                                      std::min((groups + 7) / 8, kTxChunkBytes / per_group)});
+  // scratch: lengths [groups][d] | wire lengths [groups][n] | statuses [groups] | keystream | stages
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off = round_up(off + bytes, 256); return o; };
-  const size_t o_in = take(cg * d * slot_in), o_lens = take(cg * d * 2), o_wire = take(zc ? 16 : cg * n * slot_out),
-               o_wl = take(zc ? 16 : cg * n * 2), o_st = take(zc ? 16 : cg), o_pad = take(pad ? need : 16);
-  uint8_t* buf[kStreams] = {};
-  struct Release {
+  const size_t o_lens = take(groups * d * 2), o_wl = take(groups * n * 2), o_st = take(groups),
+               o_pad = take(pad ? need : 16), o_stages = off;
+  const size_t o_in = 0, o_wire = round_up(cg * d * slot_in, 256), stage_bytes = o_wire + round_up(cg * n * slot_out, 256);
+  uint8_t* base = nullptr;
+  st = scratch_alloc(c, o_stages + size_t(kTxStages) * stage_bytes, sk, reinterpret_cast<void**>(&base));
+  if (st) return st;
+  constexpr int kEv = 3 * kTxStages + 1;  // in[b] | kernel[b] | out[b] (stage free) | ready
+  hipEvent_t ev[kEv] = {};
+  struct Release {  // the copy streams finish before the scratch goes back (also on an early return)
     ugo_fec* c;
-    uint8_t** b;
+    uint8_t* p;
+    hipEvent_t* e;
     ~Release() {
-      for (int i = 0; i < kStreams; ++i)
-        if (b[i]) (void)scratch_free(c, b[i], c->streams[i]);
+      (void)hipStreamSynchronize(c->streams[1]);
+      (void)hipStreamSynchronize(c->streams[2]);
+      (void)scratch_free(c, p, c->streams[0]);
+      for (int i = 0; i < kEv; ++i)
+        if (e[i]) (void)hipEventDestroy(e[i]);
     }
-  } release{c, buf};
-  for (int i = 0; i < kStreams; ++i) {
-    st = scratch_alloc(c, off, c->streams[i], reinterpret_cast<void**>(&buf[i]));
-    if (st) return st;
-    if (pad && hipMemcpyAsync(buf[i] + o_pad, pad, need, hipMemcpyHostToDevice, c->streams[i]) != hipSuccess)
-      return UGO_FEC_ERR_HIP;
-  }
+  } release{c, base, ev};
+  for (int i = 0; i < kEv; ++i)
+    if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) return UGO_FEC_ERR_HIP;
+  uint16_t* dlens = reinterpret_cast<uint16_t*>(base + o_lens);
+  uint16_t* dwl = reinterpret_cast<uint16_t*>(base + o_wl);
+  int8_t* dst = reinterpret_cast<int8_t*>(base + o_st);
+  uint8_t* dpad = pad ? base + o_pad : nullptr;
+  if ((pad && hipMemcpyAsync(dpad, pad, need, hipMemcpyHostToDevice, sk) != hipSuccess) ||
+      hipEventRecord(ev[3 * kTxStages], sk) != hipSuccess ||  // the scratch is this call's from here on
+      hipStreamWaitEvent(sin, ev[3 * kTxStages], 0) != hipSuccess ||
+      hipStreamWaitEvent(sout, ev[3 * kTxStages], 0) != hipSuccess ||
+      hipMemcpyAsync(dlens, lens, groups * d * 2, hipMemcpyHostToDevice, sin) != hipSuccess)
+    return UGO_FEC_ERR_HIP;
   ugo::kern::TxArgs a{};
   a.desc = c->d_encdesc;
   a.slot_in = slot_in;
@@ -1762,33 +1794,40 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
   a.p = static_cast<uint32_t>(c->p);
   a.dpad = c->dpad;
   a.epad = c->epad;
+  a.pad = dpad;
   const int dmax = ugo::kern::has_const_encode(c->d, c->p) ? 0 : ugo::kern::apply_dmax(c->d);
   size_t k = 0;
   for (size_t g0 = 0; g0 < groups; g0 += cg, ++k) {
     const size_t gn = std::min(cg, groups - g0);
-    const int si = static_cast<int>(k % kStreams);
-    const hipStream_t s = c->streams[si];
-    uint8_t* b = buf[si];
-    if (hipMemcpyAsync(b + o_in, pkts + g0 * d * slot_in, gn * d * slot_in, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(b + o_lens, lens + g0 * d, gn * d * 2, hipMemcpyHostToDevice, s) != hipSuccess)
+    const int b = static_cast<int>(k % kTxStages);
+    uint8_t* sb = base + o_stages + b * stage_bytes;
+    // input: the stage's previous output (chunk k - kTxStages) must have left; chunk 0's event also
+    // covers the lengths, copied before it on the same stream
+    if ((k >= size_t(kTxStages) && hipStreamWaitEvent(sin, ev[2 * kTxStages + b], 0) != hipSuccess) ||
+        hipMemcpyAsync(sb + o_in, pkts + g0 * d * slot_in, gn * d * slot_in, hipMemcpyHostToDevice, sin) !=
+            hipSuccess ||
+        hipEventRecord(ev[b], sin) != hipSuccess || hipStreamWaitEvent(sk, ev[b], 0) != hipSuccess)
       return UGO_FEC_ERR_HIP;
-    a.pkts = b + o_in;
-    a.lens = reinterpret_cast<const uint16_t*>(b + o_lens);
-    a.pad = pad ? b + o_pad : nullptr;
-    a.wire = zc ? zwire + g0 * n * slot_out : b + o_wire;
-    a.wire_lens = zc ? zlens + g0 * n : reinterpret_cast<uint16_t*>(b + o_wl);
-    a.status = !status ? nullptr : zc ? zstatus + g0 : reinterpret_cast<int8_t*>(b + o_st);
+    a.pkts = sb + o_in;
+    a.lens = dlens + g0 * d;
+    a.wire = sb + o_wire;
+    a.wire_lens = dwl + g0 * n;
+    a.status = status ? dst + g0 : nullptr;
     a.first_seq = static_cast<uint32_t>((uint64_t(first_seq) + uint64_t(g0) * n) % paws);
     a.g0 = 0;
     a.groups = gn;
-    if (ugo::kern::launch_tx_assemble(dmax, a, s) != hipSuccess) return UGO_FEC_ERR_HIP;
-    if (zc) continue;
-    if (hipMemcpyAsync(wire + g0 * n * slot_out, b + o_wire, gn * n * slot_out, hipMemcpyDeviceToHost, s) !=
+    if (ugo::kern::launch_tx_assemble(dmax, a, sk) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (hipEventRecord(ev[kTxStages + b], sk) != hipSuccess ||
+        hipStreamWaitEvent(sout, ev[kTxStages + b], 0) != hipSuccess ||
+        hipMemcpyAsync(wire + g0 * n * slot_out, sb + o_wire, gn * n * slot_out, hipMemcpyDeviceToHost, sout) !=
             hipSuccess ||
-        hipMemcpyAsync(wire_lens + g0 * n, b + o_wl, gn * n * 2, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        (status && hipMemcpyAsync(status + g0, b + o_st, gn, hipMemcpyDeviceToHost, s) != hipSuccess))
+        hipEventRecord(ev[2 * kTxStages + b], sout) != hipSuccess)
       return UGO_FEC_ERR_HIP;
   }
+  // the wire lengths and statuses of every chunk: one copy each, behind the last chunk's kernel
+  if (hipMemcpyAsync(wire_lens, dwl, groups * n * 2, hipMemcpyDeviceToHost, sout) != hipSuccess ||
+      (status && hipMemcpyAsync(status, dst, groups, hipMemcpyDeviceToHost, sout) != hipSuccess))
+    return UGO_FEC_ERR_HIP;
   for (int i = 0; i < kStreams; ++i)
     if (hipStreamSynchronize(c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
   return UGO_FEC_OK;
