@@ -762,9 +762,9 @@ def pcie_ceiling(dev, world, nbytes=1 << 30, reps=5):
     (ugo_fec_host_alloc) copied to the device, back, and both directions at once
     on two streams, with the copy calls the host paths use (hipMemcpyAsync,
     libugoprobe's ugo_probe_pcie).  GB/s are per GPU; "bidirectional" counts
-    both directions' bytes.  (Round 5's first lines timed torch copies of
-    tensors over this memory, which torch takes for pageable and synchronises
-    after each copy: the two directions never overlapped, 57.6 GB/s.)"""
+    both directions' bytes.  (Round 5's first lines timed torch tensor copies,
+    whose two directions never overlapped -- over this memory or with torch's
+    own pinned tensors: 57.1-57.6 GB/s "both at once".)"""
     import ctypes
 
     import numpy as np
