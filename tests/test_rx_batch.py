@@ -404,6 +404,68 @@ def test_rx_recover_host_vs_oracle(gpu, encrypt, first_group, max_out, pinned):
 
 
 @pytest.mark.gpu
+def test_rx_recover_host_many_chunks_matches_device_path(gpu):
+    """A ring past rx_recover_host's chunk cap (32 chunks per call; the chunks
+    grow with the ring): 120,000 (10+3) groups, 5 % loss, shuffled, RC4 --
+    ~1.48M packets, 2.2 GB pinned -- against the device-resident path
+    (rx_assemble + lossy_groups + reconstruct_list, each checked against the
+    oracle above): the recovered shards in `recovered` order, their places,
+    the presence masks."""
+    d, p, S, G, slot = 10, 3, 1470, 120000, 1488
+    n, pitch = d + p, 1472
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    seq = torch.arange(G * n, device="cuda", dtype=torch.int64)
+    seq = seq[torch.rand(G * n, device="cuda", generator=gen) >= 0.05]
+    seq = seq[torch.randperm(seq.numel(), device="cuda", generator=gen)]
+    npk = seq.numel()
+    assert npk > 32 * ((64 << 20) // slot)  # past the cap
+    pad = fec.rc4_keystream(KEY, slot)
+    dpad = torch.frombuffer(bytearray(pad), dtype=torch.uint8).cuda()
+    w = torch.randint(0, 256, (npk, slot), dtype=torch.uint8, device="cuda", generator=gen)
+    hdr = torch.zeros((npk, 6), dtype=torch.uint8, device="cuda")
+    for b in range(4):
+        hdr[:, b] = ((seq >> (8 * b)) & 0xFF).to(torch.uint8)
+    hdr[:, 4] = torch.where(seq % n < d, 0xF1, 0xF2).to(torch.uint8)
+    w[:, :6] = hdr ^ dpad[:6]
+    lens = torch.full((npk,), 1476, dtype=torch.int16, device="cuda")
+    codec = fec.New(d, p)
+    bat = torch.empty((n, G, pitch), dtype=torch.uint8, device="cuda")
+    pr = torch.zeros(G, dtype=torch.int64, device="cuda")
+    codec.rx_assemble(w, lens, bat, pr, shard_size=S, pad=dpad)
+    lst, cnt = codec.lossy_groups(pr, data_only=True)
+    lo = torch.empty((G, p, pitch), dtype=torch.uint8, device="cuda")
+    codec.reconstruct_list(bat, pr, lst, cnt, lo, shard_size=S, data_only=True)
+    k = int(cnt.item())
+    pm = pr[lst[:k].long()]
+    lost = ((pm[:, None] >> torch.arange(d, device="cuda")) & 1) == 0
+    have = ((pm[:, None] >> torch.arange(n, device="cuda")) & 1).sum(1)
+    lost &= (have >= d)[:, None]
+    jj, rr = torch.nonzero(lost, as_tuple=True)
+    want_index = (lst[:k].long()[jj] * n + rr).cpu().numpy()
+    want_rows = lo[:k][torch.arange(p, device="cuda")[None, :] < lost.sum(1)[:, None]]
+    del bat, lo
+    bufs = []
+    try:
+        ring = fec.host_alloc(npk * slot).reshape(npk, slot)
+        bufs.append(ring)
+        hl = fec.host_alloc(npk * 2).view(np.uint16)
+        bufs.append(hl.view(np.uint8))
+        torch.from_numpy(ring).copy_(w)
+        hl[:] = 1476
+        del w
+        pres = np.zeros(G, np.uint64)
+        nrec, index, out, stats = codec.rx_recover_host(ring, hl, S, G, pad=pad, present_out=pres)
+        assert np.array_equal(pres.view(np.int64), pr.cpu().numpy())
+        assert stats.tolist() == [npk, 0, 0, 0, 0]
+        assert nrec == len(want_index)
+        assert np.array_equal(index[:nrec].astype(np.int64), want_index)
+        assert torch.equal(torch.from_numpy(out[:nrec, :S]).cuda(), want_rows[:, :S])
+    finally:
+        for a in bufs:
+            fec.host_free(a)
+
+
+@pytest.mark.gpu
 def test_rx_assemble_rejects_pageable_host_memory(gpu):
     """A ring the GPU cannot reach is refused up front, not faulted on."""
     codec = fec.New(10, 3)

@@ -154,6 +154,56 @@ def test_tx_assemble_host_vs_sender_loop(gpu, d, p, max_len, G, key, pinned):
 
 
 @pytest.mark.gpu
+def test_tx_assemble_host_many_chunks_matches_device_path(gpu):
+    """A batch past tx_assemble_host's chunk cap (32 chunks per call; the
+    chunks grow with the batch): 3,400 (32,8) groups of up to 9,006-B packets
+    in pinned memory, against the device-resident tx_assemble (itself checked
+    against the sender loop above) -- every wire packet within its length,
+    the wire lengths and the statuses, header-only and bad groups included."""
+    d, p, max_len, G = 32, 8, 9006, 3400
+    n, slot = d + p, (max_len + 15) // 16 * 16
+    enc = fec.New(d, p)
+    gen = torch.Generator(device="cuda").manual_seed(77)
+    dp = torch.randint(0, 256, (G * d, slot), dtype=torch.uint8, device="cuda", generator=gen)
+    ln = torch.randint(6, max_len + 1, (G * d,), dtype=torch.int32, device="cuda", generator=gen)
+    ln[7 * d:8 * d] = 6         # a header-only group: no parity
+    ln[11 * d + 3] = 5          # a bad group
+    ln = ln.to(torch.int16)
+    pad = fec.rc4_keystream(KEY, slot)
+    dw = torch.empty((G * n, slot), dtype=torch.uint8, device="cuda")
+    dwl = torch.empty(G * n, dtype=torch.int16, device="cuda")
+    dst = torch.empty(G, dtype=torch.int8, device="cuda")
+    enc.tx_assemble(dp, ln, dw, dwl, pad=torch.frombuffer(bytearray(pad), dtype=torch.uint8).cuda(),
+                    max_len=max_len, status=dst)
+    bufs = []
+
+    def pinned(nbytes):
+        a = fec.host_alloc(nbytes)
+        bufs.append(a)
+        return a
+
+    try:
+        hp = pinned(G * d * slot).reshape(G * d, slot)
+        hl = pinned(G * d * 2).view(np.uint16)
+        hw = pinned(G * n * slot).reshape(G * n, slot)
+        hwl = pinned(G * n * 2).view(np.uint16)
+        hst = pinned(G).view(np.int8)
+        torch.from_numpy(hp).copy_(dp)
+        hl[:] = ln.cpu().numpy().view(np.uint16)
+        hst[:] = -1
+        enc.tx_assemble_host(hp, hl, hw, hwl, pad=pad, max_len=max_len, status=hst)
+        want_l = dwl.cpu().numpy().view(np.uint16)
+        assert np.array_equal(hwl, want_l)
+        assert np.array_equal(hst, dst.cpu().numpy())
+        got = torch.from_numpy(hw).cuda()
+        keep = torch.arange(slot, device="cuda")[None, :] < dwl.to(torch.int32).view(-1, 1)
+        assert torch.equal(got[keep], dw[keep])
+    finally:
+        for a in bufs:
+            fec.host_free(a)
+
+
+@pytest.mark.gpu
 def test_tx_assemble_bad_length_group_and_arguments(gpu):
     d, p, n = 10, 3, 13
     enc = fec.New(d, p)

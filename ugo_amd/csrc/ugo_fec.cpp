@@ -1610,11 +1610,15 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   uint8_t* base = nullptr;
   st = scratch_alloc(c, off, s0, reinterpret_cast<void**>(&base));
   if (st) return st;
-  struct Release {
+  struct Release {  // the copy streams finish before the scratch goes back (also on an early return)
     ugo_fec* c;
     uint8_t* p;
     hipStream_t s;
-    ~Release() { (void)scratch_free(c, p, s); }
+    ~Release() {
+      (void)hipStreamSynchronize(c->streams[1]);
+      (void)hipStreamSynchronize(c->streams[2]);
+      (void)scratch_free(c, p, s);
+    }
   } release{c, base, s0};
   uint8_t* batch = base + o_batch;
   uint64_t* dpres = reinterpret_cast<uint64_t*>(base + o_pres);
