@@ -186,7 +186,10 @@ static Ring make_ring(uint64_t G, uint32_t n, uint32_t d, uint32_t slot, const s
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 15;
   const bool shuffle = !(argc > 2 && std::string(argv[2]) == "inorder");
-  const uint32_t d = 10, n = 13, S = 1470, slot = 1488;
+  const uint32_t d = 10, n = 13, S = 1470;
+  // RXG_SLOT: the ring's slot stride (default 1488 = round_up(1476, 16); 1536 puts every packet on
+  // 128-B lines of its own).  The PATTERN / copy lines assume 1488.
+  const uint32_t slot = getenv("RXG_SLOT") ? static_cast<uint32_t>(atoi(getenv("RXG_SLOT"))) : 1488u;
   // RXG_PITCH: the batch's row pitch (default 1472 = round_up(S, 16); 1536 puts every row piece on its own
   // 128-B lines)
   const uint32_t pitch = getenv("RXG_PITCH") ? static_cast<uint32_t>(atoi(getenv("RXG_PITCH"))) : 1472u;
@@ -568,9 +571,9 @@ int main(int argc, char** argv) {
     std::sort(v.t.begin(), v.t.end());
     const double med = v.t[v.t.size() / 2];
     printf("{\"variant\":\"%s\",\"ring\":\"%s\",\"pitch\":%u,\"packets\":%llu,\"median_us\":%.2f,\"min_us\":%.2f,"
-           "\"GBps\":%.1f,\"frac\":%.4f}\n",
+           "\"GBps\":%.1f,\"frac\":%.4f,\"slot\":%u}\n",
            v.name.c_str(), shuffle ? "shuffled" : "inorder", pitch, (unsigned long long)npk, med, v.t[0],
-           bytes / med / 1e3, bytes / med / 1e3 / 8000.0);
+           bytes / med / 1e3, bytes / med / 1e3 / 8000.0, slot);
   }
   return 0;
 }
