@@ -226,6 +226,7 @@ int main(int argc, char** argv) {
       {"round-4 second form: k_rx_place MODE 4 (ds_bpermute realignment, header load), 8192 blocks", PROD, 7, 0, 0},
       {"production kernel, 8192 blocks", PROD, 0, 0, 8192},
       {"production, gated claim / re-place on 1024 blocks", PROD, 40, 0, 0},
+      {"production with the byte masks on every chunk (round-5 first form, TAILB 0)", PROD, 42, 0, 0},
       {"production, claim words filled by a gated pass (not by begin), gated passes on 1024 blocks", PROD, 41, 0, 0},
       {"production (round 3): begin + place (MODE 0, 2048 blocks) + gated fill/claim/re-place", PROD_OLD, 0, 0, 2048},
       {"production with the place kernel's presence atomics removed (MODE 1, timing only)", PROD, 1, 0, 0},
@@ -337,6 +338,18 @@ int main(int argc, char** argv) {
     a.dup = dup;
     a.prev = prev;
     const uint32_t blocks = v.grid ? v.grid : rx_blocks(a);
+    if (v.kind == PROD && v.order == 42) {
+      k_rx_place_h<3, 3, 0, 0><<<blocks, 256, 0, s>>>(a);
+      RxArgs f = a;
+      f.win = win;
+      f.gate = dup;
+      f.dup = nullptr;
+      f.stats = nullptr;
+      f.fixup = 1;
+      CK(launch_rx_claim(f, s));
+      k_rx_place_h<3, 3, 0, 0><<<1024, 256, 0, s>>>(f);
+      return;
+    }
     if (v.kind == PROD && (v.order == 40 || v.order == 41)) {
       k_rx_place_h<3, 3><<<blocks, 256, 0, s>>>(a);
       if (v.order == 41) CK(launch_rx_fill(win, a.groups * n, dup, s));

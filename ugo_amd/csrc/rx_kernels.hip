@@ -110,7 +110,13 @@ struct RxAccount {
 // while one unaligned 16-B store of the row's last 16 payload bytes, which
 // leaves the padding unwritten, gained nothing (498.2 / 529.3 us): the partial
 // line, not the store count, is the cost.
-template <int NTS>
+// TAILB (round 5): the byte masks only for a chunk that reaches past L, behind
+// a branch -- a packet has one such chunk, in one of its passes, so a wave
+// skips the masks in the passes where none of its lanes holds one: VALU
+// instructions 128.5 -> 94.0 per packet, time unchanged (454.9 vs 454.7 us in
+// order, 468.4 vs 468.3 shuffled; profiles/r5/rxpmc/, rxgather/r5_tailb.jsonl):
+// the kernel is not VALU-bound.  TAILB 0: masks on every chunk (A/B).
+template <int NTS, int TAILB = 1>
 __device__ __forceinline__ void rx_put(uint8_t* row, uint32_t o, uint32_t L, const u32x4& A, uint32_t nx,
                                        uint32_t ny) {
   uint32_t w[4];
@@ -118,11 +124,13 @@ __device__ __forceinline__ void rx_put(uint8_t* row, uint32_t o, uint32_t L, con
   w[1] = __builtin_amdgcn_alignbyte(A.w, A.z, 2);
   w[2] = __builtin_amdgcn_alignbyte(nx, A.w, 2);
   w[3] = __builtin_amdgcn_alignbyte(ny, nx, 2);
+  if (!TAILB || o + 16u > L) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
-    const uint32_t b0 = o + 4u * j;
-    const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
-    w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+    for (int j = 0; j < 4; ++j) {  // zero bytes past the payload
+      const uint32_t b0 = o + 4u * j;
+      const uint32_t keep = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
+      w[j] &= keep >= 4u ? 0xffffffffu : ((1u << (8u * keep)) - 1u);
+    }
   }
   const u32x4 v = {w[0], w[1], w[2], w[3]};
   if constexpr (NTS)
@@ -213,7 +221,7 @@ __global__ __launch_bounds__(256) void k_rx_scatter(RxArgs a) {
 // RUNS (A/B): 0 = grid-stride over packet pairs (wave w: pairs w, w + nwaves,
 // ...); 1 = each wave takes one contiguous run of packet pairs, so the line a
 // packet's slot shares with the next packet's is read by the same wave.
-template <int NP, int NT = 3, int RUNS = 0>
+template <int NP, int NT = 3, int RUNS = 0, int TAILB = 1>
 __global__ __launch_bounds__(256) void k_rx_place_h(RxArgs a) {
   if (rx_gated_off(a)) return;
   __shared__ uint32_t bstats[5];
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(256) void k_rx_place_h(RxArgs a) {
         }
       }
       if (!ok || o >= a.S) continue;
-      rx_put<(NT & 2)>(dst, o, L, Aq, nx, ny);
+      rx_put<(NT & 2), TAILB>(dst, o, L, Aq, nx, ny);
     }
     if (hl == 0) acct.issue(a, bstats, why, grp - a.first_group, row);
   }
