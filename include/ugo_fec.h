@@ -365,9 +365,11 @@ int ugo_fec_rx_recover_host(ugo_fec* ctx, const uint8_t* wire, size_t slot_strid
                             size_t out_row_stride, size_t max_out, uint32_t* out_index, size_t* n_out);
 
 /* ugo_fec_tx_assemble with every buffer in host memory (pinned for full-rate
- * DMA): the groups go through the device in chunks, each chunk's data packets
- * H2D, assembled, its wire packets, lengths and statuses D2H, chunks
- * pipelined over three streams.  Same arguments and results; synchronous. */
+ * DMA): the groups go through the device in chunks -- each chunk's data
+ * packets H2D, assembled, its wire packets D2H, the three on streams of their
+ * own through four device stages, so both copy directions run at once; the
+ * lengths go in and the wire lengths and statuses come back with one copy
+ * each.  Same arguments and results; synchronous. */
 int ugo_fec_tx_assemble_host(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, const uint16_t* lens,
                              size_t groups, uint32_t first_seq, const uint8_t* pad, size_t max_len,
                              uint8_t* wire, size_t slot_out, uint16_t* wire_lens, int8_t* status);
