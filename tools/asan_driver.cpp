@@ -9,6 +9,7 @@
 // the sent payloads), so any memory error, UB or wrong byte stops it.
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -286,6 +287,106 @@ void tx_rx_batch() {
   ugo_fec_destroy(ctx);
 }
 
+// round 5: the lossy-group list + list reconstruct on a device batch, and
+// the host-memory RX / TX paths (pinned and pageable buffers, max_out below
+// the count, the TX chunk cap): results against tx_assemble / the data they
+// were built from
+void host_rx_tx_paths(bool pinned) {
+  const int d = 10, p = 3, n = 13;
+  const size_t G = 200, max_len = 1476, slot = 1488, S = max_len - 6, pitch = 1472;
+  ugo_fec* ctx = nullptr;
+  EXPECT(ugo_fec_create(0, d, p, &ctx) == UGO_FEC_OK);
+  if (!ctx) return;
+  std::vector<void*> owned;
+  auto buf = [&](size_t bytes) {
+    void* v = nullptr;
+    if (pinned) {
+      EXPECT(ugo_fec_host_alloc(bytes, &v) == UGO_FEC_OK);
+    } else {
+      v = std::calloc(bytes, 1);
+    }
+    owned.push_back(v);
+    return static_cast<uint8_t*>(v);
+  };
+  uint8_t* pkts = buf(G * d * slot);
+  auto* lens = reinterpret_cast<uint16_t*>(buf(G * d * 2));
+  uint8_t* wire = buf(G * n * slot);
+  auto* wlens = reinterpret_cast<uint16_t*>(buf(G * n * 2));
+  auto* status = reinterpret_cast<int8_t*>(buf(G));
+  uint8_t pad[1488];
+  EXPECT(ugo_fec_rc4_keystream(reinterpret_cast<const uint8_t*>("1234567890123456"), 16, pad, slot) == UGO_FEC_OK);
+  for (size_t i = 0; i < G * d * slot; ++i) pkts[i] = rb();
+  for (size_t i = 0; i < G * d; ++i) lens[i] = static_cast<uint16_t>(i % 37 == 5 ? 700 : max_len);
+  EXPECT(ugo_fec_tx_assemble_host(ctx, pkts, slot, lens, G, 0, pad, max_len, wire, slot, wlens, status) ==
+         UGO_FEC_OK);
+  for (size_t g = 0; g < G; ++g) EXPECT(status[g] == 0);
+  // the ring: every group loses data packet g % d, group 7 loses 4 packets (below d shards)
+  std::vector<size_t> keep;
+  for (size_t g = 0; g < G; ++g)
+    for (int r = 0; r < n; ++r)
+      if (r != static_cast<int>(g % d) && !(g == 7 && r < 4)) keep.push_back(g * n + r);
+  uint8_t* ring = buf(keep.size() * slot);
+  auto* rlens = reinterpret_cast<uint16_t*>(buf(keep.size() * 2));
+  for (size_t i = 0; i < keep.size(); ++i) {
+    std::memcpy(ring + i * slot, wire + keep[i] * slot, slot);
+    rlens[i] = wlens[keep[i]];
+  }
+  for (size_t max_out : {size_t(3 * G), size_t(17), size_t(0)}) {
+    uint8_t* out = buf(3 * G * pitch);
+    auto* index = reinterpret_cast<uint32_t*>(buf(3 * G * 4));
+    auto* present = reinterpret_cast<uint64_t*>(buf(G * 8));
+    uint32_t stats[5] = {};
+    size_t nrec = 0;
+    EXPECT(ugo_fec_rx_recover_host(ctx, ring, slot, rlens, keep.size(), pad, 0, G, S, present, stats, out, pitch,
+                                   max_out, index, &nrec) == UGO_FEC_OK);
+    EXPECT(nrec == G - 1);  // group 7 recovers nothing
+    EXPECT(stats[0] == keep.size());
+    const size_t m = std::min(nrec, max_out);
+    for (size_t r = 0, g = 0; r < m; ++r, ++g) {
+      if (g == 7) ++g;
+      const size_t k = g % d;
+      EXPECT(index[r] == g * n + k);
+      const size_t L = lens[g * d + k];  // the lost packet's length: its bytes past L recover as zeros
+      EXPECT(std::memcmp(out + r * pitch, pkts + (g * d + k) * slot + 6, L - 6) == 0);
+    }
+  }
+  // the device-path pair on a device copy of the assembled batch
+  uint8_t *dshards = nullptr, *dout = nullptr;
+  uint64_t* dpres = nullptr;
+  uint32_t *dlist = nullptr, *dcount = nullptr, *dstats = nullptr;
+  uint8_t* dring = nullptr;
+  uint16_t* drlens = nullptr;
+  EXPECT(hipMalloc(&dshards, n * G * pitch) == hipSuccess && hipMalloc(&dout, G * p * pitch) == hipSuccess &&
+         hipMalloc(&dpres, G * 8) == hipSuccess && hipMalloc(&dlist, G * 4) == hipSuccess &&
+         hipMalloc(&dcount, 4) == hipSuccess && hipMalloc(&dstats, 20) == hipSuccess &&
+         hipMalloc(&dring, keep.size() * slot) == hipSuccess && hipMalloc(&drlens, keep.size() * 2) == hipSuccess);
+  EXPECT(hipMemcpy(dring, ring, keep.size() * slot, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(drlens, rlens, keep.size() * 2, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemset(dpres, 0, G * 8) == hipSuccess);
+  uint8_t* dpad = nullptr;
+  EXPECT(hipMalloc(&dpad, slot) == hipSuccess && hipMemcpy(dpad, pad, slot, hipMemcpyHostToDevice) == hipSuccess);
+  EXPECT(ugo_fec_rx_assemble(ctx, dring, slot, drlens, keep.size(), dpad, 0, G, dshards, S, G * pitch, pitch, dpres,
+                             dstats, nullptr) == UGO_FEC_OK);
+  EXPECT(ugo_fec_lossy_groups(ctx, dpres, G, UGO_FEC_RECONSTRUCT_DATA_ONLY, dlist, dcount, nullptr) == UGO_FEC_OK);
+  EXPECT(ugo_fec_reconstruct_list(ctx, dshards, dpres, G, dlist, dcount, G, S, G * pitch, pitch, dout, pitch, p * pitch,
+                                  UGO_FEC_RECONSTRUCT_DATA_ONLY, nullptr, nullptr) == UGO_FEC_OK);
+  EXPECT(hipDeviceSynchronize() == hipSuccess);
+  uint32_t cnt = 0;
+  EXPECT(hipMemcpy(&cnt, dcount, 4, hipMemcpyDeviceToHost) == hipSuccess);
+  EXPECT(cnt == G);  // every group has a lost data row (group 7 listed, with no output)
+  for (void* q : {static_cast<void*>(dshards), static_cast<void*>(dout), static_cast<void*>(dpres),
+                  static_cast<void*>(dlist), static_cast<void*>(dcount), static_cast<void*>(dstats),
+                  static_cast<void*>(dring), static_cast<void*>(drlens), static_cast<void*>(dpad)})
+    (void)hipFree(q);
+  for (void* v : owned) {
+    if (pinned)
+      ugo_fec_host_free(v);
+    else
+      std::free(v);
+  }
+  ugo_fec_destroy(ctx);
+}
+
 // the per-call service's failure paths (round 4): a forced stall past the
 // watchdog timeout (the block leaves within the grace period: ERR_HIP, later
 // calls on the launch path), a restart, and a block that never leaves within
@@ -396,6 +497,8 @@ int main() {
   fec_object(16, UGO_FECCONN_BATCH_OVERLAP);
   fec_object(4, 0, true);
   tx_rx_batch();
+  host_rx_tx_paths(true);
+  host_rx_tx_paths(false);
   fec_object_alloc_failure();
   service_watchdog();
   std::printf("{\"asan_driver\": \"%s\", \"failures\": %d}\n", failures ? "FAIL" : "ok", failures);
