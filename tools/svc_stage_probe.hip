@@ -6,7 +6,7 @@
 // reading them from HBM.  Measured: the block's own read time (wall_clock64
 // around its loads, one 512-thread block as k_service), and the host's write +
 // fence time; many repetitions, medians.  Not product code.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/svc_stage_probe tools/svc_stage_probe.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Xarch_host -mavx2 -o tools/svc_stage_probe tools/svc_stage_probe.hip
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
 
