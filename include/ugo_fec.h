@@ -55,7 +55,8 @@ extern "C" {
  *    destination order (index + gather) -- same results. */
 /* 8: rx_assemble writes each placed row in whole 16-B chunks: its bytes
  *    [shard_size, round_up(shard_size, 16)) become zero; ugo_fec_lossy_groups,
- *    ugo_fec_reconstruct_list, ugo_fec_rx_recover_host, ugo_fec_tx_assemble_host. */
+ *    ugo_fec_reconstruct_list, ugo_fec_recover_data, ugo_fec_rx_recover_host,
+ *    ugo_fec_tx_assemble_host. */
 #define UGO_FEC_ABI_VERSION 8
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
@@ -197,6 +198,23 @@ int ugo_fec_reconstruct_list(ugo_fec* ctx, const uint8_t* shards, const uint64_t
                              size_t shard_size, size_t row_stride, size_t group_stride, uint8_t* out,
                              size_t out_row_stride, size_t out_entry_stride, unsigned flags, int8_t* status,
                              void* stream);
+
+/* `input`'s recovery over a device batch in one call (ugo/fec.go:190-207):
+ * every group with a lost data shard and at least d shards is reconstructed
+ * (DATA_ONLY) and its lost data shards are written row-compact, in the order
+ * `input` appends them to `recovered` (groups ascending, each group's lost
+ * rows ascending): shard r at out + r*out_row_stride, shard_size bytes, for
+ * r < min(*count, max_rows) (rows past max_rows are not written), with
+ * index[r] = group * (d+p) + row.  *count (device u32) = the number of
+ * recovered shards, written on `stream` (no host synchronisation; the
+ * lossy-group list and the row offsets are stream-ordered scratch).  A group
+ * below d shards recovers nothing, as in `input`.  Code d+p <= 16, 16-B
+ * aligned rows and strides (as the fast path); out 16-B aligned,
+ * out_row_stride a multiple of 16 >= round_up(shard_size, 16); max_rows = 0
+ * counts only (out and index may be NULL). */
+int ugo_fec_recover_data(ugo_fec* ctx, const uint8_t* shards, const uint64_t* present, size_t groups,
+                         size_t shard_size, size_t row_stride, size_t group_stride, uint8_t* out,
+                         size_t out_row_stride, size_t max_rows, uint32_t* index, uint32_t* count, void* stream);
 
 /* The device address of p (device memory of ctx's GPU: p itself; pinned host
  * memory: its device mapping, which on ROCm is the host address), or

@@ -641,6 +641,53 @@ def test_lossy_list_and_reconstruct_list_vs_oracle(gpu, d, p, S, pitch, shard_ma
         assert np.array_equal(got, exp_ip)
 
 
+@pytest.mark.parametrize("d,p,S,pitch,shard_major,G", [
+    (10, 3, 1470, 1472, True, 900),   # ugo's RX batch: k_apply_p list form
+    (10, 3, 1350, 1360, False, 333),  # group-major
+    (6, 2, 77, 80, True, 257),        # rows < 64 chunks: k_apply list form
+    (10, 5, 1200, 1200, False, 64),   # p > 4: k_apply list form
+])
+def test_recover_data_vs_oracle(gpu, d, p, S, pitch, shard_major, G):
+    """ugo_fec_recover_data: `input`'s recovered list of a device batch (groups
+    ascending, lost data rows ascending, groups below d shards nothing) against
+    the oracle's ReconstructData, row-compact with each shard's place; the
+    count on the device; max_rows below the count writes only that many rows."""
+    n = d + p
+    host = _rand(G, n, pitch, 93 + d + p + G).numpy()
+    rs_ref.c_encode(d, p, host, S=S)
+    rng = np.random.default_rng(G + d + 7)
+    masks = np.zeros(G, np.uint64)
+    for g in range(G):
+        e = int(rng.choice([0, 0, 1, 2, p, p + 1]))
+        m = (1 << n) - 1
+        for r in rng.choice(n, size=min(e, n), replace=False):
+            m &= ~(1 << int(r))
+        masks[g] = m
+    inp = _erase(host, masks, n)
+    enc = fec.New(d, p)
+    dm = _masks_to_dev(masks)
+    t_in = _dev(np.ascontiguousarray(inp.transpose(1, 0, 2)) if shard_major else inp)
+    want = inp.copy()
+    rc, want_st = rs_ref.c_reconstruct(d, p, want, masks, S=S, data_only=True)
+    rec = [(g, r) for g in range(G) if want_st[g] == 0 for r in range(d) if not (int(masks[g]) >> r) & 1]
+    opitch = (S + 15) // 16 * 16
+    for max_rows in (max(len(rec), 1), max(len(rec) // 2, 1)):
+        out = torch.full((max_rows, opitch), 0xA5, dtype=torch.uint8, device="cuda")
+        idx = torch.full((max_rows,), -1, dtype=torch.int32, device="cuda")
+        before = t_in.clone()
+        cnt = enc.recover_data(t_in, dm, out, idx, shard_size=S, shard_major=shard_major)
+        torch.cuda.synchronize()
+        assert torch.equal(t_in, before), "recover_data wrote its input"
+        assert int(cnt.item()) == len(rec)
+        m = min(max_rows, len(rec))
+        o, ix = out.cpu().numpy(), idx.cpu().numpy()
+        assert ix[:m].tolist() == [g * n + r for g, r in rec[:m]]
+        assert (ix[m:] == -1).all()
+        for k, (g, r) in enumerate(rec[:m]):
+            assert np.array_equal(o[k, :S], want[g, r, :S]), (k, g, r)
+        assert (o[m:] == 0xA5).all()
+
+
 @pytest.mark.parametrize("d,p,S,G,table_max", [
     (10, 3, 1350, 777, "16"),   # the bench's dense rows: 8 groups per pseudo-group, k_apply_p on 2-B aligned groups
     (10, 3, 1350, 777, "0"),    # same with per-group descriptors (k_prepare)

@@ -88,10 +88,6 @@ __device__ __forceinline__ uint8_t* out_row(const Batch& a, uint8_t* gp, uint64_
 
 // List forms: entry g's output i at out + oent + i*orstride, where oent is
 // the entry's offset -- row-compact (a.rowoff) or entry-strided.
-__device__ __forceinline__ uint64_t list_out_off(const Batch& a, uint64_t g) {
-  return a.rowoff ? static_cast<uint64_t>(a.rowoff[g]) * a.orstride : g * a.ogstride;
-}
-
 __device__ __forceinline__ uint8_t* out_row_at(const Batch& a, uint8_t* gp, uint64_t oent, uint32_t off, uint32_t r,
                                               uint32_t i) {
   return a.out ? a.out + oent + static_cast<uint64_t>(i) * a.orstride + off : gp + static_cast<uint64_t>(r) * a.rstride;
@@ -219,7 +215,8 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
   const uint32_t e = a.data_only ? ((hdr >> 8) & 0xffu) : (hdr & 0xffu);
   if (st != 0 || e == 0) return;
   uint8_t* gp = a.base + grow * a.gstride + static_cast<uint64_t>(c) * 16u;
-  const uint64_t oent = LIST ? list_out_off(a, g) : g * a.ogstride;
+  const uint32_t rbase = LIST && a.rowoff ? a.rowoff[g] : 0u;  // row-compact: the entry's first output row
+  const uint64_t oent = !LIST ? g * a.ogstride : a.rowoff ? uint64_t(rbase) * a.orstride : g * a.ogstride;
   constexpr int NW = (DMAX + 3) / 4;
   uint32_t rows[NW];
 #pragma unroll
@@ -242,8 +239,9 @@ __global__ __launch_bounds__(256) void k_apply(Batch a) {
 #pragma unroll
     for (int w = 0; w < NW; ++w) cw[w] = ld32(coef + i * a.dpad + 4 * w);
     const V4 y = horner_var<DMAX>(x, cw);
+    if (LIST && a.rowoff && rbase + i >= a.max_rows) break;  // rows past the caller's room
     store16<NT>(out_row_at(a, gp, oent, c * 16u, orow[i], i), y, nb);
-    if (LIST && a.rowid && c == 0) a.rowid[a.rowoff[g] + i] = static_cast<uint32_t>(grow * a.n + orow[i]);
+    if (LIST && a.rowid && c == 0) a.rowid[rbase + i] = static_cast<uint32_t>(grow * a.n + orow[i]);
   }
 }
 
@@ -525,7 +523,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   uint32_t mB;  // all-ones in group-B lanes; opaque to the optimizer (see p_tables)
   asm("v_mov_b32 %0, %1" : "=v"(mB) : "v"(inB ? ~0u : 0u));
   uint8_t* gp = a.base + grow * a.gstride + static_cast<uint64_t>(c) * 16u;
-  const uint64_t oent = LIST ? list_out_off(a, g) : g * a.ogstride;
+  const uint32_t rbase = LIST && a.rowoff ? a.rowoff[g] : 0u;  // row-compact: the entry's first output row
+  const uint64_t oent = !LIST ? g * a.ogstride : a.rowoff ? uint64_t(rbase) * a.orstride : g * a.ogstride;
   const uint32_t nb = a.S - c * 16u;
   V4 x[DMAX];
   if constexpr (GLR > 0) {  // survivors 0..GLR-1 by LDS-DMA nt, the rest to registers (host: d == 10)
@@ -564,8 +563,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (int i = 0; i < EMAX; ++i) {
     if (i >= static_cast<int>(e)) continue;
     const uint32_t r = (orows >> (8 * i)) & 0xffu;
+    if (LIST && a.rowoff && rbase + i >= a.max_rows) continue;  // rows past the caller's room
     store16<NT>(out_row_at(a, gp, oent, c * 16u, r, i), acc[i], nb);
-    if (LIST && a.rowid && c == 0) a.rowid[a.rowoff[g] + i] = static_cast<uint32_t>(grow * a.n + r);
+    if (LIST && a.rowid && c == 0) a.rowid[rbase + i] = static_cast<uint32_t>(grow * a.n + r);
   }
   if (wst) a.status[g] = 0;
 }

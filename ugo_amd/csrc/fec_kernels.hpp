@@ -39,6 +39,7 @@ struct Batch {
   const uint32_t* rowoff;   // list form, nullable: entry j's output i is row rowoff[j] + i of out (row-compact,
   uint32_t* rowid;          //   out + row*orstride), and rowid[rowoff[j] + i] = list[j]*n + its erased row
                             //   (nullable; needs rowoff; n = d + p)
+  uint32_t max_rows;        //   with rowoff: rows at or past max_rows are not written
 };
 
 struct Prep {

@@ -1053,10 +1053,12 @@ int lossy_list_dev(ugo_fec* c, const uint64_t* present, size_t groups, unsigned 
 int reconstruct_list_dev(ugo_fec* c, const uint8_t* shards, const uint64_t* present, const uint32_t* list,
                          const uint32_t* count, size_t max_entries, size_t S, const Layout& L, uint8_t* out,
                          size_t out_row_stride, size_t out_entry_stride, unsigned flags, int8_t* status,
-                         hipStream_t s, const uint32_t* rowoff = nullptr, uint32_t* rowid = nullptr) {
+                         hipStream_t s, const uint32_t* rowoff = nullptr, uint32_t* rowid = nullptr,
+                         uint32_t max_rows = 0xffffffffu) {
   ugo::kern::Batch a = base_batch(c, const_cast<uint8_t*>(shards), S, L);
-  a.rowoff = rowoff;  // row-compact outputs (rx_recover_host)
+  a.rowoff = rowoff;  // row-compact outputs (rx_recover_host, ugo_fec_recover_data)
   a.rowid = rowid;
+  a.max_rows = max_rows;
   a.n = static_cast<uint32_t>(c->n);
   a.out = out;
   a.ogstride = out_entry_stride;
@@ -1314,6 +1316,48 @@ int ugo_fec_reconstruct_list(ugo_fec* c, const uint8_t* shards, const uint64_t* 
   TimerScope ts(c);
   return reconstruct_list_dev(c, shards, present, list, count, max_entries, S, L, out, out_row_stride,
                               out_entry_stride, flags, status, static_cast<hipStream_t>(stream));
+}
+
+int ugo_fec_recover_data(ugo_fec* c, const uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
+                         size_t row_stride, size_t group_stride, uint8_t* out, size_t out_row_stride, size_t max_rows,
+                         uint32_t* index, uint32_t* count, void* stream) {
+  const Layout L{row_stride, group_stride};
+  int st = check_batch(c, shards, groups, S, L);
+  if (st) return st;
+  if (!present || !count || c->n > 16 || !c->d_table || groups * size_t(c->n) >= 0xffffffffull ||
+      max_rows > 0xffffffffull || (max_rows && (!out || !index)))
+    return UGO_FEC_ERR_INVALID_ARG;
+  if (!fast_layout(c, shards, L, S)) return UGO_FEC_ERR_INVALID_ARG;
+  if (max_rows) {
+    if (reinterpret_cast<uintptr_t>(out) % 16 || out_row_stride % 16 || out_row_stride < round_up(S, 16))
+      return UGO_FEC_ERR_INVALID_ARG;
+    const size_t in_ext = extent(S, row_stride, size_t(c->n), group_stride, groups);
+    const size_t out_ext = (max_rows - 1) * out_row_stride + S;
+    const uintptr_t i0 = reinterpret_cast<uintptr_t>(shards), o0 = reinterpret_cast<uintptr_t>(out);
+    if (o0 < i0 + in_ext && i0 < o0 + out_ext) return UGO_FEC_ERR_INVALID_ARG;
+  }
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (!device_view(shards) || !device_view(present) || !device_view(out) || !device_view(index) ||
+      !device_view(count))
+    return UGO_FEC_ERR_INVALID_ARG;
+  TimerScope ts(c);
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  if (groups == 0) return hip_status(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
+  // scratch: the lossy-group list | each entry's first output row | the entry count
+  void* scratch = nullptr;
+  st = scratch_alloc(c, groups * 8 + 16, s, &scratch);
+  if (st) return st;
+  uint32_t* list = static_cast<uint32_t*>(scratch);
+  uint32_t* rowoff = list + groups;
+  uint32_t* entries = rowoff + groups;
+  st = lossy_list_dev(c, present, groups, UGO_FEC_RECONSTRUCT_DATA_ONLY, list, entries, s, rowoff, count);
+  if (!st && max_rows)
+    st = reconstruct_list_dev(c, shards, present, list, entries, groups, S, L, out, out_row_stride, 0,
+                              UGO_FEC_RECONSTRUCT_DATA_ONLY, nullptr, s, rowoff, index,
+                              static_cast<uint32_t>(max_rows));
+  const int fr = scratch_free(c, scratch, s);
+  return st ? st : fr;
 }
 
 int ugo_fec_reconstruct(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,

@@ -147,6 +147,7 @@ def load_library(path: str = LIB_PATH):
                                             ctypes.POINTER(sz)]
     lib.ugo_fec_tx_assemble_host.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp]
     lib.ugo_fec_reconstruct_list.argtypes = [vp, vp, vp, sz, vp, vp, sz, sz, sz, sz, vp, sz, sz, u, vp, vp]
+    lib.ugo_fec_recover_data.argtypes = [vp, vp, vp, sz, sz, sz, sz, vp, sz, sz, vp, vp, vp]
     lib.ugo_fec_device_address.argtypes = [vp, vp, ctypes.POINTER(vp)]
     lib.ugo_fec_timing_begin.argtypes = [vp, sz]
     lib.ugo_fec_timing_end.argtypes = [vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
@@ -331,6 +332,26 @@ class Encoder:
             self._h, shards.data_ptr(), present.data_ptr(), G, lst.data_ptr(), count.data_ptr(), m, S, rs, gs,
             None if out is None else out.data_ptr(), ors, oes, RECONSTRUCT_DATA_ONLY if data_only else 0,
             None if status is None else status.data_ptr(), _stream_handle(stream)))
+
+    def recover_data(self, shards, present, out, index, count=None, shard_size: Optional[int] = None,
+                     stream=None, shard_major: bool = True):
+        """ugo_fec_recover_data: `input`'s recovered data shards of a device batch,
+        row-compact in `recovered` order: out[r, :shard_size] (out: contiguous
+        uint8 CUDA [max_rows, row]), index[r] = group*(d+p) + row (int32 CUDA
+        [max_rows]); returns count (int32 CUDA [1], the number recovered,
+        written on the stream)."""
+        import torch
+
+        G, pitch, rs, gs = self._geom(shards, shard_major)
+        _require(present.is_contiguous() and present.numel() == G and present.element_size() == 8)
+        S = pitch if shard_size is None else shard_size
+        _require(out.is_contiguous() and out.element_size() == 1 and out.dim() == 2 and out.shape[1] >= S)
+        _require(index.is_contiguous() and index.element_size() == 4 and index.numel() >= out.shape[0])
+        cnt = torch.empty(1, dtype=torch.int32, device=present.device) if count is None else count
+        _raise(load_library().ugo_fec_recover_data(
+            self._h, shards.data_ptr(), present.data_ptr(), G, S, rs, gs, out.data_ptr(), out.shape[1], out.shape[0],
+            index.data_ptr(), cnt.data_ptr(), _stream_handle(stream)))
+        return cnt
 
     def rx_recover_host(self, wire: np.ndarray, lens: np.ndarray, shard_size: int, groups: int,
                         first_group: int = 0, pad: Optional[bytes] = None, out: Optional[np.ndarray] = None,
