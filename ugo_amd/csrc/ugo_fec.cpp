@@ -1768,10 +1768,14 @@ constexpr size_t kTxChunkBytes = size_t(UGO_TX_CHUNK_MIB) << 20;  // a stage's i
 // At most kTxMaxChunks chunks per call: the chunks grow with the batch past
 // that.  Calls of more chunks ran 2-4x slower, with everything enqueued at once
 // (64-MiB chunks at 65,536 / 131,072 / 262,144 groups: 26.7 / 52-130 / 210 ms;
-// 32-MiB chunks at 65,536: 48-54 ms), and bounding the enqueue from the host
+// 32-MiB chunks at 65,536: 48-54 ms); bounding the enqueue from the host
 // (waiting for chunk k - 16 or k - 8 before enqueueing chunk k) was slower
-// still (42 / 122 / 249 ms) -- profiles/r5/host_tx_chunk_ab*.jsonl.
-constexpr size_t kTxMaxChunks = 32;
+// still (42 / 122 / 249 ms), and so was spreading each copy direction over
+// two streams (43.7 ms at 65,536) -- profiles/r5/host_tx_chunk_ab*.jsonl.
+#ifndef UGO_TX_MAX_CHUNKS
+#define UGO_TX_MAX_CHUNKS 32
+#endif
+constexpr size_t kTxMaxChunks = UGO_TX_MAX_CHUNKS;
 
 int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const uint16_t* lens, size_t groups,
                              uint32_t first_seq, const uint8_t* pad, size_t max_len, uint8_t* wire, size_t slot_out,
