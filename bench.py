@@ -1440,6 +1440,29 @@ def rx_tx_leg(args, dev_index, reps=12):
             sel = (ed > i) & okg  # groups below d shards: no output in either form
             ok_list = ok_list and bool(torch.equal(louts[0][:k][sel, i, :S], outs[0][i, lg[sel], :S]))
         rec_list_k = kernel_ms(rec_list, fec.KERNEL_IDS["reconstruct"], reps)
+        # the same recovery as `input` returns it (ugo_fec_recover_data): the lost data shards
+        # row-compact in `recovered` order with their places, the count on the device
+        rdo = [torch.empty((G * min(d, p), pitch), dtype=torch.uint8, device=dev) for _ in range(2)]
+        rdi = [torch.empty(G * min(d, p), dtype=torch.int32, device=dev) for _ in range(2)]
+        rdc = [torch.empty(1, dtype=torch.int32, device=dev) for _ in range(2)]
+
+        def rec_data(r):
+            i = r % 2
+            enc.recover_data(bats[i], pres[i], rdo[i], rdi[i], count=rdc[i], shard_size=S)
+
+        for r in range(2):
+            rx(r)
+            rec_data(r)
+        torch.cuda.synchronize()
+        nr = int(rdc[0].item())
+        lost = ((pres[0][lg][:, None] >> torch.arange(d, device=dev)) & 1) == 0
+        lost &= okg[:, None]
+        jj, rr = torch.nonzero(lost, as_tuple=True)
+        want_rows = louts[0][:k][torch.arange(p, device=dev)[None, :] < lost.sum(1)[:, None]]
+        ok_rd = nr == int(jj.numel()) and bool(torch.equal(rdi[0][:nr].long(), lg[jj] * n + rr)) and bool(
+            torch.equal(rdo[0][:nr, :S], want_rows[:, :S]))
+        rec_data_k = kernel_ms(rec_data, fec.KERNEL_IDS["reconstruct"], reps)
+        del rdo, rdi, rdc
         # ceilings: the compute-free twins of both forms on the same buffers (after the checks: wrong bytes)
         twin_ms = probe_recover_twin_ms(bats, outs, pres, None, None, G, S, pitch, bats[0].stride(0),
                                         outs[0].stride(0), outs[0].stride(1), reps, stream.cuda_stream)
@@ -1463,6 +1486,8 @@ def rx_tx_leg(args, dev_index, reps=12):
             "reconstruct_list_twin_ms": round(ltwin_ms, 4),
             "reconstruct_list_frac_of_ceiling": round(ltwin_ms / rec_list_k, 4),
             "recovery_faster": "list" if rec_list_k < rec_k else "into", "verify_list_eq_into": ok_list,
+            "recover_data_ms": round(rec_data_k, 4), "recover_data_frac": frac(rec_bytes, rec_data_k),
+            "verify_recover_data": ok_rd,
             "stats": stats, "verify_spot_4096": ok}
         del rings, bats, pres, outs, lsts, cnts, louts
         torch.cuda.empty_cache()
