@@ -387,10 +387,21 @@ int ugo_fec_rx_recover_host(ugo_fec* ctx, const uint8_t* wire, size_t slot_strid
  * packets H2D, assembled, its wire packets D2H, the three on streams of their
  * own through four device stages, so both copy directions run at once; the
  * lengths go in and the wire lengths and statuses come back with one copy
- * each.  Same arguments and results; synchronous. */
+ * each.  When `wire` is pinned, the context may instead have the kernel write
+ * the wire packets through its device mapping (no D2H copy): it times both
+ * routes on its first large calls and keeps the faster (UGO_TX_HOST_OUT=copy
+ * or =mapped pins one).  Same arguments and results (the bytes of a wire slot
+ * past its wire_len are unspecified); synchronous. */
 int ugo_fec_tx_assemble_host(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, const uint16_t* lens,
                              size_t groups, uint32_t first_seq, const uint8_t* pad, size_t max_len,
                              uint8_t* wire, size_t slot_out, uint16_t* wire_lens, int8_t* status);
+
+/* The route ugo_fec_tx_assemble_host takes for a pinned wire buffer: 0 = D2H
+ * copy, 1 = mapped write (the tuned choice, or 0 before any tuning); seconds
+ * per byte (input + output) last measured for each route, 0 if never, into
+ * spb[2] when not NULL, and the context's tuned calls into *calls when not
+ * NULL.  Host-side state only. */
+int ugo_fec_tx_host_route(const ugo_fec* ctx, double* spb, uint64_t* calls);
 
 /* RC4 keystream (crypto/rc4 KSA + PRGA) of a key, host memory: the pad above
  * for ugo's fixed-key rc4StreamCrypto (ugo/crypto.go:14-39). */

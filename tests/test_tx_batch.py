@@ -111,14 +111,18 @@ def test_tx_assemble_vs_sender_loop(gpu, d, p, max_len, G, key, wrap):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,p,max_len,G,key,pinned", [
-    (10, 3, 1476, 97, KEY, True),    # headline geometry: >= 4 chunks over the 3 streams
-    (10, 3, 1476, 5, None, False),   # pageable buffers, one group per chunk
-    (5, 3, 700, 33, KEY, True),      # descriptor kernel
+@pytest.mark.parametrize("d,p,max_len,G,key,pinned,route", [
+    (10, 3, 1476, 97, KEY, True, "copy"),     # headline geometry: >= 4 chunks over the 3 streams
+    (10, 3, 1476, 97, KEY, True, "mapped"),   # the kernel writes the pinned wire buffer itself
+    (10, 3, 1476, 5, None, False, "mapped"),  # pageable buffers (no mapping: the copy route), one group per chunk
+    (5, 3, 700, 33, KEY, True, "copy"),       # descriptor kernel
+    (5, 3, 700, 33, KEY, True, "mapped"),
 ])
-def test_tx_assemble_host_vs_sender_loop(gpu, d, p, max_len, G, key, pinned):
+def test_tx_assemble_host_vs_sender_loop(gpu, monkeypatch, d, p, max_len, G, key, pinned, route):
     """ugo_fec_tx_assemble_host (host memory in and out, chunks pipelined over
-    three streams) against the restated sender loop, statuses included."""
+    three streams; wire packets by D2H copy or written through the pinned
+    buffer's mapping) against the restated sender loop, statuses included."""
+    monkeypatch.setenv("UGO_TX_HOST_OUT", route)
     n = d + p
     enc = fec.New(d, p)
     pk, lens = _batch(d, G, 300 + d + G, max_len)
@@ -154,12 +158,19 @@ def test_tx_assemble_host_vs_sender_loop(gpu, d, p, max_len, G, key, pinned):
 
 
 @pytest.mark.gpu
-def test_tx_assemble_host_many_chunks_matches_device_path(gpu):
+@pytest.mark.parametrize("route", ["copy", "mapped", "auto"])
+def test_tx_assemble_host_many_chunks_matches_device_path(gpu, monkeypatch, route):
     """A batch past tx_assemble_host's chunk cap (32 chunks per call; the
     chunks grow with the batch): 3,400 (32,8) groups of up to 9,006-B packets
     in pinned memory, against the device-resident tx_assemble (itself checked
     against the sender loop above) -- every wire packet within its length,
-    the wire lengths and the statuses, header-only and bad groups included."""
+    the wire lengths and the statuses, header-only and bad groups included.
+    route "auto": seven calls on a fresh context (two warm-up, the copy route
+    timed twice, the mapped route twice, the faster), each checked."""
+    if route == "auto":
+        monkeypatch.delenv("UGO_TX_HOST_OUT", raising=False)
+    else:
+        monkeypatch.setenv("UGO_TX_HOST_OUT", route)
     d, p, max_len, G = 32, 8, 9006, 3400
     n, slot = d + p, (max_len + 15) // 16 * 16
     enc = fec.New(d, p)
@@ -190,14 +201,18 @@ def test_tx_assemble_host_many_chunks_matches_device_path(gpu):
         hst = pinned(G).view(np.int8)
         torch.from_numpy(hp).copy_(dp)
         hl[:] = ln.cpu().numpy().view(np.uint16)
-        hst[:] = -1
-        enc.tx_assemble_host(hp, hl, hw, hwl, pad=pad, max_len=max_len, status=hst)
         want_l = dwl.cpu().numpy().view(np.uint16)
-        assert np.array_equal(hwl, want_l)
-        assert np.array_equal(hst, dst.cpu().numpy())
-        got = torch.from_numpy(hw).cuda()
         keep = torch.arange(slot, device="cuda")[None, :] < dwl.to(torch.int32).view(-1, 1)
-        assert torch.equal(got[keep], dw[keep])
+        for call in range(7 if route == "auto" else 1):
+            hst[:] = -1
+            hwl[:] = 0
+            hw[:, :64] = 0xAB
+            enc.tx_assemble_host(hp, hl, hw, hwl, pad=pad, max_len=max_len, status=hst)
+            assert np.array_equal(hwl, want_l), f"call {call}"
+            assert np.array_equal(hst, dst.cpu().numpy()), f"call {call}"
+            got = torch.from_numpy(hw).cuda()
+            assert torch.equal(got[keep], dw[keep]), f"call {call}"
+            del got
     finally:
         for a in bufs:
             fec.host_free(a)

@@ -99,6 +99,11 @@ struct ugo_fec {
   // d+p > 64: decode descriptors built on the host, one per erasure pattern
   // (klauspost caches its inversions per pattern the same way)
   std::unordered_map<std::string, std::vector<uint8_t>> wide_cache;
+  // host TX output route (tx_route): seconds per byte of the staged copy [0] and the mapped
+  // write [1], the faster of the two, and the tuned calls so far
+  double tx_spb[2] = {0.0, 0.0};
+  int tx_best = 0;
+  uint64_t tx_tuned = 0;
   size_t stage_groups = 0;  // groups per staging buffer
   size_t stage_pitch = 0;
   // launch timing (ugo_fec_timing_begin/end)
@@ -1753,10 +1758,10 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
 // small copy between two large ones costs the engine ~0.1 ms,
 // profiles/r5/host_rx_trace).  Round 5's first form (H2D -> kernel -> D2H per
 // chunk on three round-robin streams, a stream's next input behind its
-// previous output) took 30.6 ms for 65,536 (10+3) groups; the kernel writing
-// pinned outputs through their device mapping instead of the D2H copies took
-// 37.0-37.5 ms against 30.7-30.9 (tools/host_txrx_ab.py,
-// profiles/r5/host_txrx_ab.jsonl).
+// previous output) took 30.6 ms for 65,536 (10+3) groups (tools/host_txrx_ab.py,
+// profiles/r5/host_txrx_ab.jsonl); the kernel reading the pinned data packets
+// through their mapping instead of the H2D copies, 40.1-40.3 ms
+// (profiles/r5/host_tx_route_ab.md).
 #ifndef UGO_TX_STAGES
 #define UGO_TX_STAGES 4
 #endif
@@ -1777,6 +1782,70 @@ constexpr size_t kTxChunkBytes = size_t(UGO_TX_CHUNK_MIB) << 20;  // a stage's i
 #endif
 constexpr size_t kTxMaxChunks = UGO_TX_MAX_CHUNKS;
 
+// The wire packets leave either through the stage and a D2H copy on streams[2]
+// (route 0) or written by the kernel itself through the pinned wire buffer's
+// device mapping (route 1, no D2H copy).  Route 0 reaches 26.0 ms for 65,536
+// (10+3) groups when the runtime runs the two copy directions on different DMA
+// engines, and 40.5 ms when it serializes them -- which of the two depends on
+// the copies other streams of the process made before the context's first
+// (one torch stream's 4-KiB copy ahead of the library's first flips it, and a
+// second flips it back; timing the two copies together on 8 MiB at the first
+// call did not tell the cases apart); route 1 takes 30.4 ms either way, and
+// mixing the routes per chunk lands in between (profiles/r5/host_tx_route_ab.md).
+// So a context tunes over its calls of at least kTxTuneBytes: the first two
+// warm up on route 0 (a context's first copy-route calls ran 31-44 ms before
+// settling), the next two time route 0 and the two after route 1 (the faster of
+// each pair: a route's first call after a switch can run slow), later
+// calls take the faster route and fold their time into its figure, and the
+// last two of every kTxRetune re-time the other.  UGO_TX_HOST_OUT=copy or
+// =mapped pins a route (tests); an unmapped (pageable) wire buffer takes route 0.
+constexpr size_t kTxTuneBytes = size_t(64) << 20;
+constexpr uint64_t kTxRetune = 64;
+
+const char* tx_route_pin() {
+  const char* e = getenv("UGO_TX_HOST_OUT");
+  return e && (!strcmp(e, "copy") || !strcmp(e, "mapped")) ? e : nullptr;
+}
+
+// the route call t of the tuning sequence takes; probe: 1 = the first of a timed pair, 2 = its second
+int tx_route_at(const ugo_fec* c, uint64_t t, int* probe) {
+  *probe = 0;
+  if (t < 2) return 0;
+  if (t < 6) {
+    *probe = t % 2 ? 2 : 1;
+    return t < 4 ? 0 : 1;
+  }
+  const uint64_t e = (t - 6) % kTxRetune;
+  if (e + 2 < kTxRetune) return c->tx_best;
+  *probe = e + 2 == kTxRetune ? 1 : 2;
+  return 1 - c->tx_best;
+}
+
+int tx_route(ugo_fec* c, bool mapped, size_t bytes) {
+  const char* pin = tx_route_pin();
+  if (!mapped || (pin && pin[0] == 'c')) return 0;
+  if (pin) return 1;
+  if (bytes < kTxTuneBytes) return c->tx_best;
+  int probe;
+  return tx_route_at(c, c->tx_tuned, &probe);
+}
+
+void tx_route_done(ugo_fec* c, bool mapped, int route, size_t bytes, double seconds) {
+  if (!mapped || bytes < kTxTuneBytes || tx_route_pin()) return;
+  int probe;
+  const uint64_t t = c->tx_tuned++;
+  if (tx_route_at(c, t, &probe) != route) return;  // not the call the sequence planned (cannot happen)
+  const double v = seconds / double(bytes);
+  double& f = c->tx_spb[route];
+  if (t < 2) return;
+  if (probe == 1) {
+    f = v;
+    return;  // the pair's second call decides
+  }
+  f = probe == 2 ? std::min(f, v) : 0.75 * f + 0.25 * v;
+  c->tx_best = c->tx_spb[1] > 0.0 && c->tx_spb[1] < c->tx_spb[0] ? 1 : 0;
+}
+
 int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const uint16_t* lens, size_t groups,
                              uint32_t first_seq, const uint8_t* pad, size_t max_len, uint8_t* wire, size_t slot_out,
                              uint16_t* wire_lens, int8_t* status) {
@@ -1796,6 +1865,10 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
   if (st) return st;
   const hipStream_t sk = c->streams[0], sin = c->streams[1], sout = c->streams[2];
   const size_t per_group = d * slot_in + n * slot_out;
+  uint8_t* zwire = wire;  // route 1: the wire buffer's device view
+  const bool mapped = device_view(zwire);
+  const int route = tx_route(c, mapped, groups * per_group);
+  const auto t_call = std::chrono::steady_clock::now();
   // groups per chunk: a stage of at most kTxChunkBytes, at least 8 chunks so the two directions
   // overlap, at most kTxMaxChunks
   const size_t cg = std::max<size_t>({size_t(1), (groups + kTxMaxChunks - 1) / kTxMaxChunks,
@@ -1862,13 +1935,17 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
       return UGO_FEC_ERR_HIP;
     a.pkts = sb + o_in;
     a.lens = dlens + g0 * d;
-    a.wire = sb + o_wire;
+    a.wire = route ? zwire + g0 * n * slot_out : sb + o_wire;
     a.wire_lens = dwl + g0 * n;
     a.status = status ? dst + g0 : nullptr;
     a.first_seq = static_cast<uint32_t>((uint64_t(first_seq) + uint64_t(g0) * n) % paws);
     a.g0 = 0;
     a.groups = gn;
     if (ugo::kern::launch_tx_assemble(dmax, a, sk) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (route) {  // the stage is free once the kernel has read it
+      if (hipEventRecord(ev[2 * kTxStages + b], sk) != hipSuccess) return UGO_FEC_ERR_HIP;
+      continue;
+    }
     if (hipEventRecord(ev[kTxStages + b], sk) != hipSuccess ||
         hipStreamWaitEvent(sout, ev[kTxStages + b], 0) != hipSuccess ||
         hipMemcpyAsync(wire + g0 * n * slot_out, sb + o_wire, gn * n * slot_out, hipMemcpyDeviceToHost, sout) !=
@@ -1877,12 +1954,27 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
       return UGO_FEC_ERR_HIP;
   }
   // the wire lengths and statuses of every chunk: one copy each, behind the last chunk's kernel
+  if (route &&
+      (hipEventRecord(ev[kTxStages], sk) != hipSuccess || hipStreamWaitEvent(sout, ev[kTxStages], 0) != hipSuccess))
+    return UGO_FEC_ERR_HIP;
   if (hipMemcpyAsync(wire_lens, dwl, groups * n * 2, hipMemcpyDeviceToHost, sout) != hipSuccess ||
       (status && hipMemcpyAsync(status, dst, groups, hipMemcpyDeviceToHost, sout) != hipSuccess))
     return UGO_FEC_ERR_HIP;
   for (int i = 0; i < kStreams; ++i)
     if (hipStreamSynchronize(c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
+  tx_route_done(c, mapped, route, groups * per_group,
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t_call).count());
   return UGO_FEC_OK;
+}
+
+int ugo_fec_tx_host_route(const ugo_fec* c, double* spb, uint64_t* calls) {
+  if (!c) return UGO_FEC_ERR_INVALID_ARG;
+  if (spb) {
+    spb[0] = c->tx_spb[0];
+    spb[1] = c->tx_spb[1];
+  }
+  if (calls) *calls = c->tx_tuned;
+  return c->tx_best;
 }
 
 int ugo_fec_packet_decode(ugo_fec* c, const uint8_t* pkts, size_t slot, const uint16_t* lens, size_t npk,
