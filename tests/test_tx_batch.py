@@ -118,13 +118,13 @@ def test_tx_assemble_vs_sender_loop(gpu, d, p, max_len, G, key, wrap):
     (5, 3, 700, 33, KEY, True, "copy"),       # descriptor kernel
     (5, 3, 700, 33, KEY, True, "mapped"),
 ])
-def test_tx_assemble_host_vs_sender_loop(gpu, monkeypatch, d, p, max_len, G, key, pinned, route):
+def test_tx_assemble_host_vs_sender_loop(gpu, d, p, max_len, G, key, pinned, route):
     """ugo_fec_tx_assemble_host (host memory in and out, chunks pipelined over
     three streams; wire packets by D2H copy or written through the pinned
     buffer's mapping) against the restated sender loop, statuses included."""
-    monkeypatch.setenv("UGO_TX_HOST_OUT", route)
     n = d + p
     enc = fec.New(d, p)
+    enc.set_tx_host_route(route)
     pk, lens = _batch(d, G, 300 + d + G, max_len)
     slot = (max_len + 15) // 16 * 16
     first_seq = 13 * n
@@ -159,7 +159,7 @@ def test_tx_assemble_host_vs_sender_loop(gpu, monkeypatch, d, p, max_len, G, key
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("route", ["copy", "mapped", "auto"])
-def test_tx_assemble_host_many_chunks_matches_device_path(gpu, monkeypatch, route):
+def test_tx_assemble_host_many_chunks_matches_device_path(gpu, route):
     """A batch past tx_assemble_host's chunk cap (32 chunks per call; the
     chunks grow with the batch): 3,400 (32,8) groups of up to 9,006-B packets
     in pinned memory, against the device-resident tx_assemble (itself checked
@@ -167,13 +167,10 @@ def test_tx_assemble_host_many_chunks_matches_device_path(gpu, monkeypatch, rout
     the wire lengths and the statuses, header-only and bad groups included.
     route "auto": seven calls on a fresh context (two warm-up, the copy route
     timed twice, the mapped route twice, the faster), each checked."""
-    if route == "auto":
-        monkeypatch.delenv("UGO_TX_HOST_OUT", raising=False)
-    else:
-        monkeypatch.setenv("UGO_TX_HOST_OUT", route)
     d, p, max_len, G = 32, 8, 9006, 3400
     n, slot = d + p, (max_len + 15) // 16 * 16
     enc = fec.New(d, p)
+    enc.set_tx_host_route(None if route == "auto" else route)
     gen = torch.Generator(device="cuda").manual_seed(77)
     dp = torch.randint(0, 256, (G * d, slot), dtype=torch.uint8, device="cuda", generator=gen)
     ln = torch.randint(6, max_len + 1, (G * d,), dtype=torch.int32, device="cuda", generator=gen)

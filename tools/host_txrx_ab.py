@@ -43,6 +43,8 @@ def main():
         st.synchronize()
         dummies.append(st)
     enc = fec.Encoder(d, p, device=0)
+    if os.environ.get("HAB_ROUTE"):  # copy / mapped: pin tx_assemble_host's route (default: tuned)
+        enc.set_tx_host_route(os.environ["HAB_ROUTE"])
     gen = torch.Generator(device=dev).manual_seed(11)
     padb = fec.rc4_keystream(b"1234567890123456", slot)
     if "rxfirst" in sys.argv[3:]:  # as bench.py: the host RX case first, on the same context

@@ -103,6 +103,7 @@ struct ugo_fec {
   // write [1], the faster of the two, and the tuned calls so far
   double tx_spb[2] = {0.0, 0.0};
   int tx_best = 0;
+  int tx_pin = -1;  // ugo_fec_set_tx_host_route: -1 tune, 0 / 1 that route
   uint64_t tx_tuned = 0;
   size_t stage_groups = 0;  // groups per staging buffer
   size_t stage_pitch = 0;
@@ -1797,15 +1798,10 @@ constexpr size_t kTxMaxChunks = UGO_TX_MAX_CHUNKS;
 // settling), the next two time route 0 and the two after route 1 (the faster of
 // each pair: a route's first call after a switch can run slow), later
 // calls take the faster route and fold their time into its figure, and the
-// last two of every kTxRetune re-time the other.  UGO_TX_HOST_OUT=copy or
-// =mapped pins a route (tests); an unmapped (pageable) wire buffer takes route 0.
+// last two of every kTxRetune re-time the other.  ugo_fec_set_tx_host_route
+// pins a route; an unmapped (pageable) wire buffer takes route 0.
 constexpr size_t kTxTuneBytes = size_t(64) << 20;
 constexpr uint64_t kTxRetune = 64;
-
-const char* tx_route_pin() {
-  const char* e = getenv("UGO_TX_HOST_OUT");
-  return e && (!strcmp(e, "copy") || !strcmp(e, "mapped")) ? e : nullptr;
-}
 
 // the route call t of the tuning sequence takes; probe: 1 = the first of a timed pair, 2 = its second
 int tx_route_at(const ugo_fec* c, uint64_t t, int* probe) {
@@ -1822,16 +1818,15 @@ int tx_route_at(const ugo_fec* c, uint64_t t, int* probe) {
 }
 
 int tx_route(ugo_fec* c, bool mapped, size_t bytes) {
-  const char* pin = tx_route_pin();
-  if (!mapped || (pin && pin[0] == 'c')) return 0;
-  if (pin) return 1;
+  if (!mapped || c->tx_pin == 0) return 0;
+  if (c->tx_pin == 1) return 1;
   if (bytes < kTxTuneBytes) return c->tx_best;
   int probe;
   return tx_route_at(c, c->tx_tuned, &probe);
 }
 
 void tx_route_done(ugo_fec* c, bool mapped, int route, size_t bytes, double seconds) {
-  if (!mapped || bytes < kTxTuneBytes || tx_route_pin()) return;
+  if (!mapped || bytes < kTxTuneBytes || c->tx_pin >= 0) return;
   int probe;
   const uint64_t t = c->tx_tuned++;
   if (tx_route_at(c, t, &probe) != route) return;  // not the call the sequence planned (cannot happen)
@@ -1964,6 +1959,12 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
     if (hipStreamSynchronize(c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
   tx_route_done(c, mapped, route, groups * per_group,
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t_call).count());
+  return UGO_FEC_OK;
+}
+
+int ugo_fec_set_tx_host_route(ugo_fec* c, int route) {
+  if (!c || route < -1 || route > 1) return UGO_FEC_ERR_INVALID_ARG;
+  c->tx_pin = route;
   return UGO_FEC_OK;
 }
 

@@ -147,6 +147,7 @@ def load_library(path: str = LIB_PATH):
                                             ctypes.POINTER(sz)]
     lib.ugo_fec_tx_assemble_host.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp]
     lib.ugo_fec_tx_host_route.argtypes = [vp, vp, vp]
+    lib.ugo_fec_set_tx_host_route.argtypes = [vp, ctypes.c_int]
     lib.ugo_fec_reconstruct_list.argtypes = [vp, vp, vp, sz, vp, vp, sz, sz, sz, sz, vp, sz, sz, u, vp, vp]
     lib.ugo_fec_recover_data.argtypes = [vp, vp, vp, sz, sz, sz, sz, vp, sz, sz, vp, vp, vp]
     lib.ugo_fec_device_address.argtypes = [vp, vp, ctypes.POINTER(vp)]
@@ -403,6 +404,11 @@ class Encoder:
         r = load_library().ugo_fec_tx_host_route(self._h, spb, ctypes.byref(calls))
         _raise(min(r, 0))
         return r, [spb[0], spb[1]], calls.value
+
+    def set_tx_host_route(self, route: Optional[str]):
+        """ugo_fec_set_tx_host_route: "copy", "mapped", or None (tune)."""
+        _require(route in (None, "copy", "mapped"))
+        _raise(load_library().ugo_fec_set_tx_host_route(self._h, {None: -1, "copy": 0, "mapped": 1}[route]))
 
     def reconstruct_rows(self, rows, present, out, shard_size: int, data_only=False, status=None, stream=None,
                          out_shard_major: bool = True):
