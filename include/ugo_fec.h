@@ -387,25 +387,18 @@ int ugo_fec_rx_recover_host(ugo_fec* ctx, const uint8_t* wire, size_t slot_strid
  * packets H2D, assembled, its wire packets D2H, the three on streams of their
  * own through four device stages, so both copy directions run at once; the
  * lengths go in and the wire lengths and statuses come back with one copy
- * each.  When `wire` is pinned, the context may instead have the kernel write
- * the wire packets through its device mapping (no D2H copy): it times both
- * routes on its first large calls and keeps the faster
- * (ugo_fec_set_tx_host_route pins one).  Same arguments and results (the bytes of a wire slot
- * past its wire_len are unspecified); synchronous. */
+ * each (ugo_fec_set_tx_host_route: the wire packets written through the
+ * buffer's mapping instead).  Same arguments and results (the bytes of a wire
+ * slot past its wire_len are unspecified); synchronous. */
 int ugo_fec_tx_assemble_host(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, const uint16_t* lens,
                              size_t groups, uint32_t first_seq, const uint8_t* pad, size_t max_len,
                              uint8_t* wire, size_t slot_out, uint16_t* wire_lens, int8_t* status);
 
-/* The route ugo_fec_tx_assemble_host takes for a pinned wire buffer: 0 = D2H
- * copy, 1 = mapped write (the tuned choice, or 0 before any tuning); seconds
- * per byte (input + output) last measured for each route, 0 if never, into
- * spb[2] when not NULL, and the context's tuned calls into *calls when not
- * NULL.  Host-side state only. */
-int ugo_fec_tx_host_route(const ugo_fec* ctx, double* spb, uint64_t* calls);
-
-/* Pins the route of ugo_fec_tx_assemble_host for a pinned wire buffer: 0 = D2H
- * copy, 1 = mapped write, -1 = tune (the default).  UGO_FEC_ERR_INVALID_ARG for
- * any other value. */
+/* The route of ugo_fec_tx_assemble_host's wire packets: 0 = through the
+ * device stage and a D2H copy (the default), 1 = written by the kernel through
+ * the wire buffer's device mapping, no D2H copy (only when the wire buffer is
+ * pinned and 16-B aligned; otherwise the call takes route 0).  Both give the
+ * same packets and lengths.  UGO_FEC_ERR_INVALID_ARG for any other value. */
 int ugo_fec_set_tx_host_route(ugo_fec* ctx, int route);
 
 /* RC4 keystream (crypto/rc4 KSA + PRGA) of a key, host memory: the pad above

@@ -43,7 +43,7 @@ def main():
         st.synchronize()
         dummies.append(st)
     enc = fec.Encoder(d, p, device=0)
-    if os.environ.get("HAB_ROUTE"):  # copy / mapped: pin tx_assemble_host's route (default: tuned)
+    if os.environ.get("HAB_ROUTE"):  # copy / mapped: tx_assemble_host's wire route (default copy)
         enc.set_tx_host_route(os.environ["HAB_ROUTE"])
     gen = torch.Generator(device=dev).manual_seed(11)
     padb = fec.rc4_keystream(b"1234567890123456", slot)

@@ -99,12 +99,7 @@ struct ugo_fec {
   // d+p > 64: decode descriptors built on the host, one per erasure pattern
   // (klauspost caches its inversions per pattern the same way)
   std::unordered_map<std::string, std::vector<uint8_t>> wide_cache;
-  // host TX output route (tx_route): seconds per byte of the staged copy [0] and the mapped
-  // write [1], the faster of the two, and the tuned calls so far
-  double tx_spb[2] = {0.0, 0.0};
-  int tx_best = 0;
-  int tx_pin = -1;  // ugo_fec_set_tx_host_route: -1 tune, 0 / 1 that route
-  uint64_t tx_tuned = 0;
+  int tx_route = 0;  // host TX wire route (ugo_fec_set_tx_host_route): 0 D2H copy, 1 mapped write
   size_t stage_groups = 0;  // groups per staging buffer
   size_t stage_pitch = 0;
   // launch timing (ugo_fec_timing_begin/end)
@@ -547,10 +542,30 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
   return UGO_FEC_OK;
 }
 
+// The host paths' stream i: 0 kernels, 1 H2D copies, 2 D2H copies.  HIP maps
+// the streams of a process onto a small pool of hardware queues per priority
+// class (GPU_MAX_HW_QUEUES, 4 here) in creation order, and a queue processes
+// its packets in order: when the H2D stream and the D2H stream shared one, the
+// D2H copy kernels waited behind the next chunk's H2D dependency and the host
+// TX call's two copy directions ran one after the other -- 40.5 ms instead of
+// 26.6 for 65,536 (10+3) groups, depending on how many streams the process had
+// made before (profiles/r5/host_tx_route_ab.md).  The H2D stream now comes from
+// the low-priority class (its own queue pool; its packets are copies and event
+// waits, which priority does not slow): 26.0-27.6 ms whatever came before.  A
+// full CU mask (a queue of its own per stream) and low / normal / high classes
+// measured the same, but cost a queue per context or share the service's class.
+hipError_t create_stream(int i, hipStream_t* s) {
+  if (i == 1) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return hipErrorInvalidValue;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 int ensure_streams(ugo_fec* c) {
   for (int i = 0; i < kStreams; ++i)
-    if (!c->streams[i] && hipStreamCreateWithFlags(&c->streams[i], hipStreamNonBlocking) != hipSuccess)
-      return UGO_FEC_ERR_HIP;
+    if (!c->streams[i] && create_stream(i, &c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
   return UGO_FEC_OK;
 }
 
@@ -568,8 +583,7 @@ int ensure_stage(ugo_fec* c, size_t pitch) {
   }
   c->stage_groups = 0;
   for (int i = 0; i < kStreams; ++i) {
-    if (!c->streams[i] && hipStreamCreateWithFlags(&c->streams[i], hipStreamNonBlocking) != hipSuccess)
-      return UGO_FEC_ERR_HIP;
+    if (!c->streams[i] && create_stream(i, &c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_stage[i], want * gbytes + 16) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_mask[i], want * mask_words(c) * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_status[i], want) != hipSuccess) return UGO_FEC_ERR_HIP;
@@ -1783,63 +1797,12 @@ constexpr size_t kTxChunkBytes = size_t(UGO_TX_CHUNK_MIB) << 20;  // a stage's i
 #endif
 constexpr size_t kTxMaxChunks = UGO_TX_MAX_CHUNKS;
 
-// The wire packets leave either through the stage and a D2H copy on streams[2]
-// (route 0) or written by the kernel itself through the pinned wire buffer's
-// device mapping (route 1, no D2H copy).  Route 0 reaches 26.0 ms for 65,536
-// (10+3) groups when the runtime runs the two copy directions on different DMA
-// engines, and 40.5 ms when it serializes them -- which of the two depends on
-// the copies other streams of the process made before the context's first
-// (one torch stream's 4-KiB copy ahead of the library's first flips it, and a
-// second flips it back; timing the two copies together on 8 MiB at the first
-// call did not tell the cases apart); route 1 takes 30.4 ms either way, and
-// mixing the routes per chunk lands in between (profiles/r5/host_tx_route_ab.md).
-// So a context tunes over its calls of at least kTxTuneBytes: the first two
-// warm up on route 0 (a context's first copy-route calls ran 31-44 ms before
-// settling), the next two time route 0 and the two after route 1 (the faster of
-// each pair: a route's first call after a switch can run slow), later
-// calls take the faster route and fold their time into its figure, and the
-// last two of every kTxRetune re-time the other.  ugo_fec_set_tx_host_route
-// pins a route; an unmapped (pageable) wire buffer takes route 0.
-constexpr size_t kTxTuneBytes = size_t(64) << 20;
-constexpr uint64_t kTxRetune = 64;
-
-// the route call t of the tuning sequence takes; probe: 1 = the first of a timed pair, 2 = its second
-int tx_route_at(const ugo_fec* c, uint64_t t, int* probe) {
-  *probe = 0;
-  if (t < 2) return 0;
-  if (t < 6) {
-    *probe = t % 2 ? 2 : 1;
-    return t < 4 ? 0 : 1;
-  }
-  const uint64_t e = (t - 6) % kTxRetune;
-  if (e + 2 < kTxRetune) return c->tx_best;
-  *probe = e + 2 == kTxRetune ? 1 : 2;
-  return 1 - c->tx_best;
-}
-
-int tx_route(ugo_fec* c, bool mapped, size_t bytes) {
-  if (!mapped || c->tx_pin == 0) return 0;
-  if (c->tx_pin == 1) return 1;
-  if (bytes < kTxTuneBytes) return c->tx_best;
-  int probe;
-  return tx_route_at(c, c->tx_tuned, &probe);
-}
-
-void tx_route_done(ugo_fec* c, bool mapped, int route, size_t bytes, double seconds) {
-  if (!mapped || bytes < kTxTuneBytes || c->tx_pin >= 0) return;
-  int probe;
-  const uint64_t t = c->tx_tuned++;
-  if (tx_route_at(c, t, &probe) != route) return;  // not the call the sequence planned (cannot happen)
-  const double v = seconds / double(bytes);
-  double& f = c->tx_spb[route];
-  if (t < 2) return;
-  if (probe == 1) {
-    f = v;
-    return;  // the pair's second call decides
-  }
-  f = probe == 2 ? std::min(f, v) : 0.75 * f + 0.25 * v;
-  c->tx_best = c->tx_spb[1] > 0.0 && c->tx_spb[1] < c->tx_spb[0] ? 1 : 0;
-}
+// The wire packets leave through the stage and a D2H copy on streams[2]
+// (route 0), or, pinned by ugo_fec_set_tx_host_route, written by the kernel
+// itself through the pinned wire buffer's device mapping (route 1, no D2H
+// copy: 30.4 ms for 65,536 (10+3) groups against 26.0-27.6,
+// profiles/r5/host_tx_route_ab.md).  An unmapped (pageable) or unaligned wire
+// buffer takes route 0.
 
 int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const uint16_t* lens, size_t groups,
                              uint32_t first_seq, const uint8_t* pad, size_t max_len, uint8_t* wire, size_t slot_out,
@@ -1860,10 +1823,9 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
   if (st) return st;
   const hipStream_t sk = c->streams[0], sin = c->streams[1], sout = c->streams[2];
   const size_t per_group = d * slot_in + n * slot_out;
-  uint8_t* zwire = wire;  // route 1: the wire buffer's device view
-  const bool mapped = device_view(zwire);
-  const int route = tx_route(c, mapped, groups * per_group);
-  const auto t_call = std::chrono::steady_clock::now();
+  uint8_t* zwire = wire;  // route 1: the wire buffer's device view, 16-B aligned
+  const int route =
+      c->tx_route == 1 && device_view(zwire) && reinterpret_cast<uintptr_t>(zwire) % 16 == 0 ? 1 : 0;
   // groups per chunk: a stage of at most kTxChunkBytes, at least 8 chunks so the two directions
   // overlap, at most kTxMaxChunks
   const size_t cg = std::max<size_t>({size_t(1), (groups + kTxMaxChunks - 1) / kTxMaxChunks,
@@ -1930,14 +1892,14 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
       return UGO_FEC_ERR_HIP;
     a.pkts = sb + o_in;
     a.lens = dlens + g0 * d;
-    a.wire = route ? zwire + g0 * n * slot_out : sb + o_wire;
+    a.wire = route == 1 ? zwire + g0 * n * slot_out : sb + o_wire;
     a.wire_lens = dwl + g0 * n;
     a.status = status ? dst + g0 : nullptr;
     a.first_seq = static_cast<uint32_t>((uint64_t(first_seq) + uint64_t(g0) * n) % paws);
     a.g0 = 0;
     a.groups = gn;
     if (ugo::kern::launch_tx_assemble(dmax, a, sk) != hipSuccess) return UGO_FEC_ERR_HIP;
-    if (route) {  // the stage is free once the kernel has read it
+    if (route == 1) {  // the stage is free once the kernel has read it
       if (hipEventRecord(ev[2 * kTxStages + b], sk) != hipSuccess) return UGO_FEC_ERR_HIP;
       continue;
     }
@@ -1949,7 +1911,7 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
       return UGO_FEC_ERR_HIP;
   }
   // the wire lengths and statuses of every chunk: one copy each, behind the last chunk's kernel
-  if (route &&
+  if (route == 1 &&
       (hipEventRecord(ev[kTxStages], sk) != hipSuccess || hipStreamWaitEvent(sout, ev[kTxStages], 0) != hipSuccess))
     return UGO_FEC_ERR_HIP;
   if (hipMemcpyAsync(wire_lens, dwl, groups * n * 2, hipMemcpyDeviceToHost, sout) != hipSuccess ||
@@ -1957,25 +1919,13 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
     return UGO_FEC_ERR_HIP;
   for (int i = 0; i < kStreams; ++i)
     if (hipStreamSynchronize(c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
-  tx_route_done(c, mapped, route, groups * per_group,
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t_call).count());
   return UGO_FEC_OK;
 }
 
 int ugo_fec_set_tx_host_route(ugo_fec* c, int route) {
-  if (!c || route < -1 || route > 1) return UGO_FEC_ERR_INVALID_ARG;
-  c->tx_pin = route;
+  if (!c || route < 0 || route > 1) return UGO_FEC_ERR_INVALID_ARG;
+  c->tx_route = route;
   return UGO_FEC_OK;
-}
-
-int ugo_fec_tx_host_route(const ugo_fec* c, double* spb, uint64_t* calls) {
-  if (!c) return UGO_FEC_ERR_INVALID_ARG;
-  if (spb) {
-    spb[0] = c->tx_spb[0];
-    spb[1] = c->tx_spb[1];
-  }
-  if (calls) *calls = c->tx_tuned;
-  return c->tx_best;
 }
 
 int ugo_fec_packet_decode(ugo_fec* c, const uint8_t* pkts, size_t slot, const uint16_t* lens, size_t npk,

@@ -146,7 +146,6 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_rx_recover_host.argtypes = [vp, vp, sz, vp, sz, vp, ctypes.c_uint64, sz, sz, vp, vp, vp, sz, sz, vp,
                                             ctypes.POINTER(sz)]
     lib.ugo_fec_tx_assemble_host.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp]
-    lib.ugo_fec_tx_host_route.argtypes = [vp, vp, vp]
     lib.ugo_fec_set_tx_host_route.argtypes = [vp, ctypes.c_int]
     lib.ugo_fec_reconstruct_list.argtypes = [vp, vp, vp, sz, vp, vp, sz, sz, sz, sz, vp, sz, sz, u, vp, vp]
     lib.ugo_fec_recover_data.argtypes = [vp, vp, vp, sz, sz, sz, sz, vp, sz, sz, vp, vp, vp]
@@ -396,19 +395,12 @@ class Encoder:
             None if padb is None else padb.ctypes.data, max_len, wire.ctypes.data, wire.shape[1],
             wire_lens.ctypes.data, None if status is None else status.ctypes.data))
 
-    def tx_host_route(self):
-        """ugo_fec_tx_host_route: (route, [copy s/B, mapped s/B], tuned calls) of
-        tx_assemble_host's wire-packet route (0: D2H copy, 1: mapped write)."""
-        spb = (ctypes.c_double * 2)()
-        calls = ctypes.c_uint64()
-        r = load_library().ugo_fec_tx_host_route(self._h, spb, ctypes.byref(calls))
-        _raise(min(r, 0))
-        return r, [spb[0], spb[1]], calls.value
-
-    def set_tx_host_route(self, route: Optional[str]):
-        """ugo_fec_set_tx_host_route: "copy", "mapped", or None (tune)."""
-        _require(route in (None, "copy", "mapped"))
-        _raise(load_library().ugo_fec_set_tx_host_route(self._h, {None: -1, "copy": 0, "mapped": 1}[route]))
+    def set_tx_host_route(self, route: str):
+        """ugo_fec_set_tx_host_route: tx_assemble_host's wire packets by D2H
+        copy ("copy", the default) or written through the pinned buffer's
+        mapping ("mapped")."""
+        _require(route in ("copy", "mapped"))
+        _raise(load_library().ugo_fec_set_tx_host_route(self._h, {"copy": 0, "mapped": 1}[route]))
 
     def reconstruct_rows(self, rows, present, out, shard_size: int, data_only=False, status=None, stream=None,
                          out_shard_major: bool = True):
