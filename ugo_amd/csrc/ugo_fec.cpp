@@ -542,18 +542,19 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
   return UGO_FEC_OK;
 }
 
-// The host paths' stream i: 0 kernels, 1 H2D copies, 2 D2H copies.  HIP maps
-// the streams of a process onto a small pool of hardware queues per priority
-// class (GPU_MAX_HW_QUEUES, 4 here) in creation order, and a queue processes
-// its packets in order: when the H2D stream and the D2H stream shared one, the
-// D2H copy kernels waited behind the next chunk's H2D dependency and the host
-// TX call's two copy directions ran one after the other -- 40.5 ms instead of
-// 26.6 for 65,536 (10+3) groups, depending on how many streams the process had
-// made before (profiles/r5/host_tx_route_ab.md).  The H2D stream now comes from
-// the low-priority class (its own queue pool; its packets are copies and event
-// waits, which priority does not slow): 26.0-27.6 ms whatever came before.  A
-// full CU mask (a queue of its own per stream) and low / normal / high classes
-// measured the same, but cost a queue per context or share the service's class.
+// The host paths' streams: 0 kernels (and host TX's D2H copies), 1 H2D copies,
+// 2 the other RX copy stream / the staged paths' third stream.  HIP maps a
+// process's streams onto a small pool of hardware queues per priority class
+// (GPU_MAX_HW_QUEUES, 4 here) in creation order, and a queue processes its
+// packets in order: when host TX's H2D stream shared a queue with its D2H
+// stream, each D2H copy waited behind the next chunk's H2D dependency and the
+// two copy directions ran one after the other -- 40.5 ms instead of 26.6 for
+// 65,536 (10+3) groups, depending on how many streams the process had made
+// before (profiles/r5/host_tx_route_ab.md).  Stream 1 comes from the
+// low-priority class, a pool of its own (its packets are copies and event
+// waits, which priority does not slow).  A full CU mask (a queue per stream)
+// and low / normal / high classes measured the same, but cost a queue per
+// context or share the per-call service's class.
 hipError_t create_stream(int i, hipStream_t* s) {
   if (i == 1) {
     int least = 0, greatest = 0;
@@ -1765,11 +1766,14 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
 }
 
 // The TX path from host memory to host memory: groups in chunks through
-// kTxStages device stages, one stream per role -- the data packets' H2D on
-// streams[1], tx_assemble on streams[0], the wire packets' D2H on streams[2] --
-// joined by events, so each copy engine streams its direction without waiting
-// for the other; the lengths go in with one copy ahead of the first chunk and
-// the wire lengths and statuses come back with one copy after the last (a
+// kTxStages device stages -- the data packets' H2D on streams[1] (its own
+// hardware queue, create_stream), tx_assemble and then the wire packets' D2H on
+// streams[0] -- joined by events, so the two copy directions run at once (a
+// third stream for the D2H copies ran 25.9-28.6 ms over six process histories,
+// the D2H behind the kernel on its stream 26.5-26.6 in all six,
+// profiles/r5/host_tx_route/host_tx_d2h_stream.jsonl); the lengths go in with
+// one copy ahead of the first chunk and the wire lengths and statuses come back
+// with one copy after the last (a
 // small copy between two large ones costs the engine ~0.1 ms,
 // profiles/r5/host_rx_trace).  Round 5's first form (H2D -> kernel -> D2H per
 // chunk on three round-robin streams, a stream's next input behind its
@@ -1821,7 +1825,7 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
   TimerScope ts(c);
   int st = ensure_streams(c);
   if (st) return st;
-  const hipStream_t sk = c->streams[0], sin = c->streams[1], sout = c->streams[2];
+  const hipStream_t sk = c->streams[0], sin = c->streams[1];
   const size_t per_group = d * slot_in + n * slot_out;
   uint8_t* zwire = wire;  // route 1: the wire buffer's device view, 16-B aligned
   const int route =
@@ -1839,7 +1843,7 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
   uint8_t* base = nullptr;
   st = scratch_alloc(c, o_stages + size_t(kTxStages) * stage_bytes, sk, reinterpret_cast<void**>(&base));
   if (st) return st;
-  constexpr int kEv = 3 * kTxStages + 1;  // in[b] | kernel[b] | out[b] (stage free) | ready
+  constexpr int kEv = 2 * kTxStages + 1;  // in[b] | out[b] (stage free) | ready
   hipEvent_t ev[kEv] = {};
   struct Release {  // the copy streams finish before the scratch goes back (also on an early return)
     ugo_fec* c;
@@ -1860,9 +1864,8 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
   int8_t* dst = reinterpret_cast<int8_t*>(base + o_st);
   uint8_t* dpad = pad ? base + o_pad : nullptr;
   if ((pad && hipMemcpyAsync(dpad, pad, need, hipMemcpyHostToDevice, sk) != hipSuccess) ||
-      hipEventRecord(ev[3 * kTxStages], sk) != hipSuccess ||  // the scratch is this call's from here on
-      hipStreamWaitEvent(sin, ev[3 * kTxStages], 0) != hipSuccess ||
-      hipStreamWaitEvent(sout, ev[3 * kTxStages], 0) != hipSuccess ||
+      hipEventRecord(ev[2 * kTxStages], sk) != hipSuccess ||  // the scratch is this call's from here on
+      hipStreamWaitEvent(sin, ev[2 * kTxStages], 0) != hipSuccess ||
       hipMemcpyAsync(dlens, lens, groups * d * 2, hipMemcpyHostToDevice, sin) != hipSuccess)
     return UGO_FEC_ERR_HIP;
   ugo::kern::TxArgs a{};
@@ -1885,7 +1888,7 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
     uint8_t* sb = base + o_stages + b * stage_bytes;
     // input: the stage's previous output (chunk k - kTxStages) must have left; chunk 0's event also
     // covers the lengths, copied before it on the same stream
-    if ((k >= size_t(kTxStages) && hipStreamWaitEvent(sin, ev[2 * kTxStages + b], 0) != hipSuccess) ||
+    if ((k >= size_t(kTxStages) && hipStreamWaitEvent(sin, ev[kTxStages + b], 0) != hipSuccess) ||
         hipMemcpyAsync(sb + o_in, pkts + g0 * d * slot_in, gn * d * slot_in, hipMemcpyHostToDevice, sin) !=
             hipSuccess ||
         hipEventRecord(ev[b], sin) != hipSuccess || hipStreamWaitEvent(sk, ev[b], 0) != hipSuccess)
@@ -1898,24 +1901,17 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
     a.first_seq = static_cast<uint32_t>((uint64_t(first_seq) + uint64_t(g0) * n) % paws);
     a.g0 = 0;
     a.groups = gn;
-    if (ugo::kern::launch_tx_assemble(dmax, a, sk) != hipSuccess) return UGO_FEC_ERR_HIP;
-    if (route == 1) {  // the stage is free once the kernel has read it
-      if (hipEventRecord(ev[2 * kTxStages + b], sk) != hipSuccess) return UGO_FEC_ERR_HIP;
-      continue;
-    }
-    if (hipEventRecord(ev[kTxStages + b], sk) != hipSuccess ||
-        hipStreamWaitEvent(sout, ev[kTxStages + b], 0) != hipSuccess ||
-        hipMemcpyAsync(wire + g0 * n * slot_out, sb + o_wire, gn * n * slot_out, hipMemcpyDeviceToHost, sout) !=
-            hipSuccess ||
-        hipEventRecord(ev[2 * kTxStages + b], sout) != hipSuccess)
+    // the wire packets out behind the kernel on its stream (route 1: already written); the stage
+    // is free after that
+    if (ugo::kern::launch_tx_assemble(dmax, a, sk) != hipSuccess ||
+        (route == 0 && hipMemcpyAsync(wire + g0 * n * slot_out, sb + o_wire, gn * n * slot_out,
+                                      hipMemcpyDeviceToHost, sk) != hipSuccess) ||
+        hipEventRecord(ev[kTxStages + b], sk) != hipSuccess)
       return UGO_FEC_ERR_HIP;
   }
   // the wire lengths and statuses of every chunk: one copy each, behind the last chunk's kernel
-  if (route == 1 &&
-      (hipEventRecord(ev[kTxStages], sk) != hipSuccess || hipStreamWaitEvent(sout, ev[kTxStages], 0) != hipSuccess))
-    return UGO_FEC_ERR_HIP;
-  if (hipMemcpyAsync(wire_lens, dwl, groups * n * 2, hipMemcpyDeviceToHost, sout) != hipSuccess ||
-      (status && hipMemcpyAsync(status, dst, groups, hipMemcpyDeviceToHost, sout) != hipSuccess))
+  if (hipMemcpyAsync(wire_lens, dwl, groups * n * 2, hipMemcpyDeviceToHost, sk) != hipSuccess ||
+      (status && hipMemcpyAsync(status, dst, groups, hipMemcpyDeviceToHost, sk) != hipSuccess))
     return UGO_FEC_ERR_HIP;
   for (int i = 0; i < kStreams; ++i)
     if (hipStreamSynchronize(c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
