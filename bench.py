@@ -932,7 +932,7 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
                               "entry-form list reconstruct, D2H of every entry's p row slots",
             "zero_copy_wire_GBps": None if t_zc is None else round(wire_bytes / t_zc / 1e9, 2),
             "verify_vs_device_path": ok,
-            "path": "pinned ring -> H2D in >= 4 chunks on 2 copy streams, each chunk assembled as it lands -> "
+            "path": "pinned ring -> H2D in >= 4 chunks on one copy stream, each chunk assembled as it lands -> "
                     "lossy-group list with row offsets -> data-only list reconstruct, row-compact -> D2H of "
                     "the recovered shards only (ugo's `recovered` order)"}
         box.clear()

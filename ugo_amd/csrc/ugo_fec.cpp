@@ -1633,9 +1633,9 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
 
 // ---- host-memory RX and TX paths ---------------------------
 // The whole RX path from host memory to host memory: a received packet ring in
-// pinned memory (a recvmmsg batch) is copied to the device in chunks on two
-// copy streams, each chunk assembled (rx_assemble_dev, one call per chunk into
-// one batch: first copy wins across the calls) on a third stream as soon as its
+// pinned memory (a recvmmsg batch) is copied to the device in chunks on one
+// copy stream, each chunk assembled (rx_assemble_dev, one call per chunk into
+// one batch: first copy wins across the calls) on a second stream as soon as its
 // copy lands, so copies and kernels overlap; then the lossy-group list, the
 // data-only Reconstruct of those groups into a row-compact output (the
 // `recovered` list of ugo/fec.go:203-207), and the D2H of those rows only.
@@ -1657,7 +1657,7 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   TimerScope ts(c);
   int st = ensure_streams(c);
   if (st) return st;
-  const hipStream_t s0 = c->streams[0];  // assembly and recovery; copies on streams 1 and 2
+  const hipStream_t s0 = c->streams[0];  // assembly and recovery; copies on streams[1]
   const size_t n = size_t(c->n), pitch = round_up(S, 16), slots = size_t(std::min(c->d, c->p));
   // packets per chunk: at most a 64-MiB stage, at least 4 chunks so copies and assembly overlap, and
   // at most 32 chunks (the chunks grow with the ring past that: see kTxMaxChunks)
@@ -1724,7 +1724,10 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   for (size_t k = 0; k < nchunks; ++k) {
     for (; next < nchunks && next < k + kRxStages; ++next) {
       const int b = static_cast<int>(next % kRxStages);
-      const hipStream_t cs = c->streams[1 + (next & 1)];
+      // every ring copy on streams[1] (its own hardware queue, create_stream): 23.1-23.2 ms over six
+      // process histories, against 22.3-25.0 alternating streams 1 and 2
+      // (profiles/r5/host_tx_route/host_rx_copy_streams_*.jsonl)
+      const hipStream_t cs = c->streams[1];
       const size_t p0 = next * cpk, m = std::min(cpk, npk - p0);
       if (hipStreamWaitEvent(cs, ev[kRxStages + b], 0) != hipSuccess ||
           hipMemcpyAsync(base + o_stage + b * stage_bytes, wire + p0 * slot_stride, m * slot_stride,
@@ -1801,7 +1804,7 @@ constexpr size_t kTxChunkBytes = size_t(UGO_TX_CHUNK_MIB) << 20;  // a stage's i
 #endif
 constexpr size_t kTxMaxChunks = UGO_TX_MAX_CHUNKS;
 
-// The wire packets leave through the stage and a D2H copy on streams[2]
+// The wire packets leave through the stage and a D2H copy behind the kernel
 // (route 0), or, pinned by ugo_fec_set_tx_host_route, written by the kernel
 // itself through the pinned wire buffer's device mapping (route 1, no D2H
 // copy: 30.4 ms for 65,536 (10+3) groups against 26.0-27.6,
