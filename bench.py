@@ -926,6 +926,8 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             "groups_per_rank": G, "packets_per_rank": npk, "loss": 0.05, "rc4": True, "recovered_shards_rank0": nrec,
             "rx_ms": round(t_rx * 1e3, 3), "wire_GBps": round(wire_bytes / t_rx / 1e9, 2),
             "pcie_GBps_per_gpu": round(pcie / t_rx / 1e9, 2), "rank0_alone_ms": round(t_rx_mine * 1e3, 3),
+            "pcie_bound_ms": _r3(pcie_bound_ms(res.get("pcie_ceiling"), npk * (slot + 2), nrec * S)),
+            "of_pcie_bound": _r3(pcie_bound_ms(res.get("pcie_ceiling"), npk * (slot + 2), nrec * S), t_rx * 1e3),
             "rep_ms": [round(t * 1e3, 2) for t in rx_reps],
             "zero_copy_ring_ms": None if t_zc is None else round(t_zc * 1e3, 3),
             "zero_copy_note": "rx_assemble reading the pinned ring in place, then the public lossy list + "
@@ -973,6 +975,9 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             "groups_per_rank": G, "packets_out_per_rank": G * n, "rc4": True, "tx_ms": round(t_tx * 1e3, 3),
             "wire_GBps": round(world * G * n * 1476 / t_tx / 1e9, 2),
             "pcie_GBps_per_gpu": round(G * (d + n) * slot / t_tx / 1e9, 2), "rank0_alone_ms": round(t_tx_mine * 1e3, 3),
+            "pcie_bound_ms": _r3(pcie_bound_ms(res.get("pcie_ceiling"), G * d * (slot + 2), G * n * (slot + 2))),
+            "of_pcie_bound": _r3(pcie_bound_ms(res.get("pcie_ceiling"), G * d * (slot + 2), G * n * (slot + 2)),
+                                 t_tx * 1e3),
             "rep_ms": [round(t * 1e3, 2) for t in tx_reps],
             "verify_vs_device_path": ok,
             "path": "pinned data packets -> H2D -> tx_assemble -> D2H of the wire packets, group chunks through "
@@ -987,6 +992,31 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
         enc.close()
         torch.cuda.empty_cache()
     return res, ok_all and st["err"] is None
+
+
+def _r3(x, div=None):
+    """round(x, 3), or x / div rounded; None passes through."""
+    if x is None:
+        return None
+    return round(x / div if div else x, 3)
+
+
+def pcie_bound_ms(ceiling, h2d_bytes, d2h_bytes):
+    """The least time the measured link allows for h2d_bytes in and d2h_bytes
+    out, both directions streaming at once: each direction at half the measured
+    two-way rate while both run, then the longer one alone at its one-way rate.
+    None without a ceiling."""
+    try:
+        h2d, d2h, both = ceiling["h2d_GBps"] * 1e9, ceiling["d2h_GBps"] * 1e9, ceiling["bidirectional_GBps"] * 1e9
+    except (KeyError, TypeError):
+        return None
+    if not d2h_bytes:
+        return h2d_bytes / h2d * 1e3
+    if not h2d_bytes:
+        return d2h_bytes / d2h * 1e3
+    t1 = min(h2d_bytes, d2h_bytes) / (both / 2)  # both directions at once
+    rest = max(h2d_bytes, d2h_bytes) - t1 * both / 2
+    return (t1 + rest / (h2d if h2d_bytes > d2h_bytes else d2h)) * 1e3
 
 
 def timed_reps(call, reps, world, all_out=None):
