@@ -401,6 +401,17 @@ int ugo_fec_tx_assemble_host(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, 
  * same packets and lengths.  UGO_FEC_ERR_INVALID_ARG for any other value. */
 int ugo_fec_set_tx_host_route(ugo_fec* ctx, int route);
 
+/* on = 1: the host paths' H2D copy stream (ugo_fec_rx_recover_host,
+ * ugo_fec_tx_assemble_host, the staged *_host paths) comes from the
+ * low-priority stream class, whose hardware queues are a pool of their own, so
+ * it never shares one with the context's kernel stream.  Measured: host TX
+ * 26.5-26.6 ms for 65,536 (10+3) groups whatever streams the process made
+ * before, against 26.5 ms in five of six process histories and 40.1 in the
+ * sixth with on = 0 (the default); but the extra hardware queue slowed
+ * concurrent device work 33-39 % in one process while a per-call service block
+ * was resident.  Synchronizes and replaces the stream when it exists. */
+int ugo_fec_set_host_copy_queue(ugo_fec* ctx, int on);
+
 /* RC4 keystream (crypto/rc4 KSA + PRGA) of a key, host memory: the pad above
  * for ugo's fixed-key rc4StreamCrypto (ugo/crypto.go:14-39). */
 int ugo_fec_rc4_keystream(const uint8_t* key, size_t key_len, uint8_t* out, size_t n);

@@ -158,18 +158,21 @@ def test_tx_assemble_host_vs_sender_loop(gpu, d, p, max_len, G, key, pinned, rou
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("route", ["copy", "mapped"])
-def test_tx_assemble_host_many_chunks_matches_device_path(gpu, route):
+@pytest.mark.parametrize("route,copy_queue", [("copy", False), ("mapped", False), ("copy", True)])
+def test_tx_assemble_host_many_chunks_matches_device_path(gpu, route, copy_queue):
     """A batch past tx_assemble_host's chunk cap (32 chunks per call; the
     chunks grow with the batch): 3,400 (32,8) groups of up to 9,006-B packets
     in pinned memory, against the device-resident tx_assemble (itself checked
     against the sender loop above) -- every wire packet within its length,
     the wire lengths and the statuses, header-only and bad groups included.
-    Two calls on the context, each checked."""
+    Two calls on the context, each checked; copy_queue: the first two with the
+    low-priority copy stream (ugo_fec_set_host_copy_queue), a third after
+    switching it off again."""
     d, p, max_len, G = 32, 8, 9006, 3400
     n, slot = d + p, (max_len + 15) // 16 * 16
     enc = fec.New(d, p)
     enc.set_tx_host_route(route)
+    enc.set_host_copy_queue(copy_queue)
     gen = torch.Generator(device="cuda").manual_seed(77)
     dp = torch.randint(0, 256, (G * d, slot), dtype=torch.uint8, device="cuda", generator=gen)
     ln = torch.randint(6, max_len + 1, (G * d,), dtype=torch.int32, device="cuda", generator=gen)
@@ -199,7 +202,9 @@ def test_tx_assemble_host_many_chunks_matches_device_path(gpu, route):
         hl[:] = ln.cpu().numpy().view(np.uint16)
         want_l = dwl.cpu().numpy().view(np.uint16)
         keep = torch.arange(slot, device="cuda")[None, :] < dwl.to(torch.int32).view(-1, 1)
-        for call in range(2):
+        for call in range(3 if copy_queue else 2):
+            if call == 2:
+                enc.set_host_copy_queue(False)  # the stream is replaced between calls
             hst[:] = -1
             hwl[:] = 0
             hw[:, :64] = 0xAB

@@ -336,6 +336,19 @@ void host_rx_tx_paths(bool pinned) {
     }
   }
   EXPECT(ugo_fec_set_tx_host_route(ctx, 0) == UGO_FEC_OK);
+  // the low-priority copy stream, switched on between calls (the stream is replaced): same packets
+  EXPECT(ugo_fec_set_host_copy_queue(ctx, 2) == UGO_FEC_ERR_INVALID_ARG);
+  EXPECT(ugo_fec_set_host_copy_queue(ctx, 1) == UGO_FEC_OK);
+  {
+    uint8_t* wire3 = buf(G * n * slot);
+    auto* wlens3 = reinterpret_cast<uint16_t*>(buf(G * n * 2));
+    EXPECT(ugo_fec_tx_assemble_host(ctx, pkts, slot, lens, G, 0, pad, max_len, wire3, slot, wlens3, nullptr) ==
+           UGO_FEC_OK);
+    for (size_t i = 0; i < G * n; ++i) {
+      EXPECT(wlens3[i] == wlens[i]);
+      EXPECT(std::memcmp(wire3 + i * slot, wire + i * slot, wlens[i]) == 0);
+    }
+  }
   // the ring: every group loses data packet g % d, group 7 loses 4 packets (below d shards)
   std::vector<size_t> keep;
   for (size_t g = 0; g < G; ++g)

@@ -43,6 +43,8 @@ def main():
         st.synchronize()
         dummies.append(st)
     enc = fec.Encoder(d, p, device=0)
+    if os.environ.get("HAB_COPYQ"):  # 1: the low-priority copy stream (ugo_fec_set_host_copy_queue)
+        enc.set_host_copy_queue(os.environ["HAB_COPYQ"] == "1")
     if os.environ.get("HAB_ROUTE"):  # copy / mapped: tx_assemble_host's wire route (default copy)
         enc.set_tx_host_route(os.environ["HAB_ROUTE"])
     gen = torch.Generator(device=dev).manual_seed(11)

@@ -1,0 +1,53 @@
+"""bench.py's service_interference leg on its own (a resident per-call service
+block against the bench step and a pinned-host encode on the same GPU), for
+A/B runs of library builds (UGO_FEC_LIB).  SVI_TX=1: one host TX call first, on
+a context left open through the samples.  Prints one JSON line.  Not product
+code.
+
+  python3 tools/svc_interference.py LABEL
+"""
+import json
+import os
+import sys
+import types
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def main():
+    import numpy as np
+
+    import bench
+    from ugo_amd import fec
+
+    label = sys.argv[1] if len(sys.argv) > 1 else "?"
+    args = types.SimpleNamespace(seed=0x5EED)
+    enc = fec.New(10, 3, device=0)
+    raw = fec.host_alloc(64 * 13 * 1472)
+    keep = []
+    if os.environ.get("SVI_TX"):  # a host TX call first, on a context that stays open (as an application's)
+        G, d, n, slot = 4096, 10, 13, 1488
+        tx = fec.New(d, 3, device=0)
+        pk = fec.host_alloc(G * d * slot).reshape(G * d, slot)
+        ln = fec.host_alloc(G * d * 2).view(np.uint16)
+        wire = fec.host_alloc(G * n * slot).reshape(G * n, slot)
+        wl = fec.host_alloc(G * n * 2).view(np.uint16)
+        pk[:] = 1
+        ln[:] = 1476
+        tx.tx_assemble_host(pk, ln, wire, wl, max_len=1476)
+        keep = [tx, pk, ln, wire, wl]
+    try:
+        res = bench.service_interference(args, 0, enc, raw)
+    finally:
+        fec.host_free(raw)
+        enc.close()
+        if keep:
+            for b in keep[1:]:
+                fec.host_free(b.reshape(-1).view(np.uint8))
+            keep[0].close()
+    res["label"] = label
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

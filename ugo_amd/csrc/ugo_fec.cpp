@@ -100,6 +100,7 @@ struct ugo_fec {
   // (klauspost caches its inversions per pattern the same way)
   std::unordered_map<std::string, std::vector<uint8_t>> wide_cache;
   int tx_route = 0;  // host TX wire route (ugo_fec_set_tx_host_route): 0 D2H copy, 1 mapped write
+  bool host_copy_queue = false;  // ugo_fec_set_host_copy_queue: streams[1] from the low-priority class
   size_t stage_groups = 0;  // groups per staging buffer
   size_t stage_pitch = 0;
   // launch timing (ugo_fec_timing_begin/end)
@@ -543,20 +544,20 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
 }
 
 // The host paths' streams: 0 kernels (and host TX's D2H copies), 1 H2D copies,
-// 2 the other RX copy stream / the staged paths' third stream.  HIP maps a
-// process's streams onto a small pool of hardware queues per priority class
-// (GPU_MAX_HW_QUEUES, 4 here) in creation order, and a queue processes its
-// packets in order: when host TX's H2D stream shared a queue with its D2H
-// stream, each D2H copy waited behind the next chunk's H2D dependency and the
-// two copy directions ran one after the other -- 40.5 ms instead of 26.6 for
-// 65,536 (10+3) groups, depending on how many streams the process had made
-// before (profiles/r5/host_tx_route_ab.md).  Stream 1 comes from the
-// low-priority class, a pool of its own (its packets are copies and event
-// waits, which priority does not slow).  A full CU mask (a queue per stream)
-// and low / normal / high classes measured the same, but cost a queue per
-// context or share the per-call service's class.
-hipError_t create_stream(int i, hipStream_t* s) {
-  if (i == 1) {
+// 2 the staged paths' third stream.  HIP maps a process's streams onto a small
+// pool of hardware queues per priority class (GPU_MAX_HW_QUEUES, 4 here), and a
+// queue processes its packets in order.  When host TX's H2D stream shared a
+// queue with the stream its D2H copies ran on, each D2H copy waited behind the
+// next chunk's H2D dependency and the two copy directions ran one after the
+// other: 40.5 ms instead of 26.6 for 65,536 (10+3) groups, depending on the
+// streams the process had made before (profiles/r5/host_tx_route_ab.md).  With
+// ugo_fec_set_host_copy_queue, stream 1 comes from the low-priority class, a
+// pool of its own: 26.5-26.6 ms in every history tried.  It is not the default:
+// the extra hardware queue cost concurrent device work 33-39 % in the bench's
+// process while a per-call service block was resident (1-4 % without it), and
+// with the normal class the host TX call ran 26.5 ms in five of six histories.
+hipError_t create_stream(const ugo_fec* c, int i, hipStream_t* s) {
+  if (i == 1 && c->host_copy_queue) {
     int least = 0, greatest = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return hipErrorInvalidValue;
     return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
@@ -566,7 +567,7 @@ hipError_t create_stream(int i, hipStream_t* s) {
 
 int ensure_streams(ugo_fec* c) {
   for (int i = 0; i < kStreams; ++i)
-    if (!c->streams[i] && create_stream(i, &c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (!c->streams[i] && create_stream(c, i, &c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
   return UGO_FEC_OK;
 }
 
@@ -584,7 +585,7 @@ int ensure_stage(ugo_fec* c, size_t pitch) {
   }
   c->stage_groups = 0;
   for (int i = 0; i < kStreams; ++i) {
-    if (!c->streams[i] && create_stream(i, &c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
+    if (!c->streams[i] && create_stream(c, i, &c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_stage[i], want * gbytes + 16) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_mask[i], want * mask_words(c) * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_status[i], want) != hipSuccess) return UGO_FEC_ERR_HIP;
@@ -1724,9 +1725,9 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   for (size_t k = 0; k < nchunks; ++k) {
     for (; next < nchunks && next < k + kRxStages; ++next) {
       const int b = static_cast<int>(next % kRxStages);
-      // every ring copy on streams[1] (its own hardware queue, create_stream): 23.1-23.2 ms over six
-      // process histories, against 22.3-25.0 alternating streams 1 and 2
-      // (profiles/r5/host_tx_route/host_rx_copy_streams_*.jsonl)
+      // every ring copy on streams[1]: 23.4-24.2 ms over six process histories (23.1-23.2 with the
+      // low-priority copy queue), against 22.3-25.0 alternating streams 1 and 2
+      // (profiles/r5/host_tx_route/host_rx_copy_streams_*.jsonl, host_tx_normal_2stream.jsonl)
       const hipStream_t cs = c->streams[1];
       const size_t p0 = next * cpk, m = std::min(cpk, npk - p0);
       if (hipStreamWaitEvent(cs, ev[kRxStages + b], 0) != hipSuccess ||
@@ -1769,11 +1770,11 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
 }
 
 // The TX path from host memory to host memory: groups in chunks through
-// kTxStages device stages -- the data packets' H2D on streams[1] (its own
-// hardware queue, create_stream), tx_assemble and then the wire packets' D2H on
-// streams[0] -- joined by events, so the two copy directions run at once (a
-// third stream for the D2H copies ran 25.9-28.6 ms over six process histories,
-// the D2H behind the kernel on its stream 26.5-26.6 in all six,
+// kTxStages device stages -- the data packets' H2D on streams[1], tx_assemble
+// and then the wire packets' D2H on streams[0] -- joined by events, so the two
+// copy directions run at once (with the low-priority copy queue, a third stream
+// for the D2H copies ran 25.9-28.6 ms over six process histories, the D2H
+// behind the kernel on its stream 26.5-26.6 in all six,
 // profiles/r5/host_tx_route/host_tx_d2h_stream.jsonl); the lengths go in with
 // one copy ahead of the first chunk and the wire lengths and statuses come back
 // with one copy after the last (a
@@ -1918,6 +1919,21 @@ int ugo_fec_tx_assemble_host(ugo_fec* c, const uint8_t* pkts, size_t slot_in, co
     return UGO_FEC_ERR_HIP;
   for (int i = 0; i < kStreams; ++i)
     if (hipStreamSynchronize(c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
+  return UGO_FEC_OK;
+}
+
+int ugo_fec_set_host_copy_queue(ugo_fec* c, int on) {
+  if (!c || (on != 0 && on != 1)) return UGO_FEC_ERR_INVALID_ARG;
+  if (c->poisoned) return UGO_FEC_ERR_HIP;
+  if (c->host_copy_queue == (on == 1)) return UGO_FEC_OK;
+  DeviceGuard g(c->device);
+  if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
+  if (c->streams[1]) {  // made again, from the other class, at the next host-path call
+    if (hipStreamSynchronize(c->streams[1]) != hipSuccess || hipStreamDestroy(c->streams[1]) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
+    c->streams[1] = nullptr;
+  }
+  c->host_copy_queue = on == 1;
   return UGO_FEC_OK;
 }
 

@@ -147,6 +147,7 @@ def load_library(path: str = LIB_PATH):
                                             ctypes.POINTER(sz)]
     lib.ugo_fec_tx_assemble_host.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp]
     lib.ugo_fec_set_tx_host_route.argtypes = [vp, ctypes.c_int]
+    lib.ugo_fec_set_host_copy_queue.argtypes = [vp, ctypes.c_int]
     lib.ugo_fec_reconstruct_list.argtypes = [vp, vp, vp, sz, vp, vp, sz, sz, sz, sz, vp, sz, sz, u, vp, vp]
     lib.ugo_fec_recover_data.argtypes = [vp, vp, vp, sz, sz, sz, sz, vp, sz, sz, vp, vp, vp]
     lib.ugo_fec_device_address.argtypes = [vp, vp, ctypes.POINTER(vp)]
@@ -394,6 +395,11 @@ class Encoder:
             self._h, pkts.ctypes.data, pkts.shape[1], lens.ctypes.data, G, first_seq,
             None if padb is None else padb.ctypes.data, max_len, wire.ctypes.data, wire.shape[1],
             wire_lens.ctypes.data, None if status is None else status.ctypes.data))
+
+    def set_host_copy_queue(self, on: bool):
+        """ugo_fec_set_host_copy_queue: the host paths' H2D copies on a
+        low-priority stream (a hardware-queue pool of its own)."""
+        _raise(load_library().ugo_fec_set_host_copy_queue(self._h, 1 if on else 0))
 
     def set_tx_host_route(self, route: str):
         """ugo_fec_set_tx_host_route: tx_assemble_host's wire packets by D2H
