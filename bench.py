@@ -981,8 +981,8 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             "rep_ms": [round(t * 1e3, 2) for t in tx_reps],
             "verify_vs_device_path": ok,
             "path": "pinned data packets -> H2D -> tx_assemble -> D2H of the wire packets, group chunks through "
-                    "4 device stages, the H2D copies on a low-priority stream (a hardware queue apart), each "
-                    "chunk's kernel and D2H on a second stream, joined by events"}
+                    "4 device stages, the H2D copies on one stream, each chunk's kernel and D2H on a second, "
+                    "joined by events (default stream classes)"}
         tb.clear()
         if st["err"]:
             res["rxtx_error_rank0"] = st["err"]
