@@ -53,6 +53,9 @@ def test_null_arguments_rejected():
     # reconstruct_into: no context, then an empty batch (a no-op whatever the pointers)
     assert lib.ugo_fec_reconstruct_into(None, None, None, 1, 16, 16, 208, None, 16, 48, 0, None, None) == 6
     assert lib.ugo_fec_reconstruct_into(None, None, None, 0, 16, 16, 208, None, 16, 48, 0, None, None) == 6
+    # the host TX route and the host paths' copy queue: no context
+    assert lib.ugo_fec_set_tx_host_route(None, 0) == 6
+    assert lib.ugo_fec_set_host_copy_queue(None, 1) == 6
 
 
 def test_missing_library_fails_loudly(tmp_path):
