@@ -1,7 +1,8 @@
 """bench.py's service_interference leg on its own (a resident per-call service
 block against the bench step and a pinned-host encode on the same GPU), for
 A/B runs of library builds (UGO_FEC_LIB).  SVI_TX=1: one host TX call first, on
-a context left open through the samples.  Prints one JSON line.  Not product
+a context left open through the samples; SVI_EXTRA=k,prio: k more torch
+streams of that priority alive through the samples.  Prints one JSON line.  Not product
 code.
 
   python3 tools/svc_interference.py LABEL
@@ -25,6 +26,19 @@ def main():
     enc = fec.New(10, 3, device=0)
     raw = fec.host_alloc(64 * 13 * 1472)
     keep = []
+    # SVI_EXTRA=k,prio: k torch streams of that priority (0 normal, -1 high), each used once, alive
+    # through the samples (more hardware queues in the process)
+    extra = []
+    if os.environ.get("SVI_EXTRA"):
+        import torch
+
+        k, prio = (int(x) for x in os.environ["SVI_EXTRA"].split(","))
+        for _ in range(k):
+            st = torch.cuda.Stream(device=0, priority=prio)
+            with torch.cuda.stream(st):
+                torch.ones(1024, device="cuda").sum()
+            st.synchronize()
+            extra.append(st)
     if os.environ.get("SVI_TX"):  # a host TX call first, on a context that stays open (as an application's)
         G, d, n, slot = 4096, 10, 13, 1488
         tx = fec.New(d, 3, device=0)
