@@ -408,7 +408,10 @@ static inline uint32_t rx_blocks(const RxArgs& a) {
 // the call -- and then costs its grid's dispatch: 1024 grid-stride blocks
 // instead of a full grid take 4 us off the call (profiles/r5/rxgather/
 // r5_gated_*; with duplicates the re-place is ~10% slower on the smaller grid).
-constexpr uint64_t kRxGatedBlocks = 1024;
+#ifndef UGO_RX_GATED_BLOCKS
+#define UGO_RX_GATED_BLOCKS 1024
+#endif
+constexpr uint64_t kRxGatedBlocks = UGO_RX_GATED_BLOCKS;
 
 hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s) {
   uint64_t blocks = (a.npk + 255) / 256;
