@@ -92,6 +92,25 @@ __global__ __launch_bounds__(256) void k_pat_scatter1(const uint8_t* src, uint8_
   const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i * 1488 + 16 * m));
   __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + doff[i] + 16 * m));
 }
+// P2r: P2 with what an index-driven RX lane would add -- the payload at byte 6 of the slot (two
+// aligned loads, the second mostly an L1/L2 hit, funnel-shifted) and the keystream chunk XORed
+// (a load per lane from a 1488-B pad, L1/L2-resident); the destination from the per-packet index
+__global__ __launch_bounds__(256) void k_pat_scatter1r(const uint8_t* src, uint8_t* dst, const uint64_t* doff,
+                                                       const uint8_t* pad, uint64_t npk) {
+  const uint64_t c = blockIdx.x * 256ull + threadIdx.x;
+  if (c >= npk * 92) return;
+  const uint64_t i = c / 92, m = c - i * 92;
+  const u32x4* sp = reinterpret_cast<const u32x4*>(src + i * 1488 + 16 * m);
+  const u32x4 a = __builtin_nontemporal_load(sp), b = __builtin_nontemporal_load(sp + 1);
+  const u32x4 k0 = *reinterpret_cast<const u32x4*>(pad + 16 * m), k1 = *reinterpret_cast<const u32x4*>(pad + 16 * m + 16);
+  const u32x4 x = a ^ k0, y = b ^ k1;
+  u32x4 v;  // bytes [6, 22) of the 32 loaded
+  v.x = __builtin_amdgcn_alignbyte(x.y, x.x, 6);
+  v.y = __builtin_amdgcn_alignbyte(x.z, x.y, 6);
+  v.z = __builtin_amdgcn_alignbyte(x.w, x.z, 6);
+  v.w = __builtin_amdgcn_alignbyte(y.x, x.w, 6);
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + doff[i] + 16 * m));
+}
 // P3 (DENSE=false) / P4 (DENSE=true): production structure -- half a wave per packet, 3 chunks per
 // lane loaded first, grid-stride over packet pairs, 2048 blocks -- to the scattered / dense destination
 template <bool DENSE>
@@ -497,6 +516,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_sidx, G * n * 4));
   CK(hipMemcpy(d_doff, doff.data(), npk * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_sidx, sidx.data(), G * n * 4, hipMemcpyHostToDevice));
+  uint8_t* d_padr;  // P2r's keystream (contents irrelevant to the timing)
+  CK(hipMalloc(&d_padr, 1504));
+  CK(hipMemset(d_padr, 0x5a, 1504));
   struct T {
     std::string name;
     std::function<void()> fn;
@@ -519,6 +541,10 @@ int main(int argc, char** argv) {
   ts.push_back({"PATTERN P2 scatter to planar, one chunk per thread, full grid", [&] {
                   const int k = cnt++ % 3;
                   k_pat_scatter1<<<(npk * 92 + 255) / 256, 256>>>(rot[k].wire, rot[k].shards, d_doff, npk);
+                }, {}});
+  ts.push_back({"PATTERN P2r: P2 + payload at byte 6 (two loads, funnel shift) + keystream XOR per lane", [&] {
+                  const int k = cnt++ % 3;
+                  k_pat_scatter1r<<<(npk * 92 + 255) / 256, 256>>>(rot[k].wire, rot[k].shards, d_doff, d_padr, npk);
                 }, {}});
   ts.push_back({"PATTERN P3 scatter to planar, half-wave per packet, grid-stride 2048", [&] {
                   const int k = cnt++ % 3;
