@@ -786,8 +786,9 @@ def pcie_ceiling(dev, world, nbytes=1 << 30, reps=5):
         out = {"h2d_GBps": round(nbytes / (tmax[0] * 1e-3) / 1e9, 2),
                "d2h_GBps": round(nbytes / (tmax[1] * 1e-3) / 1e9, 2),
                "bidirectional_GBps": round(2 * nbytes / (tmax[2] * 1e-3) / 1e9, 2),
-               "note": f"{nbytes >> 20} MiB pinned <-> device per copy (hipMemcpyAsync, one stream per direction), "
-                       "every rank at once, max over ranks, per GPU"}
+               "note": f"{nbytes >> 20} MiB pinned <-> device per copy (hipMemcpyAsync, one stream per direction; "
+                       "two-way: the best over the ordered pairs of four streams), every rank at once, max over "
+                       "ranks, per GPU"}
         del dbuf
         return out
     finally:

@@ -332,14 +332,17 @@ int ugo_probe_nt_copy(const uint8_t* const* srcs, uint8_t* const* dsts, int nbuf
 // The PCIe ceiling with the copy calls the host paths use (hipMemcpyAsync of
 // pinned host <-> device): ms_out[0] = one H2D of `bytes`, [1] one D2H, [2]
 // both at once on two streams (wall time from the first enqueue to both done),
-// medians over reps.  Whether two streams' copies run on different DMA engines
-// depends on the streams (the first probe, one fixed pair of fresh streams,
-// read 57.7 GB/s two-way in one run and 97.3 in another): [2] is the best of
-// the three pairs of three streams.
+// medians over reps.  Two streams' copies overlap only when HIP has put the
+// streams on different hardware queues, which depends on the streams the
+// process made before (one fixed pair of fresh streams read 57.7 GB/s two-way
+// in one run and 97.3 in another; three pairs of three streams 72.8 in one
+// process): [2] is the best over every ordered pair of four
+// streams, at least two of which sit on different queues of the pool of four.
 int ugo_probe_pcie(uint8_t* host_a, uint8_t* host_b, uint8_t* dev_a, uint8_t* dev_b, size_t bytes, int reps,
                    float* ms_out) {
   if (!host_a || !host_b || !dev_a || !dev_b || !ms_out || reps <= 0 || bytes == 0) return 2;
-  hipStream_t s[3] = {};
+  constexpr int kS = 4;
+  hipStream_t s[kS] = {};
   int rc = 0;
   for (auto& x : s)
     if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) rc = 1;
@@ -360,11 +363,13 @@ int ugo_probe_pcie(uint8_t* host_a, uint8_t* host_b, uint8_t* dev_a, uint8_t* de
   if (!rc) run(0, s[0], s[0], &ms_out[0]);
   if (!rc) run(1, s[0], s[0], &ms_out[1]);
   float best = 0.f;
-  for (int k = 0; k < 3 && !rc; ++k) {
-    float v = 0.f;
-    run(2, s[k], s[(k + 1) % 3], &v);
-    if (!rc && (best == 0.f || v < best)) best = v;
-  }
+  for (int i = 0; i < kS && !rc; ++i)
+    for (int j = 0; j < kS && !rc; ++j) {
+      if (i == j) continue;
+      float v = 0.f;
+      run(2, s[i], s[j], &v);
+      if (!rc && (best == 0.f || v < best)) best = v;
+    }
   ms_out[2] = best;
   for (auto& x : s)
     if (x) (void)hipStreamDestroy(x);
