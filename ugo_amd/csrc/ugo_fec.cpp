@@ -100,7 +100,10 @@ struct ugo_fec {
   // (klauspost caches its inversions per pattern the same way)
   std::unordered_map<std::string, std::vector<uint8_t>> wide_cache;
   int tx_route = 0;  // host TX wire route (ugo_fec_set_tx_host_route): 0 D2H copy, 1 mapped write
-  bool host_copy_queue = false;  // ugo_fec_set_host_copy_queue: streams[1] from the low-priority class
+#ifndef UGO_COPY_QUEUE_DEFAULT
+#define UGO_COPY_QUEUE_DEFAULT 0
+#endif
+  bool host_copy_queue = UGO_COPY_QUEUE_DEFAULT != 0;  // ugo_fec_set_host_copy_queue: streams[1] low priority
   size_t stage_groups = 0;  // groups per staging buffer
   size_t stage_pitch = 0;
   // launch timing (ugo_fec_timing_begin/end)
