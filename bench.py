@@ -927,8 +927,9 @@ def host_rxtx_cases(args, dev_index, rank, world, reps):
             "groups_per_rank": G, "packets_per_rank": npk, "loss": 0.05, "rc4": True, "recovered_shards_rank0": nrec,
             "rx_ms": round(t_rx * 1e3, 3), "wire_GBps": round(wire_bytes / t_rx / 1e9, 2),
             "pcie_GBps_per_gpu": round(pcie / t_rx / 1e9, 2), "rank0_alone_ms": round(t_rx_mine * 1e3, 3),
-            "pcie_bound_ms": _r3(pcie_bound_ms(res.get("pcie_ceiling"), npk * (slot + 2), nrec * S)),
-            "of_pcie_bound": _r3(pcie_bound_ms(res.get("pcie_ceiling"), npk * (slot + 2), nrec * S), t_rx * 1e3),
+            "pcie_bound_ms": _r3(pcie_bound_ms(res.get("pcie_ceiling"), npk * (slot + 2), nrec * S, False)),
+            "of_pcie_bound": _r3(pcie_bound_ms(res.get("pcie_ceiling"), npk * (slot + 2), nrec * S, False),
+                                 t_rx * 1e3),
             "rep_ms": [round(t * 1e3, 2) for t in rx_reps],
             "zero_copy_ring_ms": None if t_zc is None else round(t_zc * 1e3, 3),
             "zero_copy_note": "rx_assemble reading the pinned ring in place, then the public lossy list + "
@@ -1002,15 +1003,19 @@ def _r3(x, div=None):
     return round(x / div if div else x, 3)
 
 
-def pcie_bound_ms(ceiling, h2d_bytes, d2h_bytes):
+def pcie_bound_ms(ceiling, h2d_bytes, d2h_bytes, overlap=True):
     """The least time the measured link allows for h2d_bytes in and d2h_bytes
-    out, both directions streaming at once: each direction at half the measured
-    two-way rate while both run, then the longer one alone at its one-way rate.
-    None without a ceiling."""
+    out: with overlap, both directions streaming at once -- each at half the
+    measured two-way rate while both run, then the longer one alone at its
+    one-way rate; without (the output depends on all the input, as RX's
+    recovered rows do), one after the other at the one-way rates.  None
+    without a ceiling."""
     try:
         h2d, d2h, both = ceiling["h2d_GBps"] * 1e9, ceiling["d2h_GBps"] * 1e9, ceiling["bidirectional_GBps"] * 1e9
     except (KeyError, TypeError):
         return None
+    if not overlap:
+        return (h2d_bytes / h2d + d2h_bytes / d2h) * 1e3
     if not d2h_bytes:
         return h2d_bytes / h2d * 1e3
     if not h2d_bytes:
