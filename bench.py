@@ -1336,6 +1336,57 @@ def lost_and_recoverable(pm, d, n):
     return ed, have >= d
 
 
+def payload_layout_case(enc, rings, lens, pad, fbats, fpres, flsts, fcnts, flouts, G, n, p, S, FS, ppitch,
+                        kernel_ms, reps):
+    """The RX ring into the payload layout (ugo_fec_rx_assemble: [n][G][ppitch],
+    the payload realigned to column 0) and its list recovery: checked equal to
+    the frame layout's presence masks, lossy list and recovered payload columns
+    (fpres / flsts / fcnts / flouts of the frame run on rings[0]), then timed.
+    Its batches are views of the frame batches' storage (fbats, overwritten):
+    placement time depends on which physical pages back a batch (up to 15 %
+    between allocations of one process, tools/rx_frames_ab.py same), so both
+    layouts are timed on the same pages."""
+    import torch
+
+    from ugo_amd import fec
+
+    dev = rings[0].device
+    bats = [fb.view(-1)[:n * G * ppitch].view(n, G, ppitch) for fb in fbats]
+    pres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
+    lsts = [torch.empty(G, dtype=torch.int32, device=dev) for _ in range(2)]
+    cnts = [torch.empty(1, dtype=torch.int32, device=dev) for _ in range(2)]
+    outs = [torch.empty((G, p, ppitch), dtype=torch.uint8, device=dev) for _ in range(2)]
+
+    def rx(r):
+        i = r % 2
+        pres[i].zero_()
+        enc.rx_assemble(rings[i], lens, bats[i], pres[i], shard_size=S, pad=pad)
+
+    def rec_list(r):
+        i = r % 2
+        enc.lossy_groups(pres[i], data_only=True, out=lsts[i], count=cnts[i])
+        enc.reconstruct_list(bats[i], pres[i], lsts[i], cnts[i], outs[i], shard_size=S, data_only=True)
+
+    for r in range(4):
+        rx(r)
+        rec_list(r)
+    torch.cuda.synchronize()
+    k = int(cnts[0].item())
+    ok = k == int(fcnts[0].item()) and bool(torch.equal(pres[0], fpres[0])) and bool(
+        torch.equal(lsts[0][:k], flsts[0][:k]))
+    if ok:  # each entry's recovered rows (slots past its erasure count are not written by either)
+        ed, okg = lost_and_recoverable(pres[0][lsts[0][:k].long()], n - p, n)
+        for i in range(p):
+            sel = (ed > i) & okg
+            ok = ok and bool(torch.equal(outs[0][:k][sel, i, :S], flouts[0][:k][sel, i, 6:FS]))
+    rx_k = kernel_ms(rx, fec.KERNEL_IDS["rx_assemble"], reps)
+    for r in range(2):
+        rx(r)
+    rec_k = kernel_ms(rec_list, fec.KERNEL_IDS["reconstruct"], reps)
+    return {"rows": f"[{n}][G][{ppitch}] payload at column 0 (rx_assemble)", "rx_assemble_ms": round(rx_k, 4),
+            "reconstruct_list_ms": round(rec_k, 4), "verify_eq_frames": ok}
+
+
 def rx_tx_leg(args, dev_index, reps=12):
     """The §8f kernels on the driver's clock, on every rank
     (rank 0 reports its own leg plus the max over ranks of
@@ -1345,8 +1396,12 @@ def rx_tx_leg(args, dev_index, reps=12):
       * rx_assemble (ugo/conn.go:387-406 decrypt, ugo/fec.go:78-89 decode,
         :107-175 grouping / dedupe / placement): a ring of 65,536 (10+3) groups
         minus 5% uniform loss, 1476-B packets in 1488-B slots, RC4, into a
-        planar [13][G][1472] batch (S = 1470); arrival in seqid order (what a
-        UDP flow mostly delivers) and shuffled (worst case);
+        planar batch in the frame layout (ugo_fec_rx_assemble_frames, the one
+        the host RX path uses: [13][G][1536], each row the decrypted packet,
+        payload S = 1470 at column 6; the recovery below runs on the 1476-B frame
+        window), with the payload layout ([13][G][1472], realigned payload at
+        column 0) timed beside it (`payload_layout`); arrival in seqid order
+        (what a UDP flow mostly delivers) and shuffled (worst case);
       * reconstruct_into, data only, of the lossy groups of that batch
         (input's Reconstruct, ugo/fec.go:196-207), over every group, and its
         list form (lossy_groups + reconstruct_list: only the lossy groups,
@@ -1366,7 +1421,8 @@ def rx_tx_leg(args, dev_index, reps=12):
 
     from ugo_amd import fec
 
-    d, p, n, S, pitch, slot = 10, 3, 13, 1470, 1472, 1488
+    d, p, n, S, slot = 10, 3, 13, 1470, 1488
+    FS, pitch, ppitch = S + 6, 1536, 1472  # frame rows (64-B pitch) / the payload layout's rows
     G = 65536
     dev = torch.device("cuda", dev_index)
     stream = torch.cuda.current_stream(dev)
@@ -1422,11 +1478,11 @@ def rx_tx_leg(args, dev_index, reps=12):
         def rx(r):
             i = r % 2
             pres[i].zero_()
-            enc.rx_assemble(rings[i], lens, bats[i], pres[i], shard_size=S, pad=pad, stats=st)
+            enc.rx_assemble(rings[i], lens, bats[i], pres[i], shard_size=S, pad=pad, stats=st, frames=True)
 
         def rec(r):
             i = r % 2
-            enc.reconstruct_into(bats[i], pres[i], outs[i], shard_size=S, data_only=True, shard_major=True)
+            enc.reconstruct_into(bats[i], pres[i], outs[i], shard_size=FS, data_only=True, shard_major=True)
 
         for r in range(4):
             rx(r)
@@ -1438,8 +1494,8 @@ def rx_tx_leg(args, dev_index, reps=12):
         # spot check of the placement: 4,096 packets' payloads, decrypted, in their rows
         pick = torch.randint(0, npk, (4096,), device=dev, generator=gen)
         sq = seq[pick]
-        want = rings[0][pick, 6:6 + S] ^ pad[6:6 + S]
-        got = bats[0][sq % n, sq // n, :S]
+        want = rings[0][pick, :FS] ^ pad[:FS]
+        got = bats[0][sq % n, sq // n, :FS]
         ok = stats == [npk, 0, 0, 0, 0] and bool(torch.equal(got, want))
         rx_k = kernel_ms(rx, fec.KERNEL_IDS["rx_assemble"], reps)
         rx_w = wall_ms(rx, reps)
@@ -1462,7 +1518,7 @@ def rx_tx_leg(args, dev_index, reps=12):
         def rec_list(r):
             i = r % 2
             enc.lossy_groups(pres[i], data_only=True, out=lsts[i], count=cnts[i])
-            enc.reconstruct_list(bats[i], pres[i], lsts[i], cnts[i], louts[i], shard_size=S, data_only=True)
+            enc.reconstruct_list(bats[i], pres[i], lsts[i], cnts[i], louts[i], shard_size=FS, data_only=True)
 
         for r in range(4):
             rx(r)
@@ -1476,7 +1532,7 @@ def rx_tx_leg(args, dev_index, reps=12):
         ok_list = k == int((lost_data > 0).sum())
         for i in range(p):
             sel = (ed > i) & okg  # groups below d shards: no output in either form
-            ok_list = ok_list and bool(torch.equal(louts[0][:k][sel, i, :S], outs[0][i, lg[sel], :S]))
+            ok_list = ok_list and bool(torch.equal(louts[0][:k][sel, i, 6:FS], outs[0][i, lg[sel], 6:FS]))
         rec_list_k = kernel_ms(rec_list, fec.KERNEL_IDS["reconstruct"], reps)
         # the same recovery as `input` returns it (ugo_fec_recover_data): the lost data shards
         # row-compact in `recovered` order with their places, the count on the device
@@ -1486,7 +1542,7 @@ def rx_tx_leg(args, dev_index, reps=12):
 
         def rec_data(r):
             i = r % 2
-            enc.recover_data(bats[i], pres[i], rdo[i], rdi[i], count=rdc[i], shard_size=S)
+            enc.recover_data(bats[i], pres[i], rdo[i], rdi[i], count=rdc[i], shard_size=FS)
 
         for r in range(2):
             rx(r)
@@ -1498,13 +1554,17 @@ def rx_tx_leg(args, dev_index, reps=12):
         jj, rr = torch.nonzero(lost, as_tuple=True)
         want_rows = louts[0][:k][torch.arange(p, device=dev)[None, :] < lost.sum(1)[:, None]]
         ok_rd = nr == int(jj.numel()) and bool(torch.equal(rdi[0][:nr].long(), lg[jj] * n + rr)) and bool(
-            torch.equal(rdo[0][:nr, :S], want_rows[:, :S]))
+            torch.equal(rdo[0][:nr, 6:FS], want_rows[:, 6:FS]))
         rec_data_k = kernel_ms(rec_data, fec.KERNEL_IDS["reconstruct"], reps)
         del rdo, rdi, rdc
+        # the payload layout (ugo_fec_rx_assemble: realigned payload rows at column 0) on the same rings,
+        # checked against the frame rows, then timed with its list recovery
+        pl = payload_layout_case(enc, rings, lens, pad, bats, pres, lsts, cnts, louts, G, n, p, S, FS, ppitch,
+                                 kernel_ms, reps)
         # ceilings: the compute-free twins of both forms on the same buffers (after the checks: wrong bytes)
-        twin_ms = probe_recover_twin_ms(bats, outs, pres, None, None, G, S, pitch, bats[0].stride(0),
+        twin_ms = probe_recover_twin_ms(bats, outs, pres, None, None, G, FS, pitch, bats[0].stride(0),
                                         outs[0].stride(0), outs[0].stride(1), reps, stream.cuda_stream)
-        ltwin_ms = probe_recover_twin_ms(bats, louts, pres, lsts, cnts, G, S, pitch, bats[0].stride(0),
+        ltwin_ms = probe_recover_twin_ms(bats, louts, pres, lsts, cnts, G, FS, pitch, bats[0].stride(0),
                                          louts[0].stride(1), louts[0].stride(0), reps, stream.cuda_stream)
         cb = min(rx_bytes // 2, rings[0].numel(), bats[0].numel())  # each copy stays inside both buffers
         copy_ms = probe_nt_copy_ms([rings[i].data_ptr() for i in range(2)], [bats[(i + 1) % 2].data_ptr()
@@ -1526,7 +1586,10 @@ def rx_tx_leg(args, dev_index, reps=12):
             "recovery_faster": "list" if rec_list_k < rec_k else "into", "verify_list_eq_into": ok_list,
             "recover_data_ms": round(rec_data_k, 4), "recover_data_frac": frac(rec_bytes, rec_data_k),
             "verify_recover_data": ok_rd,
-            "stats": stats, "verify_spot_4096": ok}
+            "stats": stats, "verify_spot_4096": ok,
+            "layout": "frames: [13][G][1536] rows = decrypted packets, payload at column 6 (rx_assemble_frames)",
+            "payload_layout": {**pl, "rx_frac": frac(rx_bytes, pl["rx_assemble_ms"]),
+                               "reconstruct_list_frac": frac(rec_bytes, pl["reconstruct_list_ms"])}}
         del rings, bats, pres, outs, lsts, cnts, louts
         torch.cuda.empty_cache()
 

@@ -57,7 +57,10 @@ extern "C" {
  *    [shard_size, round_up(shard_size, 16)) become zero; ugo_fec_lossy_groups,
  *    ugo_fec_reconstruct_list, ugo_fec_recover_data, ugo_fec_rx_recover_host,
  *    ugo_fec_tx_assemble_host. */
-#define UGO_FEC_ABI_VERSION 8
+/* 9: ugo_fec_rx_assemble_frames (frame rows: each placed row holds its
+ *    decrypted packet, payload at column 6); ugo_fec_rx_recover_host runs on
+ *    frame rows internally (same results). */
+#define UGO_FEC_ABI_VERSION 9
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
  * that ugo/fec.go logs and swallows (ugo/fec.go:60-63, 208-210, 239-241). */
@@ -325,6 +328,25 @@ int ugo_fec_rx_assemble(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, c
                         size_t npackets, const uint8_t* pad, uint64_t first_group, size_t groups,
                         uint8_t* shards, size_t shard_size, size_t row_stride, size_t group_stride,
                         uint64_t* present, uint32_t* stats, void* stream);
+
+/* ugo_fec_rx_assemble in the FRAME layout: row seqid % (d+p) of the group
+ * receives the decrypted packet itself -- packet bytes [0, min(len,
+ * shard_size + 6)), then zeros up to round_up(shard_size + 6, 16) -- instead
+ * of its payload: header (LE32 seqid, LE16 flag) in columns 0..5, payload
+ * data[6:] in columns 6 .. 6 + shard_size, i.e. the frame ugo's sender keeps
+ * (calcECC's window starts at offset 6, ugo/fec.go:228-236, ugo/conn.go:670).
+ * Every other rule (flags, window, first copy wins, presence, stats, scratch)
+ * as ugo_fec_rx_assemble; each row slot must span round_up(shard_size + 6, 16)
+ * bytes.  A packet chunk lands at the offset it was read from, so the kernel
+ * needs no byte realignment.  Recovery: run any reconstruct entry point on the
+ * frame batch with shard size shard_size + 6.  GF(2^8) columns are
+ * independent, so payload columns of a recovered row are bit-identical to the
+ * payload-layout result; its columns 0..5 are a combination of the survivors'
+ * headers and carry no meaning (a caller reads the shard from column 6). */
+int ugo_fec_rx_assemble_frames(ugo_fec* ctx, const uint8_t* wire, size_t slot_stride, const uint16_t* lens,
+                               size_t npackets, const uint8_t* pad, uint64_t first_group, size_t groups,
+                               uint8_t* shards, size_t shard_size, size_t row_stride, size_t group_stride,
+                               uint64_t* present, uint32_t* stats, void* stream);
 
 /* TX group assembly for a batch of `groups` outgoing groups (device or pinned
  * host memory, as for RX; stream-ordered, asynchronous) -- replaces the sender loop ugo/conn.go:643-685

@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_strerror():
     lib = fec.load_library()
-    assert lib.ugo_fec_abi_version() == 8
+    assert lib.ugo_fec_abi_version() == 9
     assert fec.strerror(3) == "too few shards given"
     assert fec.strerror(5) == "shard sizes do not match"
     assert fec.strerror(4) == "no shard data"

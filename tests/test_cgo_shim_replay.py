@@ -48,7 +48,7 @@ class GoShim:
 
     def __init__(self, data_shards, parity_shards):  # func New
         self.lib = lib = fec.load_library()
-        assert lib.ugo_fec_abi_version() == 8  # C.UGO_FEC_ABI_VERSION of the header
+        assert lib.ugo_fec_abi_version() == 9  # C.UGO_FEC_ABI_VERSION of the header
         ctx = ctypes.c_void_p()
         status_err(lib.ugo_fec_create(0, data_shards, parity_shards, ctypes.byref(ctx)))
         self.ctx, self.d, self.p = ctx, data_shards, parity_shards

@@ -32,14 +32,16 @@ def test_rc4_known_answers_and_product_keystream():
         assert fec.rc4_keystream(key, 1536) == rc4_ref.keystream(key, 1536)
 
 
-def _expected_placement(wire, G, n, S, pitch, first_group):
+def _expected_placement(wire, G, n, S, pitch, first_group, frames=False):
     """The batch ugo's per-packet path builds from `wire` in ring order
     (decrypted packets): FEC.decode (ugo/fec.go:78-89), the flag filter of
     Conn.handlePacket (ugo/conn.go:395), the group/slot of input
     (ugo/fec.go:145,175), and its dedupe -- a seqid already queued drops the
     new packet, so the first copy stays (ugo/fec.go:123-129).  Returns the
     group-major batch, presence masks and stats [accepted, bad flag, out of
-    window, too short, duplicate]."""
+    window, too short, duplicate].  frames: a row holds the decrypted packet's
+    first S + 6 bytes (ugo_fec_rx_assemble_frames: header, then the payload
+    at column 6) instead of its payload."""
     want = np.zeros((G, n, pitch), np.uint8)
     masks = np.zeros(G, np.uint64)
     stats = [0, 0, 0, 0, 0]
@@ -62,7 +64,7 @@ def _expected_placement(wire, G, n, S, pitch, first_group):
             continue
         seen.add(seq)
         stats[0] += 1
-        pl = w[6:6 + S]
+        pl = w[:S + 6] if frames else w[6:6 + S]
         want[g, seq % n, :] = 0
         want[g, seq % n, :len(pl)] = np.frombuffer(pl, np.uint8)
         masks[g] |= np.uint64(1 << (seq % n))
@@ -201,16 +203,107 @@ def test_rx_assemble_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_gro
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("encrypt,S,slot", [(True, 1470, 1488), (False, 1470, 1488), (True, 2000, 2016), (True, 3000, 3024)])
-def test_rx_assemble_first_copy_wins(gpu, encrypt, S, slot):
+@pytest.mark.parametrize("full_len,encrypt,first_group,ring", [(True, True, 0, "device"), (False, True, 5, "device"),
+                                                               (False, False, 0, "device"),
+                                                               (False, True, 5, "pinned")])
+def test_rx_assemble_frames_and_reconstruct_vs_oracle(gpu, full_len, encrypt, first_group, ring):
+    """ugo_fec_rx_assemble_frames: each placed row is the decrypted packet
+    (header in columns 0..5, payload from column 6, zeros to round_up(S + 6,
+    16)); the lossy list, the list reconstruct and the in-place reconstruct run
+    on the frame window (shard size S + 6), and the payload columns of every
+    recovered row equal the oracle's Reconstruct (rs_ref) of the payload batch
+    that fec_ref's decode + grouping builds -- the rows `input` appends to
+    `recovered` (ugo/fec.go:190-207)."""
+    d, p, n, S, slot = 10, 3, 13, 1470, 1488
+    FS, pitch = S + 6, 1488
+    total_groups, G = 300, 256
+    pk = _packets(total_groups, 41, full_len)
+    rng = np.random.default_rng(42 + first_group)
+    wire = []
+    for w in pk:
+        if rng.random() < 0.15:
+            continue  # lost
+        wire.append(w)
+        if rng.random() < 0.05:
+            wire.append(w)  # duplicate
+        if rng.random() < 0.02:
+            junk = bytearray(rng.integers(0, 256, 40, dtype=np.uint8).tobytes())
+            junk[4:6] = b"\x00\x00"
+            wire.append(bytes(junk))
+    wire.append(b"\x01\x02")  # too short
+    rng.shuffle(wire)
+    ks = rc4_ref.keystream(KEY, slot)
+    slots, lens = _ring([rc4_ref.xor_stream(KEY, w) if encrypt else w for w in wire], slot)
+    want_f, masks, stats = _expected_placement(wire, G, n, S, pitch, first_group, frames=True)
+    want_p, masks_p, _ = _expected_placement(wire, G, n, S, (S + 15) // 16 * 16, first_group)
+    assert np.array_equal(masks, masks_p)
+    exp = np.ascontiguousarray(want_p[:, :, :S])
+    _, exp_st = rs_ref.c_reconstruct(d, p, exp, masks, data_only=True)
+
+    codec = fec.New(d, p)
+    sh = torch.full((n, G, pitch), 0xAB, dtype=torch.uint8, device="cuda")
+    present = torch.zeros(G, dtype=torch.int64, device="cuda")
+    st = torch.zeros(5, dtype=torch.int32, device="cuda")
+    put = (lambda t: t.pin_memory()) if ring == "pinned" else (lambda t: t.cuda())  # noqa: E731
+    pad = put(torch.frombuffer(bytearray(ks), dtype=torch.uint8)) if encrypt else None
+    codec.rx_assemble(put(torch.from_numpy(slots)), put(torch.from_numpy(lens.view(np.int16))), sh, present,
+                      first_group=first_group, shard_size=S, pad=pad, stats=st, frames=True)
+    assert np.array_equal(present.cpu().numpy().view(np.uint64), masks)
+    assert st.cpu().tolist() == stats
+    raw = sh.cpu().numpy().transpose(1, 0, 2)
+    for g in range(G):
+        for r in range(n):
+            if (int(masks[g]) >> r) & 1:
+                assert np.array_equal(raw[g, r], want_f[g, r]), (g, r)  # the frame, zeros to the row's end
+            else:
+                assert (raw[g, r] == 0xAB).all(), (g, r)
+    lst, cnt = codec.lossy_groups(present, data_only=True)
+    k = int(cnt.item())
+    want_list = [g for g in range(G) if (~int(masks[g])) & ((1 << d) - 1)]
+    assert lst.cpu().numpy()[:k].tolist() == want_list
+    lout = torch.full((G, p, pitch), 0xA5, dtype=torch.uint8, device="cuda")
+    lst_st = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    codec.reconstruct_list(sh, present, lst, cnt, lout, shard_size=FS, data_only=True, status=lst_st)
+    lo, ls = lout.cpu().numpy(), lst_st.cpu().numpy()
+    nrec = 0
+    for j, g in enumerate(want_list):
+        assert ls[j] == exp_st[g], (j, g)
+        if exp_st[g] == 0:
+            erased = [r for r in range(d) if not (int(masks[g]) >> r) & 1]
+            for i, r in enumerate(erased):
+                assert np.array_equal(lo[j, i, 6:FS], exp[g, r]), (j, g, r)
+                if full_len:  # consistent codewords: the lost packet's payload itself
+                    assert bytes(lo[j, i, 6:FS]) == pk[(g + first_group) * n + r][6:], (j, g, r)
+                nrec += 1
+    assert nrec > 0
+    status = torch.full((G,), -1, dtype=torch.int8, device="cuda")
+    codec.reconstruct_batch(sh, present, shard_size=FS, data_only=True, status=status, shard_major=True)
+    assert np.array_equal(status.cpu().numpy(), exp_st)
+    got = sh.cpu().numpy().transpose(1, 0, 2)
+    for g in range(G):
+        m = int(masks[g])
+        for r in range(n):
+            if (m >> r) & 1:
+                assert np.array_equal(got[g, r], want_f[g, r]), (g, r)  # present rows never written
+            elif r < d and exp_st[g] == 0:
+                assert np.array_equal(got[g, r, 6:FS], exp[g, r]), (g, r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("encrypt,S,slot,frames", [(True, 1470, 1488, False), (False, 1470, 1488, False),
+                                                   (True, 2000, 2016, False), (True, 3000, 3024, False),
+                                                   (True, 1470, 1488, True), (True, 3000, 3024, True)])
+def test_rx_assemble_first_copy_wins(gpu, encrypt, S, slot, frames):
     """Repeated seqids with DIFFERENT payloads and lengths (a replayed or
     corrupted packet with a valid header): the first copy in ring order is the
     one placed, as ugo's input keeps the queued packet and drops the new one
     (ugo/fec.go:123-129).  Copies sit next to each other (same wave), a wave
     apart and far apart; two runs in one process are identical.  S = 3000 runs
-    the per-pass kernel (rows of more than 128 chunks)."""
+    the per-pass kernel (rows of more than 128 chunks); frames: the frame
+    layout (k_rx_frame_h, and k_rx_frame_scatter at S = 3000)."""
     d, p, n = 10, 3, 13
-    pitch = (S + 15) // 16 * 16
+    W = S + 6 if frames else S
+    pitch = (W + 15) // 16 * 16
     G = 512
     rng = np.random.default_rng(77)
     maxlen = min(S + 6, slot)
@@ -240,7 +333,7 @@ def test_rx_assemble_first_copy_wins(gpu, encrypt, S, slot):
     wire[100:100] = [hot[:6] + bytes(rng.integers(0, 256, len(hot) - 6, dtype=np.uint8)) for _ in range(8)]
     wire.insert(0, pkt(7 * n + 12, 0xF2))
     wire.append(pkt(7 * n + 12, 0xF2))  # last copy of the first packet's seqid: dropped
-    want, masks, stats = _expected_placement(wire, G, n, S, pitch, 0)
+    want, masks, stats = _expected_placement(wire, G, n, S, pitch, 0, frames)
     assert stats[4] > 50
 
     ks = rc4_ref.keystream(KEY, slot)
@@ -255,7 +348,7 @@ def test_rx_assemble_first_copy_wins(gpu, encrypt, S, slot):
         sh = torch.full((n, G, pitch), 0xAB, dtype=torch.uint8, device="cuda")
         present = torch.zeros(G, dtype=torch.int64, device="cuda")
         st = torch.zeros(5, dtype=torch.int32, device="cuda")
-        codec.rx_assemble(ring, tl, sh, present, shard_size=S, pad=pad, stats=st)
+        codec.rx_assemble(ring, tl, sh, present, shard_size=S, pad=pad, stats=st, frames=frames)
         runs.append((sh.cpu().numpy(), present.cpu().numpy().view(np.uint64), st.cpu().tolist()))
     for got, pres, st in runs:
         assert st == stats
@@ -264,7 +357,7 @@ def test_rx_assemble_first_copy_wins(gpu, encrypt, S, slot):
         for g in range(G):
             for r in range(n):
                 if (int(masks[g]) >> r) & 1:
-                    assert np.array_equal(g_major[g, r, :S], want[g, r, :S]), (g, r)
+                    assert np.array_equal(g_major[g, r], want[g, r]), (g, r)
                 else:
                     assert (g_major[g, r] == 0xAB).all(), (g, r)  # unclaimed rows untouched
     assert np.array_equal(runs[0][0], runs[1][0])
@@ -482,15 +575,17 @@ def test_rx_assemble_rejects_pageable_host_memory(gpu):
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(d=st.integers(1, 20), p=st.integers(1, 8), S=st.integers(1, 700), G=st.integers(1, 80),
        first_group=st.integers(0, 5), loss=st.floats(0, 0.5), dup=st.floats(0, 0.3), junk=st.floats(0, 0.1),
-       encrypt=st.booleans(), seed=st.integers(0, 2**31 - 1))
-def test_rx_assemble_random_rings(gpu, d, p, S, G, first_group, loss, dup, junk, encrypt, seed):
+       encrypt=st.booleans(), seed=st.integers(0, 2**31 - 1), frames=st.booleans())
+def test_rx_assemble_random_rings(gpu, d, p, S, G, first_group, loss, dup, junk, encrypt, seed, frames):
     """Random codes, shard sizes, windows and channels (loss, duplicates with
     different payloads, bad flags, short and out-of-window packets, any ring
     order): presence masks, stats and every placed row equal the per-packet
     reference path's (first copy of a seqid wins); rows no packet claimed stay
-    untouched."""
+    untouched.  frames: the frame layout (ugo_fec_rx_assemble_frames), each row
+    the packet's first S + 6 bytes, zeros to round_up(S + 6, 16)."""
     n = d + p
-    pitch = (S + 15) // 16 * 16
+    W = S + 6 if frames else S  # bytes a placed row carries
+    pitch = (W + 15) // 16 * 16
     slot = (S + 6 + 15) // 16 * 16
     rng = np.random.default_rng(seed)
 
@@ -517,7 +612,7 @@ def test_rx_assemble_random_rings(gpu, d, p, S, G, first_group, loss, dup, junk,
     if not wire:
         return
     wire = [wire[i] for i in rng.permutation(len(wire))]
-    want, masks, stats = _expected_placement(wire, G, n, S, pitch, first_group)
+    want, masks, stats = _expected_placement(wire, G, n, S, pitch, first_group, frames)
     ks = rc4_ref.keystream(KEY, slot)
     enc = [rc4_ref.xor_stream(KEY, w) if encrypt else w for w in wire]
     slots, lens = _ring(enc, slot)
@@ -527,14 +622,14 @@ def test_rx_assemble_random_rings(gpu, d, p, S, G, first_group, loss, dup, junk,
     stt = torch.zeros(5, dtype=torch.int32, device="cuda")
     pad = torch.frombuffer(bytearray(ks), dtype=torch.uint8).cuda() if encrypt else None
     codec.rx_assemble(torch.from_numpy(slots).cuda(), torch.from_numpy(lens.view(np.int16)).cuda(), sh, present,
-                      first_group=first_group, shard_size=S, pad=pad, stats=stt)
+                      first_group=first_group, shard_size=S, pad=pad, stats=stt, frames=frames)
     assert stt.cpu().tolist() == stats
     assert np.array_equal(present.cpu().numpy().view(np.uint64), masks)
     got = sh.cpu().numpy().transpose(1, 0, 2)
     for g in range(G):
         for r in range(n):
             if (int(masks[g]) >> r) & 1:
-                assert np.array_equal(got[g, r, :S], want[g, r, :S]), (g, r)
-                assert not got[g, r, S:].any(), (g, r)  # ABI 8: whole 16-B chunks, zeros past S
+                assert np.array_equal(got[g, r, :W], want[g, r, :W]), (g, r)
+                assert not got[g, r, W:].any(), (g, r)  # ABI 8: whole 16-B chunks, zeros past the row
             else:
                 assert (got[g, r] == 0xAB).all(), (g, r)

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Builds an A/B variant of the C-ABI library with extra -D flags into
-# build_ab/<name>/libugofec.so (select it with UGO_FEC_LIB=...).  Not product.
+# tools/ablib/<name>/libugofec.so (gitignored; it travels to the GPU box) (select it with UGO_FEC_LIB=...).  Not product.
 # usage: tools/build_variant.sh <name> -DMACRO=value ...
 set -e
 name=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-out=$ROOT/build_ab/$name
+out=$ROOT/tools/ablib/$name
 mkdir -p "$out/host"
 cd "$ROOT/ugo_amd/csrc"
 F="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result $*"

@@ -326,6 +326,161 @@ __global__ __launch_bounds__(256) void k_rx_place_h(RxArgs a) {
   }
 }
 
+// Frame rows (ugo_fec_rx_assemble_frames, round 6): row seqid % n of a group
+// receives the decrypted packet itself -- bytes [0, min(len, S + 6)), zeros up
+// to round_up(S + 6, 16) -- so the payload sits at column 6 of the row.  A
+// packet chunk lands at the same offset it was loaded from: no realignment, so
+// none of the place kernel's per-chunk neighbour exchange (two ds_bpermute per
+// chunk, lane 31's extra load, the funnel shift of rx_put).  GF columns are
+// independent, so Reconstruct over the frame window (shard size S + 6) gives
+// the payload columns bit for bit; the 6 header columns of a recovered row are
+// a combination of the survivors' headers and are ignored.  This is the frame
+// TX already keeps (k_tx_c: a lane holds packet bytes [16m, 16m + 16)).
+// Presence, first-copy rule, stats and gated passes as k_rx_place_h.
+__device__ __forceinline__ u32x4 rx_keep(u32x4 v, uint32_t o, uint32_t lim) {
+  // bytes at or past lim of the chunk at o become zero (only a packet's tail chunk)
+  if (o + 16u <= lim) return v;
+  const uint32_t keep = lim > o ? lim - o : 0u;
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t b0 = 4u * j;
+    const uint32_t k = keep >= b0 + 4u ? 4u : (keep > b0 ? keep - b0 : 0u);
+    w[j] &= k >= 4u ? 0xffffffffu : ((1u << (8u * k)) - 1u);
+  }
+  return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void k_rx_frame_h(RxArgs a) {
+  if (rx_gated_off(a)) return;
+  __shared__ uint32_t bstats[5];
+  if (threadIdx.x < 5) bstats[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, hl = lane & 31u;
+  const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
+  const uint64_t nwaves = (gridDim.x * 256ull) >> 6;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  const uint32_t FS = a.S + 6u;  // frame bytes kept per row
+  const uint32_t FW = a.fill;     // bytes written per row (zeros past FS)
+  const bool chk_prev = a.prev && !(a.seen && *a.seen < a.call);
+  u32x4 K[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const uint32_t o = 16u * (32u * q + hl);
+    K[q] = (a.pad && o + 16u <= slot) ? ld16(a.pad + o) : zero;
+  }
+  RxAccount acct;
+  const uint64_t step = 2 * nwaves;
+  const int hsrc = static_cast<int>(half * 32u) * 4;  // lane 0 of this half
+  uint64_t i = 2 * wave + half;
+  uint32_t ln = i < a.npk ? a.lens[i] : 0u;
+  for (uint64_t base = 2 * wave; base < a.npk; base += step, i += step) {
+    const bool have = i < a.npk;
+    const uint8_t* pk = a.wire + i * a.slot;
+    const uint32_t len = have ? min(ln, slot) : 0u;
+    if (i + step < a.npk) ln = a.lens[i + step];  // the next packet's length
+    const uint32_t lim = len >= 6u ? min(len, FS) : 0u;  // packet bytes [0, lim) are kept
+    u32x4 A[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      A[q] = o < lim ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + o)) : zero;
+    }
+    const u32x4 A0 = A[0] ^ K[0];  // lane 0: packet bytes [0, 16) = the header
+    const uint32_t seqid = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(hsrc, static_cast<int>(A0.x)));
+    const uint32_t flag = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(hsrc, static_cast<int>(A0.y))) & 0xffffu;
+    uint32_t why = 0;
+    if (!have) why = 5;
+    else if (len < 6u) why = 3;
+    else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
+    const uint32_t row = seqid % a.n;
+    const uint64_t grp = seqid / a.n;
+    if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
+    const bool acc = why == 0;
+    uint32_t claim = static_cast<uint32_t>(i);
+    if (acc && a.win) claim = a.win[(grp - a.first_group) * a.n + row];
+    uint64_t before = 0;
+    if (acc && chk_prev) before = a.prev[grp - a.first_group];
+    if (acc && claim != static_cast<uint32_t>(i)) why = 4;
+    if (acc && ((before >> row) & 1ull)) why = 4;
+    const bool ok = why == 0;
+    uint8_t* dst = a.shards + row * a.rstride + (grp - a.first_group) * a.gstride;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const uint32_t o = 16u * (32u * q + hl);
+      if (!ok || o >= FW) continue;
+      __builtin_nontemporal_store(rx_keep(A[q] ^ K[q], o, lim), reinterpret_cast<u32x4*>(dst + o));
+    }
+    if (hl == 0) acct.issue(a, bstats, why, grp - a.first_group, row);
+  }
+  if (hl == 0) acct.settle(a, bstats);
+  if (a.stats) {
+    __syncthreads();
+    if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+  }
+}
+
+// Frame rows wider than 4 passes of 32 chunks (S + 6 > 2048, e.g. jumbo
+// packets): the same placement in a loop over passes, the header loaded by
+// every lane of the half (one broadcast request).
+__global__ __launch_bounds__(256) void k_rx_frame_scatter(RxArgs a) {
+  if (rx_gated_off(a)) return;
+  __shared__ uint32_t bstats[5];
+  if (threadIdx.x < 5) bstats[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, half = lane >> 5, hl = lane & 31u;
+  const uint64_t wave = (blockIdx.x * 256ull + threadIdx.x) >> 6;
+  const uint64_t nwaves = (gridDim.x * 256ull) >> 6;
+  const uint32_t slot = static_cast<uint32_t>(a.slot);
+  const uint32_t FS = a.S + 6u;
+  const uint32_t nq = a.fill / 16u;
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const u32x4 K0 = a.pad ? ld16(a.pad) : zero;
+  RxAccount acct;
+  const uint64_t step = 2 * nwaves;
+  uint64_t i = 2 * wave + half;
+  for (uint64_t base = 2 * wave; base < a.npk; base += step, i += step) {
+    const bool have = i < a.npk;
+    const uint8_t* pk = a.wire + i * a.slot;
+    const uint32_t len = have ? min(static_cast<uint32_t>(a.lens[i]), slot) : 0u;
+    const uint32_t lim = len >= 6u ? min(len, FS) : 0u;
+    u32x4 h = zero;
+    if (lim) h = ld16(pk) ^ K0;
+    const uint32_t seqid = h.x;
+    const uint32_t flag = h.y & 0xffffu;
+    uint32_t why = 0;
+    if (!have) why = 5;
+    else if (len < 6u) why = 3;
+    else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
+    const uint32_t row = seqid % a.n;
+    const uint64_t grp = seqid / a.n;
+    if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
+    const uint64_t gs = grp - a.first_group;
+    if (!why && a.prev && ((a.prev[gs] >> row) & 1ull)) why = 4;
+    if (!why && a.win && a.win[gs * a.n + row] != static_cast<uint32_t>(i)) why = 4;
+    if (why == 0) {
+      uint8_t* dst = a.shards + row * a.rstride + gs * a.gstride;
+      for (uint32_t q = hl; q < nq; q += 32u) {
+        const uint32_t o = 16u * q;
+        u32x4 v = zero;
+        if (o < lim) {
+          v = ld16(pk + o);
+          if (a.pad && o + 16u <= slot) v ^= ld16(a.pad + o);
+        }
+        *reinterpret_cast<u32x4*>(dst + o) = rx_keep(v, o, lim);
+      }
+    }
+    if (hl == 0) acct.issue(a, bstats, why, gs, row);
+  }
+  if (hl == 0) acct.settle(a, bstats);
+  if (a.stats) {
+    __syncthreads();
+    if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
+  }
+}
+
 // First-arrival claim: one thread per packet reads its 8 header bytes (seqid,
 // flag), classifies it exactly as the place kernels do, and takes the
 // smallest index per (group, row).  ~8 B read per 1.5-KB packet.
@@ -392,6 +547,9 @@ hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, h
   return hipGetLastError();
 }
 
+#ifndef UGO_RX_GRID_BLOCKS
+#define UGO_RX_GRID_BLOCKS 16384u
+#endif
 static inline uint32_t rx_blocks(const RxArgs& a) {
   const uint64_t waves = (a.npk + 1) / 2;
   uint64_t blocks = (waves + 3) / 4;
@@ -400,7 +558,7 @@ static inline uint32_t rx_blocks(const RxArgs& a) {
   // k_rx_place_h 0.3-1.5% faster than 8192 on two boxes and 2.5% faster than
   // 4096, 32768 no better (profiles/r4/rxgather_hgrid_*.jsonl, _g16k_*; _grid_*
   // for the earlier form)
-  if (blocks > 16384u) blocks = 16384u;
+  if (blocks > UGO_RX_GRID_BLOCKS) blocks = UGO_RX_GRID_BLOCKS;
   return static_cast<uint32_t>(blocks);
 }
 
@@ -421,10 +579,39 @@ hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Residency cap of the frame kernels: dynamic LDS they never touch holds them
+// to kRxFrameBlocks blocks per CU (0: none, the VGPR-limited occupancy).
+#ifndef UGO_RX_FRAME_BLOCKS
+#define UGO_RX_FRAME_BLOCKS 3
+#endif
+static uint32_t rx_frame_lds() {
+  static const uint32_t cap = [] {
+    if (UGO_RX_FRAME_BLOCKS <= 0) return 0u;
+    int dev = 0, lds = 160 * 1024;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
+        lds <= 4096)
+      lds = 160 * 1024;
+    return static_cast<uint32_t>(lds / UGO_RX_FRAME_BLOCKS - 1024);
+  }();
+  return cap;
+}
+
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
   uint32_t blocks = rx_blocks(a);
   if (a.gate && blocks > kRxGatedBlocks) blocks = static_cast<uint32_t>(kRxGatedBlocks);
   if (blocks == 0) return hipSuccess;
+  if (a.frame) {  // frame rows: no realignment (k_rx_frame_h)
+    const uint32_t lds = rx_frame_lds();
+    switch ((a.fill / 16u + 31u) / 32u) {
+      case 1: launch(kKRx, k_rx_frame_h<1>, dim3(blocks), dim3(256), lds, s, a); break;
+      case 2: launch(kKRx, k_rx_frame_h<2>, dim3(blocks), dim3(256), lds, s, a); break;
+      case 3: launch(kKRx, k_rx_frame_h<3>, dim3(blocks), dim3(256), lds, s, a); break;
+      case 4: launch(kKRx, k_rx_frame_h<4>, dim3(blocks), dim3(256), lds, s, a); break;
+      default: launch(kKRx, k_rx_frame_scatter, dim3(blocks), dim3(256), lds, s, a); break;
+    }
+    return hipGetLastError();
+  }
   const uint32_t passes = ((a.S + 15u) / 16u + 31u) / 32u;
   // nt loads + stores: on a cold ring and batch 493 vs 552 us with plain ones
   // (a linear copy of the same bytes: 487 us; tools/rxvariants 15 cold)

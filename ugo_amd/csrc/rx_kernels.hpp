@@ -32,6 +32,8 @@ struct RxArgs {
   uint64_t gstride;
   uint32_t S;              // shard size (payload bytes kept per row)
   uint32_t n;              // d + p
+  uint32_t frame;          // 1: frame rows -- the row holds packet bytes [0, S + 6), payload at column 6
+  uint32_t fill;           // frame rows: bytes written per row (a multiple of 16 >= S + 6; zeros past S + 6)
 };
 
 // Claims every (group, row) for its first packet in ring order (atomicMin of

@@ -577,7 +577,11 @@ int ensure_streams(ugo_fec* c) {
 int ensure_stage(ugo_fec* c, size_t pitch) {
   const size_t gbytes = size_t(c->n) * pitch;
   const size_t want = std::max<size_t>(1, kStageBytes / gbytes);
-  if (c->stage_groups >= want && c->stage_pitch == pitch && c->streams[0]) return UGO_FEC_OK;
+  // every stream first: ugo_fec_set_host_copy_queue drops streams[1], and a
+  // staged call must never fall back to the legacy null stream
+  const int se = ensure_streams(c);
+  if (se) return se;
+  if (c->stage_groups >= want && c->stage_pitch == pitch) return UGO_FEC_OK;
   for (int i = 0; i < kStreams; ++i) {
     (void)hipFree(c->d_stage[i]);
     (void)hipFree(c->d_mask[i]);
@@ -588,7 +592,6 @@ int ensure_stage(ugo_fec* c, size_t pitch) {
   }
   c->stage_groups = 0;
   for (int i = 0; i < kStreams; ++i) {
-    if (!c->streams[i] && create_stream(c, i, &c->streams[i]) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_stage[i], want * gbytes + 16) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_mask[i], want * mask_words(c) * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
     if (hipMalloc(&c->d_status[i], want) != hipSuccess) return UGO_FEC_ERR_HIP;
@@ -800,6 +803,19 @@ void svc_release(ugo_fec* c) {
   c->svc_stream = nullptr;
 }
 
+// A stream whose block faulted: destroyed, not pooled; its slot is counted
+// free so the next lease makes a fresh stream.
+void svc_discard(ugo_fec* c) {
+  if (!c->svc_stream) return;
+  (void)hipGetLastError();
+  (void)hipStreamDestroy(c->svc_stream);
+  c->svc_stream = nullptr;
+  SvcStreamPool& p = svc_pool();
+  std::lock_guard<std::mutex> lk(p.mu);
+  int& made = p.created[c->device];
+  if (made > 0) --made;
+}
+
 // Writes one request (layout: SvcBox::line): every field, then the pieces'
 // tags, then seq; returns seq.
 uint32_t svc_post(ugo_fec* c, uint32_t op, const uint8_t* mapped, size_t groups, size_t S, size_t pitch,
@@ -851,10 +867,17 @@ int svc_retire(ugo_fec* c) {
   for (uint32_t spin = 0;; ++spin) {
     if ((spin & 255u) == 0) {
       const hipError_t q = hipStreamQuery(c->svc_stream);
-      // drained (alive is 0 or the block never ran), or faulted (the block is
-      // dead): nothing of c's is left on the stream, another context may lease it
-      if (q == hipSuccess || q != hipErrorNotReady) {
+      // drained (alive is 0 or the block never ran): nothing of c's is left on
+      // the stream, another context may lease it.  Faulted (the block is dead):
+      // nothing of c's runs either, but the stream may carry the fault's sticky
+      // state, so it is dropped and its pool slot freed for a fresh stream
+      // 
+      if (q == hipSuccess) {
         svc_release(c);
+        return UGO_FEC_OK;
+      }
+      if (q != hipErrorNotReady) {
+        svc_discard(c);
         return UGO_FEC_OK;
       }
       if (std::chrono::steady_clock::now() - t0 > grace) break;
@@ -1001,11 +1024,27 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
   return UGO_FEC_OK;
 }
 
+// Bytes a frame row is written to: round_up(S + 6, 16), or -- when the row
+// slots are 64-B aligned and span it -- round_up(S + 6, 64): a row then ends on
+// a whole 64-B line instead of leaving its last line partially written (which
+// the neighbouring row's writer completes at another time).
+#ifndef UGO_RX_FRAME_FILL64
+#define UGO_RX_FRAME_FILL64 1
+#endif
+size_t rx_frame_fill(const uint8_t* shards, size_t S, size_t rstride, size_t gstride, size_t rows, size_t groups) {
+  const size_t w16 = round_up(S + 6, 16), w64 = round_up(S + 6, 64);
+  if (!UGO_RX_FRAME_FILL64 || reinterpret_cast<uintptr_t>(shards) % 64 || rstride % 64 || gstride % 64) return w16;
+  return layout_disjoint(w64, rstride, rows, gstride, groups) ? w64 : w16;
+}
+
 // rx_assemble on device views (arguments checked by the caller).
 int rx_assemble_dev(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
                     const uint8_t* pad, uint64_t first_group, size_t groups, uint8_t* shards, size_t S,
-                    size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats, hipStream_t s) {
+                    size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats, hipStream_t s,
+                    bool frame = false) {
   ugo::kern::RxArgs a{};
+  a.frame = frame ? 1u : 0u;
+  a.fill = static_cast<uint32_t>(rx_frame_fill(shards, S, row_stride, group_stride, size_t(c->n), groups));
   a.wire = wire;
   a.lens = lens;
   a.pad = pad;
@@ -1063,7 +1102,8 @@ int lossy_list_dev(ugo_fec* c, const uint64_t* present, size_t groups, unsigned 
     return hip_status(hipMemsetAsync(count, 0, sizeof(uint32_t), s));
   }
   const uint64_t nmask = c->n >= 64 ? ~0ull : ((1ull << c->n) - 1);
-  const uint64_t dmask = (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) ? ((1ull << c->d) - 1) : ~0ull;
+  const uint64_t dmask =
+      (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) && c->d < 64 ? ((1ull << c->d) - 1) : ~0ull;  // d = 64: p = 0
   const size_t blocks = (groups + ugo::kern::kLossyPerBlock - 1) / ugo::kern::kLossyPerBlock;
   void* work = nullptr;
   int st = scratch_alloc(c, 2 * blocks * sizeof(uint32_t), s, &work);
@@ -1561,10 +1601,13 @@ int ugo_fec_reconstruct_host(ugo_fec* c, uint8_t* shards, const uint64_t* presen
   return host_path(c, shards, present, groups, S, pitch, true, flags, status);
 }
 
-int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
-                        const uint8_t* pad, uint64_t first_group, size_t groups, uint8_t* shards, size_t S,
-                        size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats,
-                        void* stream) {
+namespace {
+// ugo_fec_rx_assemble / _frames: argument checks, device views, launch.  A
+// frame row spans S + 6 bytes (the packet's header columns, then the payload).
+int rx_assemble_abi(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
+                    const uint8_t* pad, uint64_t first_group, size_t groups, uint8_t* shards, size_t S,
+                    size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats, void* stream,
+                    bool frame) {
   if (!c) return UGO_FEC_ERR_INVALID_ARG;
   if (c->poisoned) return UGO_FEC_ERR_HIP;  // a service block that never left (svc_retire)
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
@@ -1573,9 +1616,10 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
     return UGO_FEC_ERR_INVALID_ARG;
   if (slot_stride % 16 || slot_stride < 16 || reinterpret_cast<uintptr_t>(wire) % 16 ||
       reinterpret_cast<uintptr_t>(shards) % 16 || row_stride % 16 || group_stride % 16 ||
-      (pad && reinterpret_cast<uintptr_t>(pad) % 16) || S > 0xffffffffu)
+      (pad && reinterpret_cast<uintptr_t>(pad) % 16) || S > 0xffffffffu - 22)
     return UGO_FEC_ERR_INVALID_ARG;
-  if (!layout_disjoint(S, row_stride, size_t(c->n), group_stride, groups)) return UGO_FEC_ERR_INVALID_ARG;
+  const size_t span = frame ? S + 6 : S;
+  if (!layout_disjoint(span, row_stride, size_t(c->n), group_stride, groups)) return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
   if (!device_view(wire) || !device_view(lens) || !device_view(pad) || !device_view(shards) ||
@@ -1583,7 +1627,24 @@ int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, con
     return UGO_FEC_ERR_INVALID_ARG;
   TimerScope ts(c);
   return rx_assemble_dev(c, wire, slot_stride, lens, npk, pad, first_group, groups, shards, S, row_stride,
-                         group_stride, present, stats, static_cast<hipStream_t>(stream));
+                         group_stride, present, stats, static_cast<hipStream_t>(stream), frame);
+}
+}  // namespace
+
+int ugo_fec_rx_assemble(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
+                        const uint8_t* pad, uint64_t first_group, size_t groups, uint8_t* shards, size_t S,
+                        size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats,
+                        void* stream) {
+  return rx_assemble_abi(c, wire, slot_stride, lens, npk, pad, first_group, groups, shards, S, row_stride,
+                         group_stride, present, stats, stream, false);
+}
+
+int ugo_fec_rx_assemble_frames(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens,
+                               size_t npk, const uint8_t* pad, uint64_t first_group, size_t groups, uint8_t* shards,
+                               size_t S, size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats,
+                               void* stream) {
+  return rx_assemble_abi(c, wire, slot_stride, lens, npk, pad, first_group, groups, shards, S, row_stride,
+                         group_stride, present, stats, stream, true);
 }
 
 int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const uint16_t* lens, size_t groups,
@@ -1643,6 +1704,11 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
 // copy lands, so copies and kernels overlap; then the lossy-group list, the
 // data-only Reconstruct of those groups into a row-compact output (the
 // `recovered` list of ugo/fec.go:203-207), and the D2H of those rows only.
+#ifndef UGO_RX_FRAMES
+#define UGO_RX_FRAMES 1
+#endif
+constexpr bool kRxFrames = UGO_RX_FRAMES != 0;
+
 int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
                             const uint8_t* pad, uint64_t first_group, size_t groups, size_t S, uint64_t* present_out,
                             uint32_t* stats_out, uint8_t* out, size_t out_row_stride, size_t max_out,
@@ -1653,7 +1719,7 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   if (S == 0) return UGO_FEC_ERR_SHARD_NO_DATA;
   if (groups == 0) return UGO_FEC_OK;
   if ((npk && (!wire || !lens)) || c->n > 16 || !c->d_table || groups * size_t(c->n) >= 0xffffffffull || npk >= 0xffffffffull ||
-      slot_stride % 16 || slot_stride < 16 || S > 0xffffffffu || out_row_stride < S ||
+      slot_stride % 16 || slot_stride < 16 || S > 0xffffffffu - 22 || out_row_stride < S ||
       (max_out && (!out || !out_index)))
     return UGO_FEC_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
@@ -1662,7 +1728,12 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   int st = ensure_streams(c);
   if (st) return st;
   const hipStream_t s0 = c->streams[0];  // assembly and recovery; copies on streams[1]
-  const size_t n = size_t(c->n), pitch = round_up(S, 16), slots = size_t(std::min(c->d, c->p));
+  // frame rows (ugo_fec_rx_assemble_frames): each row holds its decrypted packet, the payload at
+  // column 6, so placement needs no realignment; the recovery runs over the frame window
+  // (GF columns are independent) and only the payload columns of a recovered row come back
+  const size_t fo = kRxFrames ? 6 : 0, FS = S + fo;
+  // (frame rows at a 64-B pitch: whole 64-B lines per row, rx_frame_fill)
+  const size_t n = size_t(c->n), pitch = round_up(FS, kRxFrames ? 64 : 16), slots = size_t(std::min(c->d, c->p));
   // packets per chunk: at most a 64-MiB stage, at least 4 chunks so copies and assembly overlap, and
   // at most 32 chunks (the chunks grow with the ring past that: see kTxMaxChunks)
   const size_t cpk = std::max<size_t>({size_t(1), (npk + 31) / 32, std::min((npk + 3) / 4, kStageBytes / slot_stride)});
@@ -1744,7 +1815,7 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
     if (hipStreamWaitEvent(s0, ev[b], 0) != hipSuccess) return UGO_FEC_ERR_HIP;
     // (chunk 0's wait covers the lengths' copy, earlier on the same stream; later chunks follow it on s0)
     st = rx_assemble_dev(c, base + o_stage + b * stage_bytes, slot_stride, dlens + p0, m, dpad, first_group, groups,
-                         batch, S, groups * pitch, pitch, dpres, dstats, s0);
+                         batch, S, groups * pitch, pitch, dpres, dstats, s0, kRxFrames);
     if (st) return st;
     if (hipEventRecord(ev[kRxStages + b], s0) != hipSuccess) return UGO_FEC_ERR_HIP;
   }
@@ -1752,7 +1823,7 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   st = lossy_list_dev(c, dpres, groups, UGO_FEC_RECONSTRUCT_DATA_ONLY, dlist, dcount, s0, droff, dcount + 1);
   if (st) return st;
   if (max_out) {
-    st = reconstruct_list_dev(c, batch, dpres, dlist, dcount, groups, S, Layout{groups * pitch, pitch}, dout, pitch,
+    st = reconstruct_list_dev(c, batch, dpres, dlist, dcount, groups, FS, Layout{groups * pitch, pitch}, dout, pitch,
                               0, UGO_FEC_RECONSTRUCT_DATA_ONLY, nullptr, s0, droff, drid);
     if (st) return st;
   }
@@ -1764,7 +1835,7 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   hipError_t e = hipSuccess;
   if (w) {  // only the recovered rows cross PCIe: w rows of S bytes
     e = hipMemcpyAsync(out_index, drid, w * 4, hipMemcpyDeviceToHost, s0);
-    if (e == hipSuccess) e = hipMemcpy2DAsync(out, out_row_stride, dout, pitch, S, w, hipMemcpyDeviceToHost, s0);
+    if (e == hipSuccess) e = hipMemcpy2DAsync(out, out_row_stride, dout + fo, pitch, S, w, hipMemcpyDeviceToHost, s0);
   }
   if (e == hipSuccess && present_out) e = hipMemcpyAsync(present_out, dpres, groups * 8, hipMemcpyDeviceToHost, s0);
   if (e == hipSuccess && stats_out) e = hipMemcpyAsync(stats_out, dstats, 20, hipMemcpyDeviceToHost, s0);

@@ -138,6 +138,7 @@ def load_library(path: str = LIB_PATH):
     lib.ugo_fec_strerror.restype = ctypes.c_char_p
     lib.ugo_fec_abi_version.argtypes = []
     lib.ugo_fec_rx_assemble.argtypes = [vp, vp, sz, vp, sz, vp, ctypes.c_uint64, sz, vp, sz, sz, sz, vp, vp, vp]
+    lib.ugo_fec_rx_assemble_frames.argtypes = lib.ugo_fec_rx_assemble.argtypes
     lib.ugo_fec_rc4_keystream.argtypes = [vp, sz, vp, sz]
     lib.ugo_fec_tx_assemble.argtypes = [vp, vp, sz, vp, sz, ctypes.c_uint32, vp, sz, vp, sz, vp, vp, vp]
     lib.ugo_fec_packet_decode.argtypes = [vp, vp, sz, vp, sz, vp, u, vp, vp, sz, vp, sz, vp]
@@ -365,7 +366,12 @@ class Encoder:
         [max_out, row] with row >= shard_size, allocated if None) in ugo's
         `recovered` order, index[r] = window group * (d+p) + row."""
         npk, slot = wire.shape
-        _require(wire.flags.c_contiguous and lens.flags.c_contiguous and lens.size == npk and lens.itemsize == 2)
+        _require(wire.flags.c_contiguous and wire.itemsize == 1)
+        _require(lens.flags.c_contiguous and lens.size == npk and lens.itemsize == 2)
+        _require(pad is None or len(pad) >= slot, "pad must hold at least slot_stride keystream bytes")
+        if present_out is not None:  # C writes groups * 8 bytes there (ADVICE r5)
+            _require(isinstance(present_out, np.ndarray) and present_out.flags.c_contiguous
+                     and present_out.itemsize == 8 and present_out.size >= groups)
         m = groups * min(self.DataShards, self.ParityShards) if max_out is None else max_out
         if out is None:
             out = np.zeros((max(m, 1), (shard_size + 15) // 16 * 16), np.uint8)
@@ -390,6 +396,15 @@ class Encoder:
         _require(pkts.ndim == 2 and wire.ndim == 2 and pkts.shape[0] % d == 0)
         G = pkts.shape[0] // d
         _require(lens.size == G * d and wire.shape[0] == G * n and wire_lens.size == G * n)
+        # the C side copies G*d*2, G*n*2 and G bytes and reads round_up(max_len, 16) pad bytes
+        for a in (pkts, wire, lens, wire_lens):
+            _require(isinstance(a, np.ndarray) and a.flags.c_contiguous)
+        _require(pkts.itemsize == 1 and wire.itemsize == 1 and lens.itemsize == 2 and wire_lens.itemsize == 2)
+        if status is not None:
+            _require(isinstance(status, np.ndarray) and status.flags.c_contiguous and status.size == G
+                     and status.itemsize == 1)
+        _require(pad is None or len(pad) >= (max_len + 15) // 16 * 16,
+                 "pad must hold at least round_up(max_len, 16) keystream bytes")
         padb = None if pad is None else np.frombuffer(bytes(pad), np.uint8)
         _raise(load_library().ugo_fec_tx_assemble_host(
             self._h, pkts.ctypes.data, pkts.shape[1], lens.ctypes.data, G, first_seq,
@@ -442,20 +457,25 @@ class Encoder:
         return out.value or 0
 
     def rx_assemble(self, wire, lens, shards, present, first_group: int = 0, shard_size: Optional[int] = None,
-                    pad=None, stats=None, stream=None, shard_major: bool = True):
+                    pad=None, stats=None, stream=None, shard_major: bool = True, frames: bool = False):
         """RX group assembly (include/ugo_fec.h ugo_fec_rx_assemble): wire = uint8 CUDA
         tensor [npk, slot] of received packets, lens = int16/uint16 CUDA tensor [npk];
         pad = uint8 CUDA keystream (>= slot bytes) or None; present = int64 CUDA [G]
         (zeroed by the caller); stats = int32 CUDA [5] (accepted, bad flag, out of
         window, too short, duplicate) or None.  A repeated seqid keeps its first
-        copy in ring order (ugo/fec.go:123-129)."""
+        copy in ring order (ugo/fec.go:123-129).  frames=True:
+        ugo_fec_rx_assemble_frames -- a row holds the decrypted packet (payload at
+        column 6, shard_size + 6 bytes); reconstruct it with shard_size + 6."""
         if stats is not None:
             _require(stats.numel() >= 5 and stats.element_size() == 4)
         G, pitch, rs, gs = self._geom(shards, shard_major)
         npk, slot = wire.shape
         _require(wire.is_contiguous() and lens.is_contiguous() and lens.element_size() == 2 and lens.numel() == npk)
-        S = pitch if shard_size is None else shard_size
-        _raise(load_library().ugo_fec_rx_assemble(
+        S = (pitch - 6 if frames else pitch) if shard_size is None else shard_size
+        if pad is not None:
+            _require(pad.is_contiguous() and pad.element_size() == 1 and pad.numel() >= slot)
+        entry = load_library().ugo_fec_rx_assemble_frames if frames else load_library().ugo_fec_rx_assemble
+        _raise(entry(
             self._h, wire.data_ptr(), slot, lens.data_ptr(), npk, None if pad is None else pad.data_ptr(),
             first_group, G, shards.data_ptr(), S, rs, gs, present.data_ptr(),
             None if stats is None else stats.data_ptr(), _stream_handle(stream)))
