@@ -338,6 +338,32 @@ def test_host_api_pipelined(gpu):
         fec.host_free(buf)
 
 
+def test_host_staged_paths_after_copy_queue_toggle(gpu):
+    """ugo_fec_set_host_copy_queue drops the H2D stream; the staged encode_host /
+    reconstruct_host paths that follow (pageable batches, >= 3 chunks, so a
+    chunk runs on that stream) make it again instead of falling back to the
+    legacy null stream, with results equal to the oracle's in
+    every state of the switch."""
+    d, p, n, S, pitch, G = 10, 3, 13, 1350, 1360, 8000  # 64-MiB stages: 3,795 groups each -> 3 chunks
+    host = _rand(G, n, pitch, 79).numpy()
+    want = host.copy()
+    rs_ref.c_encode(d, p, want, S=S)
+    rng = np.random.default_rng(9)
+    masks = np.array([((1 << n) - 1) & ~int(sum(1 << int(r) for r in rng.choice(n, int(rng.integers(0, 4)),
+                                                                                 replace=False)))
+                      for _ in range(G)], dtype=np.uint64)
+    inp = _erase(want, masks, n)
+    enc = fec.New(d, p)
+    for on in (False, True, True, False):
+        enc.set_host_copy_queue(on)
+        got = host.copy()
+        enc.encode_host(got, S)
+        assert np.array_equal(got, want), on
+        out = inp.copy()
+        assert enc.reconstruct_host(out, masks, S) == 0
+        assert np.array_equal(out[:, :, :S], want[:, :, :S]), on
+
+
 @pytest.mark.parametrize("offset,pitch,data_only", [(256, 1360, False), (3, 1353, False), (16, 1360, True)])
 def test_host_reconstruct_pinned_zero_copy(gpu, offset, pitch, data_only):
     """Pinned host batches are reconstructed zero-copy: the kernels read the
@@ -639,6 +665,59 @@ def test_lossy_list_and_reconstruct_list_vs_oracle(gpu, d, p, S, pitch, shard_ma
                     if not (int(masks[g]) >> r) & 1 and (r < d or not data_only):
                         exp_ip[g, r, :S] = want[g, r, :S]
         assert np.array_equal(got, exp_ip)
+
+
+@pytest.mark.parametrize("G", [4096, 4097, 70000, 4 * 1048576 + 123])
+def test_lossy_list_many_tiles(gpu, G):
+    """The one-launch lossy list (k_lossy_list1: each 4,096-group tile publishes
+    its counts, every tile sums the tiles before it) over 1 to 1,025 tiles,
+    against numpy: the list, its count, and -- through ugo_fec_recover_data --
+    each entry's row offset (the recovered rows' places, in `recovered` order).
+    Repeated calls on two streams alternate, so each stream's count words are
+    reused with new epochs; a tile whose groups are all complete publishes 0."""
+    d, p = 10, 3
+    n = d + p
+    rng = np.random.default_rng(G)
+    full = (1 << n) - 1
+    masks = np.full(G, full, np.uint64)
+    lossy = rng.random(G) < 0.3
+    lossy[G // 3: G // 3 + 9000] = False  # whole complete tiles in the middle
+    for k in range(1, 5):  # 1..4 erased rows, some below d shards
+        sel = lossy & (rng.integers(1, 5, G) == k)
+        for _ in range(k):
+            masks[sel] &= ~(np.uint64(1) << rng.integers(0, n, G).astype(np.uint64))[sel]
+    dm = _masks_to_dev(masks)
+    torch.cuda.synchronize()  # the masks are on the default stream; the calls below run on two others
+    enc = fec.New(d, p)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    lst = torch.empty(G, dtype=torch.int32, device="cuda")
+    for data_only in (True, False, True):
+        scope = np.uint64(((1 << d) - 1) if data_only else full)
+        want = np.nonzero((~masks) & np.uint64(full) & scope)[0]
+        for call in range(3):
+            s = streams[call % 2]
+            with torch.cuda.stream(s):
+                lst.fill_(-1)
+                _, cnt = enc.lossy_groups(dm, data_only=data_only, out=lst, stream=s)
+            s.synchronize()
+            k = int(cnt.item())
+            assert k == len(want), (data_only, call)
+            assert np.array_equal(lst[:k].cpu().numpy(), want.astype(np.int32)), (data_only, call)
+            assert (lst[k:] == -1).all()
+    if G > 100000:
+        return
+    # row offsets: the places ugo_fec_recover_data writes for each recovered row
+    S, pitch = 16, 16
+    sh = torch.zeros((n, G, pitch), dtype=torch.uint8, device="cuda")
+    have = np.zeros(G, np.int64)
+    for r in range(n):
+        have += ((masks >> np.uint64(r)) & np.uint64(1)).astype(np.int64)
+    want_idx = [g * n + r for g in np.nonzero(have >= d)[0] for r in range(d) if not (int(masks[g]) >> r) & 1]
+    out = torch.empty((len(want_idx), pitch), dtype=torch.uint8, device="cuda")
+    idx = torch.full((len(want_idx),), -1, dtype=torch.int32, device="cuda")
+    cnt = enc.recover_data(sh, dm, out, idx, shard_size=S)
+    assert int(cnt.item()) == len(want_idx)
+    assert idx.cpu().numpy().tolist() == want_idx
 
 
 @pytest.mark.parametrize("d,p,S,pitch,shard_major,G", [

@@ -2019,6 +2019,106 @@ __global__ __launch_bounds__(1024) void k_lossy_write(const uint64_t* present, u
   }
 }
 
+// The same list in ONE launch (round 6): block b counts its
+// tile, publishes (count, rows) tagged with the call's epoch in one 64-bit word
+// (epoch << 32 | rows << 13 | count: a tile holds at most 4096 groups, 13 bits,
+// and 4096 * 32 rows, 18 bits), then waits until every block before it has
+// published and sums their words in parallel (block b reads b words over its
+// 1024 threads) -- no chained look-back, so no block waits on another's wait.
+// Forward progress: a block publishes before it waits, and the lowest block
+// that has not published is always dispatched (workgroups go out in index
+// order, so the blocks holding its XCD's slots are lower ones, which have
+// published and only wait on published blocks).  The words live in
+// context-owned memory, one buffer per stream (calls on one stream are ordered;
+// the epoch grows per call, so a word from an earlier call never matches).
+__global__ __launch_bounds__(1024) void k_lossy_list1(const uint64_t* present, uint64_t groups, uint64_t nmask,
+                                                      uint64_t dmask, uint32_t d, uint64_t* words, uint32_t epoch,
+                                                      uint32_t* list, uint32_t* count, uint32_t* rowoff,
+                                                      uint32_t* rows_total) {
+  constexpr uint32_t kPer = kLossyPerBlock / 1024u;
+  __shared__ uint32_t wsum[2][16];
+  __shared__ uint32_t base[2];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint64_t g0 = uint64_t(blockIdx.x) * kLossyPerBlock + uint64_t(t) * kPer;
+  uint32_t bits = 0, c = 0, r = 0, rk[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint64_t g = g0 + k;
+    bool l = false;
+    rk[k] = g < groups ? lossy_rows(present[g], nmask, dmask, d, l) : 0u;
+    bits |= static_cast<uint32_t>(l) << k;
+    c += l;
+    r += rk[k];
+  }
+  const uint32_t inc = wave_inclusive(c, lane), rinc = wave_inclusive(r, lane);
+  if (lane == 63u) {
+    wsum[0][wv] = inc;
+    wsum[1][wv] = rinc;
+  }
+  if (t < 2) base[t] = 0;
+  __syncthreads();
+  if (t == 0) {  // this tile's totals, published at once
+    uint32_t tc = 0, tr = 0;
+    for (uint32_t w = 0; w < 16u; ++w) {
+      tc += wsum[0][w];
+      tr += wsum[1][w];
+    }
+    const uint64_t word = (uint64_t(epoch) << 32) | (uint64_t(tr) << 13) | tc;
+    __hip_atomic_store(&words[blockIdx.x], word, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // every earlier tile's totals: thread t waits for tiles t, t + 1024, ... below this one
+  uint32_t before = 0, rbefore = 0;
+  for (uint32_t b = t; b < blockIdx.x; b += 1024u) {
+    uint64_t w;
+    uint32_t spins = 0;
+    do {
+      w = __hip_atomic_load(&words[b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (static_cast<uint32_t>(w >> 32) != epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        // a word that never arrives (seconds) is a broken invariant: fault loudly instead of hanging
+        if (++spins == (1u << 26)) __builtin_trap();
+      }
+    } while (static_cast<uint32_t>(w >> 32) != epoch);
+    before += static_cast<uint32_t>(w) & 0x1fffu;
+    rbefore += static_cast<uint32_t>(w) >> 13;
+  }
+  before = __reduce_add_sync(~0ull, before);
+  rbefore = __reduce_add_sync(~0ull, rbefore);
+  if (lane == 0) {
+    if (before) atomicAdd(&base[0], before);
+    if (rbefore) atomicAdd(&base[1], rbefore);
+  }
+  __syncthreads();
+  uint32_t wbefore = 0, wrbefore = 0;
+  for (uint32_t w = 0; w < wv; ++w) {
+    wbefore += wsum[0][w];
+    wrbefore += wsum[1][w];
+  }
+  uint32_t pos = base[0] + wbefore + inc - c, rpos = base[1] + wrbefore + rinc - r;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k)
+    if ((bits >> k) & 1u) {
+      list[pos] = static_cast<uint32_t>(g0 + k);
+      if (rowoff) rowoff[pos] = rpos;
+      ++pos;
+      rpos += rk[k];
+    }
+  if (blockIdx.x == gridDim.x - 1u && t == 1023u) {  // the last thread's ends = the totals
+    *count = pos;
+    if (rows_total) *rows_total = rpos;
+  }
+}
+
+hipError_t launch_lossy_list1(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t d,
+                              uint32_t* list, uint32_t* count, uint32_t* rowoff, uint32_t* rows, uint64_t* words,
+                              uint32_t epoch, hipStream_t s) {
+  const uint64_t blocks = (groups + kLossyPerBlock - 1) / kLossyPerBlock;
+  if (blocks == 0 || blocks > 0xffffffffull) return hipErrorInvalidValue;
+  launch(kKReconstruct, k_lossy_list1, dim3(static_cast<uint32_t>(blocks)), dim3(1024), 0, s, present, groups, nmask,
+         dmask, d, words, epoch, list, count, rowoff, rows);
+  return hipGetLastError();
+}
+
 hipError_t launch_lossy_list(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t d,
                              uint32_t* list, uint32_t* count, uint32_t* rowoff, uint32_t* rows, uint32_t* work,
                              hipStream_t s) {

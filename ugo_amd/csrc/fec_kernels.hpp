@@ -78,6 +78,12 @@ constexpr uint32_t kLossyPerBlock = 4096;
 hipError_t launch_lossy_list(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t d,
                              uint32_t* list, uint32_t* count, uint32_t* rowoff, uint32_t* rows, uint32_t* work,
                              hipStream_t s);
+// The same in one launch: `words` = one u64 per tile of context-owned memory
+// (zeroed once), reused by the calls of one stream with a new `epoch` each
+// (never 0).
+hipError_t launch_lossy_list1(const uint64_t* present, uint64_t groups, uint64_t nmask, uint64_t dmask, uint32_t d,
+                              uint32_t* list, uint32_t* count, uint32_t* rowoff, uint32_t* rows, uint64_t* words,
+                              uint32_t epoch, hipStream_t s);
 // Dense rows (group stride == S, no padding; k_apply_pd): MODE 1 / 2, d <= 16
 // (dmax 4..16), p <= 4, S >= kDenseMinS (a wave's 63 chunks span at most one
 // group boundary).  a.base = row 0 of group a.g0, 16-B aligned; a.items =

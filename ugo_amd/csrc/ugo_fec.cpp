@@ -95,6 +95,15 @@ struct ugo_fec {
   // the call id), and this context's call counter
   unsigned long long* d_rxseen = nullptr;
   unsigned long long rx_calls = 0;
+  // one-launch lossy list (k_lossy_list1): per stream, the tiles' epoch-tagged
+  // count words (context-owned, zeroed once) and that stream's call epoch
+  struct LossyWords {
+    hipStream_t s;
+    uint64_t* words;
+    size_t tiles;
+    uint32_t epoch;
+  };
+  std::vector<LossyWords> lossy_words;
   size_t zc_groups = 0;
   // d+p > 64: decode descriptors built on the host, one per erasure pattern
   // (klauspost caches its inversions per pattern the same way)
@@ -229,6 +238,7 @@ void free_ctx(ugo_fec* c) {
   (void)hipFree(c->d_encdesc);
   (void)hipFree(c->d_table);
   (void)hipFree(c->d_rxseen);
+  for (auto& lw : c->lossy_words) (void)hipFree(lw.words);
   timer_release(c);
   (void)hipHostFree(c->d_zc_mask);
   (void)hipHostFree(c->d_zc_status);
@@ -1094,7 +1104,12 @@ int rx_assemble_dev(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const u
 }
 
 
-// ugo_fec_lossy_groups on device views.
+// ugo_fec_lossy_groups on device views: one launch (k_lossy_list1), or the
+// two-launch form (k_lossy_count -> k_lossy_write) in A/B builds.
+#ifndef UGO_LOSSY_ONE_LAUNCH
+#define UGO_LOSSY_ONE_LAUNCH 1
+#endif
+constexpr bool kLossyOneLaunch = UGO_LOSSY_ONE_LAUNCH != 0;
 int lossy_list_dev(ugo_fec* c, const uint64_t* present, size_t groups, unsigned flags, uint32_t* list,
                    uint32_t* count, hipStream_t s, uint32_t* rowoff = nullptr, uint32_t* rows = nullptr) {
   if (groups == 0) {
@@ -1105,6 +1120,34 @@ int lossy_list_dev(ugo_fec* c, const uint64_t* present, size_t groups, unsigned 
   const uint64_t dmask =
       (flags & UGO_FEC_RECONSTRUCT_DATA_ONLY) && c->d < 64 ? ((1ull << c->d) - 1) : ~0ull;  // d = 64: p = 0
   const size_t blocks = (groups + ugo::kern::kLossyPerBlock - 1) / ugo::kern::kLossyPerBlock;
+  if (kLossyOneLaunch) {
+    // the stream's count words (made, or grown, on first use; zeroed once, on the call's own stream so the
+    // zeroing is ordered before the kernel -- hipMemset is asynchronous to a non-blocking stream -- and
+    // epoch 0 is never used)
+    ugo_fec::LossyWords* lw = nullptr;
+    for (auto& e : c->lossy_words)
+      if (e.s == s) lw = &e;
+    if (!lw || lw->tiles < blocks || lw->epoch == 0xffffffffu) {
+      if (lw && hipStreamSynchronize(s) != hipSuccess) return UGO_FEC_ERR_HIP;
+      const size_t tiles = std::max<size_t>(blocks, lw ? 2 * lw->tiles : 64);
+      uint64_t* w = nullptr;
+      if (hipMalloc(&w, tiles * sizeof(uint64_t)) != hipSuccess) return UGO_FEC_ERR_HIP;
+      if (hipMemsetAsync(w, 0, tiles * sizeof(uint64_t), s) != hipSuccess) {
+        (void)hipFree(w);
+        return UGO_FEC_ERR_HIP;
+      }
+      if (lw) {
+        (void)hipFree(lw->words);
+        *lw = ugo_fec::LossyWords{s, w, tiles, 0};
+      } else {
+        c->lossy_words.push_back(ugo_fec::LossyWords{s, w, tiles, 0});
+        lw = &c->lossy_words.back();
+      }
+    }
+    const uint32_t epoch = ++lw->epoch;
+    return hip_status(ugo::kern::launch_lossy_list1(present, groups, nmask, dmask, static_cast<uint32_t>(c->d), list,
+                                                    count, rowoff, rows, lw->words, epoch, s));
+  }
   void* work = nullptr;
   int st = scratch_alloc(c, 2 * blocks * sizeof(uint32_t), s, &work);
   if (st) return st;
