@@ -106,7 +106,53 @@ def summarise(d):
         print(json.dumps({"union_busy": kind, "ms": round(tot / 1e6, 3)}))
 
 
+def per_call(d):
+    """Every call of the trace (split at the 10-ms gaps run() leaves): span,
+    H2D busy / union / first-start / last-end, the gaps between consecutive H2D
+    copies, and the tail after the last H2D (recovery + D2H)."""
+    import csv
+
+    ev = []
+    for f in glob.glob(d + "/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            ev.append(("K", r["Kernel_Name"][:30], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), 0))
+    for f in glob.glob(d + "/**/*memory_copy_trace.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            nb = int(r.get("Bytes") or r.get("Size") or 0)
+            ev.append(("C", r.get("Direction", r.get("Operation", "?")), int(r["Start_Timestamp"]),
+                       int(r["End_Timestamp"]), nb))
+    ev.sort(key=lambda e: e[2])
+    calls, cur, end = [], [], 0
+    for e in ev:
+        if cur and e[2] - end > 3_000_000:
+            calls.append(cur)
+            cur = []
+        cur.append(e)
+        end = max(end, e[3])
+    calls.append(cur)
+    for k, c in enumerate(calls):
+        t0 = c[0][2]
+        h2d = sorted((s, e, nb) for kind, what, s, e, nb in c if kind == "C" and "HOST_TO_DEVICE" in what.upper()
+                     and e - s > 200_000)  # the ring copies (the trace carries no sizes): > 0.2 ms each
+        d2h = [(s, e, nb) for kind, what, s, e, nb in c if kind == "C" and "DEVICE_TO_HOST" in what.upper()]
+        gaps = [round((h2d[i + 1][0] - h2d[i][1]) / 1e3, 1) for i in range(len(h2d) - 1)]
+        span = max(e for *_, s, e, nb in c) - t0
+        rates = [round((e - s) / 1e6, 3) for s, e, nb in h2d]
+        print(json.dumps({
+            "call": k, "span_ms": round(span / 1e6, 3), "events": len(c),
+            "to_first_h2d_ms": round((h2d[0][0] - t0) / 1e6, 3) if h2d else None,
+            "h2d_n": len(h2d), "h2d_busy_ms": round(sum(e - s for s, e, _ in h2d) / 1e6, 3),
+            "h2d_ms": rates, "h2d_gaps_us": gaps,
+            "last_h2d_end_ms": round((h2d[-1][1] - t0) / 1e6, 3) if h2d else None,
+            "d2h_busy_ms": round(sum(e - s for s, e, _ in d2h) / 1e6, 3),
+            "tail_after_last_h2d_ms": round((t0 + span - h2d[-1][1]) / 1e6, 3) if h2d else None,
+            "kernel_busy_ms": round(sum(e - s for kind, _, s, e, _ in c if kind == "K") / 1e6, 3)}))
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--calls":
+        per_call(sys.argv[2])
+        sys.exit(0)
     if len(sys.argv) > 2 and sys.argv[1] == "--summarise":
         summarise(sys.argv[2])
     else:

@@ -1,7 +1,8 @@
 """bench.py's service_interference leg on its own (a resident per-call service
 block against the bench step and a pinned-host encode on the same GPU), for
 A/B runs of library builds (UGO_FEC_LIB).  SVI_TX=1: one host TX call first, on
-a context left open through the samples; SVI_EXTRA=k,prio: k more torch
+a context left open through the samples (SVI_COPYQ=1: with the low-priority
+copy queue on that context); the line carries the process's KFD queues; SVI_EXTRA=k,prio: k more torch
 streams of that priority alive through the samples.  Prints one JSON line.  Not product
 code.
 
@@ -48,6 +49,8 @@ def main():
         wl = fec.host_alloc(G * n * 2).view(np.uint16)
         pk[:] = 1
         ln[:] = 1476
+        if os.environ.get("SVI_COPYQ"):  # the opt-in low-priority H2D stream on that context
+            tx.set_host_copy_queue(True)
         tx.tx_assemble_host(pk, ln, wire, wl, max_len=1476)
         keep = [tx, pk, ln, wire, wl]
     try:
@@ -60,7 +63,27 @@ def main():
                 fec.host_free(b.reshape(-1).view(np.uint8))
             keep[0].close()
     res["label"] = label
+    res["hsa_queues"] = kfd_queues()
+    res["gpu_max_hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")
     print(json.dumps(res))
+
+
+def kfd_queues():
+    """The process's KFD user queues (/sys/class/kfd/kfd/proc/<pid>/queues), each
+    with whatever attributes the node exposes; None where the node is absent."""
+    base = f"/sys/class/kfd/kfd/proc/{os.getpid()}/queues"
+    if not os.path.isdir(base):
+        return None
+    out = []
+    for q in sorted(os.listdir(base), key=lambda x: int(x) if x.isdigit() else 0):
+        attrs = {}
+        for a in sorted(os.listdir(os.path.join(base, q))):
+            try:
+                attrs[a] = open(os.path.join(base, q, a)).read().strip()[:40]
+            except OSError as ex:
+                attrs[a] = f"<{ex.errno}>"
+        out.append({"id": q, **attrs})
+    return out
 
 
 if __name__ == "__main__":

@@ -529,6 +529,57 @@ __global__ __launch_bounds__(256) void k_rx_begin(const uint64_t* present, uint6
   if (seen && __any(any != 0) && (threadIdx.x & 63u) == 0) atomicMax(seen, call);
 }
 
+// Frame rows -> payload rows: out row r = bytes [off, off + S) of src row r,
+// zeros to round_up(S, 16); one thread per 16-B output chunk (two aligned
+// source chunks, funnel shift).  The host RX path's recovered rows on their
+// way out (only those rows: ~4 % of a ring's bytes), so the D2H copy reads
+// 16-B aligned rows.
+__global__ __launch_bounds__(256) void k_shift_rows(const uint8_t* src, uint64_t spitch, uint32_t off, uint8_t* dst,
+                                                    uint64_t dpitch, uint32_t S, uint64_t rows) {
+  const uint32_t nq = (S + 15u) / 16u;
+  const uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  if (i >= rows * nq) return;
+  const uint64_t r = i / nq;
+  const uint32_t q = static_cast<uint32_t>(i - r * nq);
+  const uint32_t o = 16u * q + off;      // first source byte of this chunk
+  const uint32_t a0 = o & ~15u, sh = o & 15u;
+  const uint8_t* row = src + r * spitch;
+  const u32x4 A = ld16(row + a0);
+  u32x4 B = {0u, 0u, 0u, 0u};
+  if (sh && a0 + 16u < off + S) B = ld16(row + a0 + 16u);  // the next chunk holds bytes of this one
+  const uint32_t w8[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+  uint32_t w[4];
+  const uint32_t dw = sh >> 2, bs = sh & 3u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)  // select without runtime-indexed arrays (dw < 4)
+      if (dw == static_cast<uint32_t>(k)) {
+        lo = w8[j + k];
+        hi = w8[j + k + 1 < 8 ? j + k + 1 : 7];
+      }
+    w[j] = __builtin_amdgcn_alignbyte(hi, lo, bs);
+  }
+  const uint32_t L = S - 16u * q;  // payload bytes of this chunk (zeros past S)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t b0 = 4u * j;
+    const uint32_t k = L >= b0 + 4u ? 4u : (L > b0 ? L - b0 : 0u);
+    w[j] &= k >= 4u ? 0xffffffffu : ((1u << (8u * k)) - 1u);
+  }
+  *reinterpret_cast<u32x4*>(dst + r * dpitch + 16u * q) = u32x4{w[0], w[1], w[2], w[3]};
+}
+
+hipError_t launch_shift_rows(const uint8_t* src, uint64_t spitch, uint32_t off, uint8_t* dst, uint64_t dpitch,
+                             uint32_t S, uint64_t rows, hipStream_t s) {
+  const uint64_t items = rows * ((S + 15u) / 16u);
+  if (items == 0) return hipSuccess;
+  launch(kKRx, k_shift_rows, dim3(static_cast<uint32_t>((items + 255) / 256)), dim3(256), 0, s, src, spitch, off, dst,
+         dpitch, S, rows);
+  return hipGetLastError();
+}
+
 hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t groups, uint32_t* dup, uint32_t* win,
                            uint64_t words, unsigned long long* seen, unsigned long long call, hipStream_t s) {
   uint64_t blocks = (groups + 255) / 256;

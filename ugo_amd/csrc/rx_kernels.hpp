@@ -47,6 +47,10 @@ hipError_t launch_rx_begin(const uint64_t* present, uint64_t* prev, uint64_t gro
 hipError_t launch_rx_fill(uint32_t* win, uint64_t words, const uint32_t* gate, hipStream_t s);
 hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s);
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s);
+// rows x [S bytes at src + r*spitch + off] -> dst + r*dpitch, zeros to round_up(S, 16)
+// (src, spitch, dst, dpitch 16-B aligned; each src row readable to round_up(off + S, 16)).
+hipError_t launch_shift_rows(const uint8_t* src, uint64_t spitch, uint32_t off, uint8_t* dst, uint64_t dpitch,
+                             uint32_t S, uint64_t rows, hipStream_t s);
 
 }  // namespace kern
 }  // namespace ugo

@@ -1047,11 +1047,17 @@ size_t rx_frame_fill(const uint8_t* shards, size_t S, size_t rstride, size_t gst
   return layout_disjoint(w64, rstride, rows, gstride, groups) ? w64 : w16;
 }
 
+// Stream-ordered scratch of one rx_assemble call: presence snapshot [groups] u64 | claim words
+// [groups][n] u32 | dup flag.
+size_t rx_scratch_bytes(const ugo_fec* c, size_t groups) {
+  return groups * sizeof(uint64_t) + (groups * size_t(c->n) + 16) * sizeof(uint32_t);
+}
+
 // rx_assemble on device views (arguments checked by the caller).
 int rx_assemble_dev(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
                     const uint8_t* pad, uint64_t first_group, size_t groups, uint8_t* shards, size_t S,
                     size_t row_stride, size_t group_stride, uint64_t* present, uint32_t* stats, hipStream_t s,
-                    bool frame = false) {
+                    bool frame = false, void* call_scratch = nullptr) {
   ugo::kern::RxArgs a{};
   a.frame = frame ? 1u : 0u;
   a.fill = static_cast<uint32_t>(rx_frame_fill(shards, S, row_stride, group_stride, size_t(c->n), groups));
@@ -1074,8 +1080,10 @@ int rx_assemble_dev(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const u
   // only then -- gated on the flag, on the device -- claim and re-place.
   // scratch: presence snapshot [groups] u64 | claim words [groups][n] u32 | dup flag
   const uint64_t words = groups * uint64_t(c->n);
-  void* scratch = nullptr;
-  int st = scratch_alloc(c, groups * sizeof(uint64_t) + (words + 16) * sizeof(uint32_t), s, &scratch);
+  // call_scratch: the caller's (rx_recover_host: one block for all its chunk calls, which run in order on s),
+  // rx_scratch_bytes(c, groups) of it
+  void* scratch = call_scratch;
+  int st = call_scratch ? UGO_FEC_OK : scratch_alloc(c, rx_scratch_bytes(c, groups), s, &scratch);
   if (st) return st;
   uint64_t* prev = static_cast<uint64_t*>(scratch);
   uint32_t* win = reinterpret_cast<uint32_t*>(prev + groups);
@@ -1099,7 +1107,7 @@ int rx_assemble_dev(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const u
   if (!st) st = hip_status(ugo::kern::launch_rx_scatter(a, s));
   if (!st) st = hip_status(ugo::kern::launch_rx_claim(f, s));
   if (!st) st = hip_status(ugo::kern::launch_rx_scatter(f, s));
-  const int fr = scratch_free(c, scratch, s);
+  const int fr = call_scratch ? UGO_FEC_OK : scratch_free(c, scratch, s);
   return st ? st : fr;
 }
 
@@ -1751,6 +1759,10 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
 #define UGO_RX_FRAMES 1
 #endif
 constexpr bool kRxFrames = UGO_RX_FRAMES != 0;
+#ifndef UGO_RX_STAGE_MIB
+#define UGO_RX_STAGE_MIB 64
+#endif
+constexpr size_t kRxStageBytes = size_t(UGO_RX_STAGE_MIB) << 20;  // ring bytes per H2D copy at most
 
 int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride, const uint16_t* lens, size_t npk,
                             const uint8_t* pad, uint64_t first_group, size_t groups, size_t S, uint64_t* present_out,
@@ -1777,18 +1789,23 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   const size_t fo = kRxFrames ? 6 : 0, FS = S + fo;
   // (frame rows at a 64-B pitch: whole 64-B lines per row, rx_frame_fill)
   const size_t n = size_t(c->n), pitch = round_up(FS, kRxFrames ? 64 : 16), slots = size_t(std::min(c->d, c->p));
-  // packets per chunk: at most a 64-MiB stage, at least 4 chunks so copies and assembly overlap, and
-  // at most 32 chunks (the chunks grow with the ring past that: see kTxMaxChunks)
-  const size_t cpk = std::max<size_t>({size_t(1), (npk + 31) / 32, std::min((npk + 3) / 4, kStageBytes / slot_stride)});
+  // packets per chunk: at most a kRxStageBytes stage, at least 4 chunks so copies and assembly overlap,
+  // and at most 32 chunks (the chunks grow with the ring past that: see kTxMaxChunks)
+  const size_t cpk =
+      std::max<size_t>({size_t(1), (npk + 31) / 32, std::min((npk + 3) / 4, kRxStageBytes / slot_stride)});
   const size_t stage_bytes = round_up(cpk * slot_stride, 256);
   // every recovered row fits: a recoverable group rebuilds at most min(d, p) data rows
   const size_t max_rows = max_out ? groups * slots : 1;
   // one scratch block: batch | present | list | row offsets | counts, stats | row ids | rows | pad | lens | ring stages
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off = round_up(off + bytes, 256); return o; };
+  // (+ the chunk calls' rx_assemble scratch, shared: they run in order on s0; + frame rows: the
+  // recovered rows shifted to payload rows at a 16-B pitch for the D2H)
+  const size_t opitch = round_up(S, 16);
   const size_t o_batch = take(n * groups * pitch), o_pres = take(groups * 8), o_list = take(groups * 4),
                o_roff = take(groups * 4), o_ctl = take(64), o_rid = take(max_rows * 4), o_out = take(max_rows * pitch),
                o_pad = take(pad ? slot_stride : 16), o_lens = take(std::max<size_t>(npk, 1) * 2),
+               o_rxs = take(rx_scratch_bytes(c, groups)), o_pk = take(kRxFrames ? max_rows * opitch : 16),
                o_stage = take(kRxStages * stage_bytes);
   uint8_t* base = nullptr;
   st = scratch_alloc(c, off, s0, reinterpret_cast<void**>(&base));
@@ -1858,7 +1875,7 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
     if (hipStreamWaitEvent(s0, ev[b], 0) != hipSuccess) return UGO_FEC_ERR_HIP;
     // (chunk 0's wait covers the lengths' copy, earlier on the same stream; later chunks follow it on s0)
     st = rx_assemble_dev(c, base + o_stage + b * stage_bytes, slot_stride, dlens + p0, m, dpad, first_group, groups,
-                         batch, S, groups * pitch, pitch, dpres, dstats, s0, kRxFrames);
+                         batch, S, groups * pitch, pitch, dpres, dstats, s0, kRxFrames, base + o_rxs);
     if (st) return st;
     if (hipEventRecord(ev[kRxStages + b], s0) != hipSuccess) return UGO_FEC_ERR_HIP;
   }
@@ -1878,7 +1895,18 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   hipError_t e = hipSuccess;
   if (w) {  // only the recovered rows cross PCIe: w rows of S bytes
     e = hipMemcpyAsync(out_index, drid, w * 4, hipMemcpyDeviceToHost, s0);
-    if (e == hipSuccess) e = hipMemcpy2DAsync(out, out_row_stride, dout + fo, pitch, S, w, hipMemcpyDeviceToHost, s0);
+    const uint8_t* rows = dout;
+    size_t rpitch = pitch;
+    if (kRxFrames && e == hipSuccess) {
+      // frame rows -> 16-B aligned payload rows first: a 2-D copy from rows at column 6 ran as the
+      // runtime's copyBufferRect kernel at ~16 GB/s (2.75 ms for 32k rows, profiles/r6/host_rx_trace),
+      // from aligned rows it is a DMA copy at the link's rate
+      e = ugo::kern::launch_shift_rows(dout, pitch, static_cast<uint32_t>(fo), base + o_pk, opitch,
+                                       static_cast<uint32_t>(S), w, s0);
+      rows = base + o_pk;
+      rpitch = opitch;
+    }
+    if (e == hipSuccess) e = hipMemcpy2DAsync(out, out_row_stride, rows, rpitch, S, w, hipMemcpyDeviceToHost, s0);
   }
   if (e == hipSuccess && present_out) e = hipMemcpyAsync(present_out, dpres, groups * 8, hipMemcpyDeviceToHost, s0);
   if (e == hipSuccess && stats_out) e = hipMemcpyAsync(stats_out, dstats, 20, hipMemcpyDeviceToHost, s0);
