@@ -59,7 +59,9 @@ extern "C" {
  *    ugo_fec_tx_assemble_host. */
 /* 9: ugo_fec_rx_assemble_frames (frame rows: each placed row holds its
  *    decrypted packet, payload at column 6); ugo_fec_rx_recover_host runs on
- *    frame rows internally (same results). */
+ *    frame rows internally (same results); the low-priority host copy queue is
+ *    on by default, and the service pool holds at most 3 queues (8 hardware
+ *    queues per process, see ugo_fec_set_host_copy_queue). */
 #define UGO_FEC_ABI_VERSION 9
 
 /* Status codes.  1..5 map 1:1 onto the klauspost/reedsolomon error values
@@ -251,7 +253,10 @@ int ugo_fec_reconstruct_host(ugo_fec* ctx, uint8_t* shards, const uint64_t* pres
  * hipFree, which synchronizes the device) waits for it to leave, i.e. up to
  * idle_us after the last call.  Stream work does not: the block runs on a
  * stream of its own priority class, so it has a hardware queue no ordinary
- * stream shares (an ordinary stream placed on its queue would wait).
+ * stream shares (an ordinary stream placed on its queue would wait).  Those
+ * queues are a per-device pool of at most 3 (with GPU_MAX_HW_QUEUES = 4: the
+ * process stays within 8 hardware queues); a context that finds the pool
+ * leased serves its calls on the launch path.
  * Failure: a call the service cannot complete (a GPU fault, or no answer
  * within the watchdog timeout, 5 s by default) turns the service off, asks the
  * workgroup to leave and waits up to the grace period (5 s by default) for it
@@ -423,15 +428,18 @@ int ugo_fec_tx_assemble_host(ugo_fec* ctx, const uint8_t* pkts, size_t slot_in, 
  * same packets and lengths.  UGO_FEC_ERR_INVALID_ARG for any other value. */
 int ugo_fec_set_tx_host_route(ugo_fec* ctx, int route);
 
-/* on = 1: the host paths' H2D copy stream (ugo_fec_rx_recover_host,
- * ugo_fec_tx_assemble_host, the staged *_host paths) comes from the
- * low-priority stream class, whose hardware queues are a pool of their own, so
- * it never shares one with the context's kernel stream.  Measured: host TX
- * 26.5-26.6 ms for 65,536 (10+3) groups whatever streams the process made
- * before, against 26.5 ms in five of six process histories and 40.1 in the
- * sixth with on = 0 (the default); but the extra hardware queue slowed
- * concurrent device work 33-39 % in one process while a per-call service block
- * was resident.  Synchronizes and replaces the stream when it exists. */
+/* on = 1 (the default since ABI 9): the host paths' H2D copy stream
+ * (ugo_fec_rx_recover_host, ugo_fec_tx_assemble_host, the staged *_host paths)
+ * comes from the low-priority stream class, whose hardware queues are a pool of
+ * their own, so it never shares one with the context's kernel stream: host TX
+ * of 65,536 (10+3) groups runs 26.5-26.6 ms whatever streams the process made
+ * before, against 40.1 ms in some process histories with on = 0.  Hardware
+ * queues: a process past 8 of them runs oversubscribed (time-sliced), which
+ * costs concurrent work ~33 % while a per-call service block is resident; the
+ * library keeps its own footprint within 8 -- the normal class, this one low
+ * queue, at most 3 service queues with GPU_MAX_HW_QUEUES = 4 -- and an
+ * application that adds priority streams of its own should count them
+ * (DESIGN.md §6.2).  Synchronizes and replaces the stream when it exists. */
 int ugo_fec_set_host_copy_queue(ugo_fec* ctx, int on);
 
 /* RC4 keystream (crypto/rc4 KSA + PRGA) of a key, host memory: the pad above

@@ -444,4 +444,63 @@ def test_service_more_contexts_than_hardware_queues(gpu):
     assert not any(t.is_alive() for t in ts)
     assert not errors, errors
     assert len(served) == nctx
-    assert 1 <= sum(served) <= 4, served
+    assert 1 <= sum(served) <= 3, served
+
+
+_QUEUE_PROBE = r"""
+import ctypes, sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+from ugo_amd import fec
+d, p, G, n, slot = 10, 3, 512, 13, 1488
+tx = fec.New(d, p)
+pk = fec.host_alloc(G * d * slot).reshape(G * d, slot); pk[:] = 1
+ln = fec.host_alloc(G * d * 2).view(np.uint16); ln[:] = 1476
+wire = fec.host_alloc(G * n * slot).reshape(G * n, slot)
+wl = fec.host_alloc(G * n * 2).view(np.uint16)
+tx.tx_assemble_host(pk, ln, wire, wl, max_len=1476)   # the default low-priority copy queue
+encs, bufs = [], []
+for k in range(6):                                    # more service contexts than the pool holds
+    e = fec.New(d, p)
+    e.service_start(idle_us=200000)
+    b = fec.host_alloc(n * 1472).reshape(1, n, 1472)
+    e.encode_host(b, 1470)
+    encs.append(e); bufs.append(b)
+for s in [torch.cuda.Stream() for _ in range(6)]:     # ordinary streams of the application
+    with torch.cuda.stream(s):
+        torch.ones(16, device="cuda").sum()
+torch.cuda.synchronize()
+for e in encs:
+    e.service_stop(); e.close()
+tx.close()
+print("done")
+"""
+
+
+def test_process_hw_queue_footprint(gpu, tmp_path):
+    """The library keeps the process within 8 hardware queues (past 8 the GPU's
+    scheduler time-slices them, and a resident service block then cost
+    concurrent work ~33 %): host TX with the default
+    low-priority copy queue, six contexts starting the per-call service, six
+    ordinary torch streams -- HIP's own queue log (AMD_LOG_LEVEL=3, in a child
+    process) shows at most 8 distinct hardware queues, one low-priority, at
+    most 3 high-priority."""
+    import os
+    import re
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "probe.py"
+    script.write_text(_QUEUE_PROBE)
+    env = dict(os.environ, AMD_LOG_LEVEL="3", GPU_MAX_HW_QUEUES="4")
+    r = subprocess.run([sys.executable, str(script), root], capture_output=True, text=True, env=env, timeout=180)
+    assert r.returncode == 0 and "done" in r.stdout, r.stderr[-2000:]
+    hw = {}
+    for m in re.finditer(r"to map on HWq=(0x[0-9a-f]+) with size \d+ with priority (\d)", r.stderr + r.stdout):
+        hw.setdefault(m.group(1), m.group(2))
+    assert hw, "no queue creation in HIP's log (log format changed?)"
+    prio = [v for v in hw.values()]
+    assert len(hw) <= 8, (len(hw), sorted(prio))
+    assert prio.count("0") == 1 and prio.count("2") <= 3, sorted(prio)

@@ -158,16 +158,20 @@ def test_tx_assemble_host_vs_sender_loop(gpu, d, p, max_len, G, key, pinned, rou
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("route,copy_queue", [("copy", False), ("mapped", False), ("copy", True)])
-def test_tx_assemble_host_many_chunks_matches_device_path(gpu, route, copy_queue):
+@pytest.mark.parametrize("route,copy_queue,service", [("copy", False, False), ("mapped", False, False),
+                                                     ("copy", True, False), ("copy", True, True)])
+def test_tx_assemble_host_many_chunks_matches_device_path(gpu, route, copy_queue, service):
     """A batch past tx_assemble_host's chunk cap (32 chunks per call; the
     chunks grow with the batch): 3,400 (32,8) groups of up to 9,006-B packets
     in pinned memory, against the device-resident tx_assemble (itself checked
     against the sender loop above) -- every wire packet within its length,
     the wire lengths and the statuses, header-only and bad groups included.
     Two calls on the context, each checked; copy_queue: the first two with the
-    low-priority copy stream (ugo_fec_set_host_copy_queue), a third after
-    switching it off again."""
+    low-priority copy stream (ugo_fec_set_host_copy_queue, the default), a
+    third after switching it off again.  service: another context's per-call
+    service block stays resident (polling, 2-s idle window) through the calls,
+    as in a process where connections use the drop-in route beside the batch
+    route."""
     d, p, max_len, G = 32, 8, 9006, 3400
     n, slot = d + p, (max_len + 15) // 16 * 16
     enc = fec.New(d, p)
@@ -192,7 +196,14 @@ def test_tx_assemble_host_many_chunks_matches_device_path(gpu, route, copy_queue
         bufs.append(a)
         return a
 
+    svc = None
     try:
+        if service:
+            svc = fec.New(10, 3)  # a (10,3) connection: the service serves codes up to d = 16
+            svc.service_start(idle_us=2_000_000)
+            one = pinned(13 * 16).reshape(1, 13, 16)
+            one[:] = 3
+            svc.encode_host(one, 16)  # served: the block is now resident
         hp = pinned(G * d * slot).reshape(G * d, slot)
         hl = pinned(G * d * 2).view(np.uint16)
         hw = pinned(G * n * slot).reshape(G * n, slot)
@@ -215,6 +226,9 @@ def test_tx_assemble_host_many_chunks_matches_device_path(gpu, route, copy_queue
             assert torch.equal(got[keep], dw[keep]), f"call {call}"
             del got
     finally:
+        if svc is not None:
+            svc.service_stop()
+            svc.close()
         for a in bufs:
             fec.host_free(a)
 

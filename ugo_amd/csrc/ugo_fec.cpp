@@ -110,9 +110,10 @@ struct ugo_fec {
   std::unordered_map<std::string, std::vector<uint8_t>> wide_cache;
   int tx_route = 0;  // host TX wire route (ugo_fec_set_tx_host_route): 0 D2H copy, 1 mapped write
 #ifndef UGO_COPY_QUEUE_DEFAULT
-#define UGO_COPY_QUEUE_DEFAULT 0
+#define UGO_COPY_QUEUE_DEFAULT 1
 #endif
   bool host_copy_queue = UGO_COPY_QUEUE_DEFAULT != 0;  // ugo_fec_set_host_copy_queue: streams[1] low priority
+  bool streams_shared = false;  // streams[1] is the process-wide low-priority copy stream (not ours to destroy)
   size_t stage_groups = 0;  // groups per staging buffer
   size_t stage_pitch = 0;
   // launch timing (ugo_fec_timing_begin/end)
@@ -218,6 +219,7 @@ int build_desc(const ugo_fec* c, uint64_t mask, uint8_t* out) { return build_des
 int hip_status(hipError_t e) { return e == hipSuccess ? UGO_FEC_OK : UGO_FEC_ERR_HIP; }
 
 int svc_stop(ugo_fec* c);
+bool is_shared_stream(const ugo_fec* c, int i);
 
 void free_ctx(ugo_fec* c) {
   if (!c) return;
@@ -246,7 +248,7 @@ void free_ctx(ugo_fec* c) {
     (void)hipFree(c->d_stage[i]);
     (void)hipFree(c->d_mask[i]);
     (void)hipFree(c->d_status[i]);
-    if (c->streams[i]) (void)hipStreamDestroy(c->streams[i]);
+    if (c->streams[i] && !is_shared_stream(c, i)) (void)hipStreamDestroy(c->streams[i]);
   }
   // this context's async scratch frees still queued on the callers' streams
   for (auto& se : c->scratch_ev) {
@@ -563,17 +565,40 @@ int reconstruct_dev(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t
 // queue with the stream its D2H copies ran on, each D2H copy waited behind the
 // next chunk's H2D dependency and the two copy directions ran one after the
 // other: 40.5 ms instead of 26.6 for 65,536 (10+3) groups, depending on the
-// streams the process had made before (profiles/r5/host_tx_route_ab.md).  With
-// ugo_fec_set_host_copy_queue, stream 1 comes from the low-priority class, a
-// pool of its own: 26.5-26.6 ms in every history tried.  It is not the default:
-// the extra hardware queue cost concurrent device work 33-39 % in the bench's
-// process while a per-call service block was resident (1-4 % without it), and
-// with the normal class the host TX call ran 26.5 ms in five of six histories.
-hipError_t create_stream(const ugo_fec* c, int i, hipStream_t* s) {
-  if (i == 1 && c->host_copy_queue) {
+// streams the process had made before (profiles/r5/host_tx_route_ab.md).  So
+// stream 1 comes from the low-priority class, a pool of its own (26.5-26.6 ms
+// in every history tried; ugo_fec_set_host_copy_queue(ctx, 0) turns it off).
+// Round 5 kept it opt-in because concurrent device work ran 33-39 % slower with
+// it and a resident service block in one process; the cause was the process's
+// hardware-queue count, not this queue (svc_queue_cap: past 8 queues the
+// scheduler time-slices), and the library now stays within 8.
+// The low-priority copy stream is ONE per device for the whole process, shared
+// by every context: HIP gives each new low-priority stream a new hardware queue
+// up to GPU_MAX_HW_QUEUES, so per-context streams took the process from 8 to 11
+// hardware queues with a handful of contexts (test_process_hw_queue_footprint).
+// Contexts that share it serialize their H2D copies on it -- they share the
+// PCIe link anyway.  Never destroyed (process lifetime).
+hipStream_t shared_copy_stream(int device) {
+  static std::mutex mu;
+  static std::unordered_map<int, hipStream_t>* streams = new std::unordered_map<int, hipStream_t>();
+  std::lock_guard<std::mutex> lk(mu);
+  hipStream_t& s = (*streams)[device];
+  if (!s) {
     int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return hipErrorInvalidValue;
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least) != hipSuccess)
+      s = nullptr;
+  }
+  return s;
+}
+
+bool is_shared_stream(const ugo_fec* c, int i) { return i == 1 && c->streams[1] && c->streams_shared; }
+
+hipError_t create_stream(ugo_fec* c, int i, hipStream_t* s) {
+  if (i == 1 && c->host_copy_queue) {
+    *s = shared_copy_stream(c->device);
+    c->streams_shared = *s != nullptr;
+    return *s ? hipSuccess : hipErrorInvalidValue;
   }
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
@@ -775,12 +800,24 @@ SvcStreamPool& svc_pool() {
   return *p;
 }
 
+// The process's hardware queues: HIP keeps up to GPU_MAX_HW_QUEUES per
+// priority class (4 by default).  Past 8 queues in one process the GPU's
+// scheduler runs them oversubscribed (time-sliced), and with a service block
+// resident -- a queue that never idles -- concurrent work in the process ran
+// 32-33 % slower, whatever the queues were: 8 normal + 1 high, or 4 normal +
+// 4 high + 1 low; at 5-8 queues in any mix the cost was -3 to +2.5 %
+// (tools/svc_interference.py with HIP's queue log, profiles/r6/queues/).  So
+// the library's own footprint stays within 8: the normal class (shared with
+// every other stream of the process), the low-priority H2D copy queue of the
+// host paths, and at most 8 - normal - low service queues (3 by default).
+constexpr int kProcessHwQueues = 8;
 int svc_queue_cap() {
   static const int cap = [] {
     int q = 4;  // HIP's default GPU_MAX_HW_QUEUES
     if (const char* env = std::getenv("GPU_MAX_HW_QUEUES"))
       if (std::atoi(env) > 0) q = std::atoi(env);
-    return std::min(q, 32);
+    q = std::min(q, 32);
+    return std::max(1, std::min(q, kProcessHwQueues - q - 1));
   }();
   return cap;
 }
@@ -944,10 +981,8 @@ int svc_stop(ugo_fec* c) {
 // streams overlap (copy engines in both directions + compute).
 int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t groups, size_t S,
               size_t pitch, bool recon, unsigned flags, int8_t* status) {
-  int st = ensure_stage(c, pitch);
-  if (st) return st;
+  int st = UGO_FEC_OK;
   const size_t gbytes = size_t(c->n) * pitch;
-  const size_t per = c->stage_groups;
   std::vector<int8_t> tmp_status;
   if (recon && !status) {
     tmp_status.resize(groups);
@@ -981,11 +1016,18 @@ int host_path(ugo_fec* c, uint8_t* shards, const uint64_t* present, size_t group
   // rows and writing the parity rows through the mapping, one synchronize --
   // instead of the three-copy pipeline, whose DMA only wins on large batches.
   if (!recon && mapped && groups * gbytes <= kZeroCopyEncodeBytes) {
+    if (!c->streams[0] && hipStreamCreateWithFlags(&c->streams[0], hipStreamNonBlocking) != hipSuccess)
+      return UGO_FEC_ERR_HIP;
     hipStream_t s = c->streams[0];
     st = encode_dev(c, mapped, groups, S, interleaved(c, pitch), s);
     if (st) return st;
     return hip_status(hipStreamSynchronize(s));
   }
+  // staged (pageable batches, large pinned encodes): the stage buffers and streams only now -- a
+  // context served by the service or zero-copy (one per connection) never holds 3 x 64 MiB of stage
+  st = ensure_stage(c, pitch);
+  if (st) return st;
+  const size_t per = c->stage_groups;
   size_t chunk = 0;
   for (size_t g0 = 0; g0 < groups; g0 += per, ++chunk) {
     const int si = static_cast<int>(chunk % kStreams);
@@ -2074,9 +2116,11 @@ int ugo_fec_set_host_copy_queue(ugo_fec* c, int on) {
   DeviceGuard g(c->device);
   if (!g.ok) return UGO_FEC_ERR_NO_DEVICE;
   if (c->streams[1]) {  // made again, from the other class, at the next host-path call
-    if (hipStreamSynchronize(c->streams[1]) != hipSuccess || hipStreamDestroy(c->streams[1]) != hipSuccess)
+    if (hipStreamSynchronize(c->streams[1]) != hipSuccess ||
+        (!is_shared_stream(c, 1) && hipStreamDestroy(c->streams[1]) != hipSuccess))
       return UGO_FEC_ERR_HIP;
     c->streams[1] = nullptr;
+    c->streams_shared = false;
   }
   c->host_copy_queue = on == 1;
   return UGO_FEC_OK;
