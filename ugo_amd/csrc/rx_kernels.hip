@@ -337,6 +337,14 @@ __global__ __launch_bounds__(256) void k_rx_place_h(RxArgs a) {
 // a combination of the survivors' headers and are ignored.  This is the frame
 // TX already keeps (k_tx_c: a lane holds packet bytes [16m, 16m + 16)).
 // Presence, first-copy rule, stats and gated passes as k_rx_place_h.
+// Measured (round 6, tools/rx_frames_ab.py, one box, same storage): 2.4-4 %
+// under the payload kernel; residency 3 blocks/CU (0.512 vs 0.539-0.553 ms at
+// 5 or uncapped, pitch 1488); rows at a 64-B pitch written to whole lines
+// (1536 for S = 1470: 0.40-0.46 vs 0.51-0.55 ms at the 1488 pitch); the same
+// frames one chunk per thread over the whole ring (the P2 shape, every lane
+// loading its packet's header and length) 0.58-0.63 ms -- a dependent header
+// load per lane outweighs the cheaper store pattern
+// (profiles/r6/rx_frames/p2_one_chunk_per_thread_ab.jsonl).
 __device__ __forceinline__ u32x4 rx_keep(u32x4 v, uint32_t o, uint32_t lim) {
   // bytes at or past lim of the chunk at o become zero (only a packet's tail chunk)
   if (o + 16u <= lim) return v;
@@ -416,70 +424,6 @@ __global__ __launch_bounds__(256) void k_rx_frame_h(RxArgs a) {
     if (hl == 0) acct.issue(a, bstats, why, grp - a.first_group, row);
   }
   if (hl == 0) acct.settle(a, bstats);
-  if (a.stats) {
-    __syncthreads();
-    if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
-  }
-}
-
-// Frame rows, one 16-B chunk per thread over the whole ring (the P2 shape of
-// a wave stores 1 KiB of one or two rows, and the address unit
-// sees one store per lane instead of the half-wave form's passes).  Frame rows
-// make it possible: a lane's chunk lands at the offset it was read from, so a
-// lane needs only its packet's header and length (the same 16 + 2 bytes for
-// all its packet's lanes: one broadcast request each), not a neighbour's
-// bytes.  Thread t takes chunk t % nc of packet t / nc, nc = a.fill / 16 (the
-// row's written chunks, >= the slot's); the packet's chunk-0 lane does the
-// presence atomic and the stats.  Needs npk * nc < 2^32 (the caller checks).
-__global__ __launch_bounds__(256) void k_rx_frame_p2(RxArgs a) {
-  if (rx_gated_off(a)) return;
-  __shared__ uint32_t bstats[5];
-  if (threadIdx.x < 5) bstats[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t nc = a.fill / 16u;
-  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t i = t / nc, q = t - i * nc;
-  const uint32_t slot = static_cast<uint32_t>(a.slot);
-  const uint32_t FS = a.S + 6u;
-  const u32x4 zero = {0u, 0u, 0u, 0u};
-  uint32_t why = 5;
-  if (i < a.npk) {
-    const uint8_t* pk = a.wire + uint64_t(i) * a.slot;
-    const uint32_t len = min(static_cast<uint32_t>(a.lens[i]), slot);
-    const uint32_t lim = len >= 6u ? min(len, FS) : 0u;
-    const uint32_t o = 16u * q;
-    u32x4 v = zero;
-    if (o < lim) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(pk + o));
-    u32x4 h = zero;
-    if (lim) h = ld16(pk);
-    if (a.pad) {
-      h ^= ld16(a.pad);
-      if (o < lim) v ^= ld16(a.pad + o);
-    }
-    const uint32_t seqid = h.x, flag = h.y & 0xffffu;
-    why = 0;
-    if (len < 6u) why = 3;
-    else if (flag != 0xf1u && flag != 0xf2u) why = 1;  // ugo/conn.go:395
-    const uint32_t row = seqid % a.n;
-    const uint64_t grp = seqid / a.n;
-    if (!why && (grp < a.first_group || grp >= a.first_group + a.groups)) why = 2;
-    const uint64_t gs = grp - a.first_group;
-    if (!why && a.prev && ((a.prev[gs] >> row) & 1ull)) why = 4;  // an earlier call's seqid
-    if (!why && a.win && a.win[gs * a.n + row] != i) why = 4;       // not the first copy
-    if (!why)
-      __builtin_nontemporal_store(rx_keep(v, o, lim), reinterpret_cast<u32x4*>(a.shards + row * a.rstride +
-                                                                                gs * a.gstride + o));
-    if (q != 0 || a.fixup) {
-      why = 5;  // one lane per packet accounts for it
-    } else if (why == 0) {
-      const unsigned long long old = atomicOr(reinterpret_cast<unsigned long long*>(&a.present[gs]), 1ull << row);
-      if (a.dup && ((old >> row) & 1ull)) {
-        why = 4;
-        *a.dup = 1u;
-      }
-    }
-  }
-  if (why < 5) atomicAdd(&bstats[why], 1u);
   if (a.stats) {
     __syncthreads();
     if (threadIdx.x < 5 && bstats[threadIdx.x]) atomicAdd(&a.stats[threadIdx.x], bstats[threadIdx.x]);
@@ -699,11 +643,6 @@ hipError_t launch_rx_claim(const RxArgs& a, hipStream_t s) {
 #ifndef UGO_RX_FRAME_BLOCKS
 #define UGO_RX_FRAME_BLOCKS 3
 #endif
-#ifndef UGO_RX_FRAME_P2
-#define UGO_RX_FRAME_P2 1
-#endif
-constexpr bool kRxFrameP2 = UGO_RX_FRAME_P2 != 0;
-
 static uint32_t rx_frame_lds() {
   static const uint32_t cap = [] {
     if (UGO_RX_FRAME_BLOCKS <= 0) return 0u;
@@ -721,13 +660,6 @@ hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
   uint32_t blocks = rx_blocks(a);
   if (a.gate && blocks > kRxGatedBlocks) blocks = static_cast<uint32_t>(kRxGatedBlocks);
   if (blocks == 0) return hipSuccess;
-  // the placement pass one chunk per thread; a gated pass (the re-place, which mostly finds its gate
-  // closed) keeps the grid-stride form on kRxGatedBlocks blocks: a closed full grid would cost its dispatch
-  if (a.frame && kRxFrameP2 && !a.gate && a.npk * uint64_t(a.fill / 16u) < 0xffffffffull) {
-    const uint64_t pb = (a.npk * uint64_t(a.fill / 16u) + 255u) / 256u;
-    launch(kKRx, k_rx_frame_p2, dim3(static_cast<uint32_t>(pb)), dim3(256), 0, s, a);
-    return hipGetLastError();
-  }
   if (a.frame) {  // frame rows: no realignment (k_rx_frame_h)
     const uint32_t lds = rx_frame_lds();
     switch ((a.fill / 16u + 31u) / 32u) {
