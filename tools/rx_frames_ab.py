@@ -190,7 +190,73 @@ def same_storage(trials=6, reps=12):
     enc.close()
 
 
+def row_pad(trials=4, reps=10):
+    """Frame rows with the planar row stride padded (G*1536 + pad) on one
+    allocation per trial: does a pad between the 13 row streams pick the fast
+    placement mode?  Every pad is timed on the same storage in each trial."""
+    import torch
+
+    from ugo_amd import fec
+
+    d, p, n, S, slot, G = 10, 3, 13, 1470, 1488, 65536
+    pads = [0, 256, 4096, 65536 + 256, (1 << 20) + 4096, (2 << 20) + 64 * 1536]
+    dev = torch.device("cuda:0")
+    enc = fec.New(d, p)
+    pad_ks = torch.frombuffer(bytearray(fec.rc4_keystream(b"1234567890123456", slot)), dtype=torch.uint8).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(0x99)
+    rx_id = fec.KERNEL_IDS["rx_assemble"]
+    seq = torch.arange(G * n, device=dev, dtype=torch.int64)
+    seq = seq[torch.rand(G * n, device=dev, generator=gen) >= 0.05]
+    orders = {"in_order": seq, "shuffled": seq[torch.randperm(seq.numel(), device=dev, generator=gen)]}
+    npk = seq.numel()
+    lens = torch.full((npk,), 1476, dtype=torch.int16, device=dev)
+    rx_bytes = npk * (1476 + S)
+    for t in range(trials):
+        dummy = torch.empty((1 + 53 * t) << 20, dtype=torch.uint8, device=dev)
+        span = n * G * 1536 + (n - 1) * max(pads)
+        flat = [torch.empty(span, dtype=torch.uint8, device=dev) for _ in range(2)]
+        pres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
+        line = {"trial": t}
+        for order, sq in orders.items():
+            rings = []
+            for _ in range(2):
+                w = torch.randint(0, 256, (npk, slot), dtype=torch.uint8, device=dev, generator=gen)
+                hdr = torch.zeros((npk, 6), dtype=torch.uint8, device=dev)
+                for b in range(4):
+                    hdr[:, b] = ((sq >> (8 * b)) & 0xFF).to(torch.uint8)
+                hdr[:, 4] = torch.where(sq % n < d, 0xF1, 0xF2).to(torch.uint8)
+                w[:, :6] = hdr ^ pad_ks[:6]
+                rings.append(w)
+            res = {}
+            for pad in (pads if t % 2 == 0 else pads[::-1]):
+                rs = G * 1536 + pad
+                bats = [f.as_strided((n, G, 1536), (rs, 1536, 1)) for f in flat]
+
+                def rx(r, bats=bats):
+                    i = r % 2
+                    pres[i].zero_()
+                    enc.rx_assemble(rings[i], lens, bats[i], pres[i], shard_size=S, pad=pad_ks, frames=True)
+
+                for r in range(3):
+                    rx(r)
+                enc.timing_begin(16 * reps)
+                for r in range(reps):
+                    rx(r)
+                recs, _ = enc.timing_end()
+                ms = float(recs["ms"][recs["kernel"] == rx_id].sum()) / reps
+                res[str(pad)] = round(ms, 4)
+            line[order] = res
+            del rings
+        print(json.dumps(line), flush=True)
+        del flat, pres, dummy
+        torch.cuda.empty_cache()
+    enc.close()
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "pad":
+        row_pad(*(int(a) for a in sys.argv[2:4]))
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "same":
         same_storage(*(int(a) for a in sys.argv[2:4]))
     else:
