@@ -403,6 +403,31 @@ void host_rx_tx_paths(bool pinned) {
   uint32_t cnt = 0;
   EXPECT(hipMemcpy(&cnt, dcount, 4, hipMemcpyDeviceToHost) == hipSuccess);
   EXPECT(cnt == G);  // every group has a lost data row (group 7 listed, with no output)
+  // round 6: the same ring into frame rows (64-B pitch), its payload columns equal the payload rows'
+  {
+    const size_t fp = 1536;
+    uint8_t* fsh = nullptr;
+    uint64_t* fpres = nullptr;
+    EXPECT(hipMalloc(&fsh, n * G * fp) == hipSuccess && hipMalloc(&fpres, G * 8) == hipSuccess &&
+           hipMemset(fpres, 0, G * 8) == hipSuccess);
+    EXPECT(ugo_fec_rx_assemble_frames(ctx, dring, slot, drlens, keep.size(), dpad, 0, G, fsh, S, G * fp, fp, fpres,
+                                      nullptr, nullptr) == UGO_FEC_OK);
+    EXPECT(hipDeviceSynchronize() == hipSuccess);
+    std::vector<uint8_t> a(n * G * pitch), b(n * G * fp);
+    std::vector<uint64_t> pa(G), pb(G);
+    EXPECT(hipMemcpy(a.data(), dshards, a.size(), hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(b.data(), fsh, b.size(), hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(pa.data(), dpres, G * 8, hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(pb.data(), fpres, G * 8, hipMemcpyDeviceToHost) == hipSuccess);
+    EXPECT(pa == pb);
+    for (size_t g = 0; g < G; ++g)
+      for (size_t r = 0; r < n; ++r)
+        if ((pa[g] >> r) & 1) {  // a placed row (the list reconstruct above rebuilt none in place)
+          EXPECT(std::memcmp(&a[r * G * pitch + g * pitch], &b[r * G * fp + g * fp + 6], S) == 0);
+        }
+    (void)hipFree(fsh);
+    (void)hipFree(fpres);
+  }
   for (void* q : {static_cast<void*>(dshards), static_cast<void*>(dout), static_cast<void*>(dpres),
                   static_cast<void*>(dlist), static_cast<void*>(dcount), static_cast<void*>(dstats),
                   static_cast<void*>(dring), static_cast<void*>(drlens), static_cast<void*>(dpad)})
