@@ -299,6 +299,14 @@ __global__ __launch_bounds__(256) void k_tx_var(TxArgs a) {
 
 }  // namespace
 
+// Round 6 (VERDICT r5 follow-up): an LDS-staged form -- a block owning 1, 2
+// or 4 whole groups, reading their data packets as one contiguous span into
+// LDS, the parity columns from LDS, the wire packets out as one contiguous
+// span (every line of a 4-group span whole) -- was bit-identical and ran
+// 0.538-0.629 ms against this kernel's 0.455 on one box (256 / 512 threads,
+// profiles/r6/tx_lds_ab.jsonl): the phases of a block serialize, and whole
+// lines do not pay here (k_tx_c on 1536-B slots, every packet on lines of its
+// own, ran 416 vs 413 us on 1488-B ones, profiles/r5/txpmc_b/).  Dropped.
 // Residency cap for the (10,3) TX kernel: dynamic LDS it never touches limits
 // it to 2 blocks (8 waves) per CU.  Fewer requests in flight run its 10-read +
 // 13-write stream mix faster on a cold ring: 450.7 us at 2 blocks/CU, 464.6 at
