@@ -1337,11 +1337,13 @@ def lost_and_recoverable(pm, d, n):
 
 
 def payload_layout_case(enc, rings, lens, pad, fbats, fpres, flsts, fcnts, flouts, G, n, p, S, FS, ppitch,
-                        kernel_ms, reps):
+                        kernel_ms, reps, rx_ms):
     """The RX ring into the payload layout (ugo_fec_rx_assemble: [n][G][ppitch],
     the payload realigned to column 0) and its list recovery: checked equal to
     the frame layout's presence masks, lossy list and recovered payload columns
-    (fpres / flsts / fcnts / flouts of the frame run on rings[0]), then timed.
+    (fpres / flsts / fcnts / flouts of the frame run on rings[0]), then its
+    recovery timed (its placement time, rx_ms, comes from the caller's
+    alternating rounds).
     Its batches are views of the frame batches' storage (fbats, overwritten):
     placement time depends on which physical pages back a batch (up to 15 %
     between allocations of one process, tools/rx_frames_ab.py same), so both
@@ -1379,12 +1381,10 @@ def payload_layout_case(enc, rings, lens, pad, fbats, fpres, flsts, fcnts, flout
         for i in range(p):
             sel = (ed > i) & okg
             ok = ok and bool(torch.equal(outs[0][:k][sel, i, :S], flouts[0][:k][sel, i, 6:FS]))
-    rx_k = kernel_ms(rx, fec.KERNEL_IDS["rx_assemble"], reps)
-    for r in range(2):
-        rx(r)
     rec_k = kernel_ms(rec_list, fec.KERNEL_IDS["reconstruct"], reps)
-    return {"rows": f"[{n}][G][{ppitch}] payload at column 0 (rx_assemble)", "rx_assemble_ms": round(rx_k, 4),
-            "reconstruct_list_ms": round(rec_k, 4), "verify_eq_frames": ok}
+    return {"rows": f"[{n}][G][{ppitch}] payload at column 0 (rx_assemble)", "rx_assemble_ms": round(rx_ms, 4),
+            "reconstruct_list_ms": round(rec_k, 4), "verify_eq_frames": ok,
+            "timing": "rx_assemble_ms: the median of 4 rounds alternating with the frame rows' on the same storage"}
 
 
 def rx_tx_leg(args, dev_index, reps=12):
@@ -1497,7 +1497,26 @@ def rx_tx_leg(args, dev_index, reps=12):
         want = rings[0][pick, :FS] ^ pad[:FS]
         got = bats[0][sq % n, sq // n, :FS]
         ok = stats == [npk, 0, 0, 0, 0] and bool(torch.equal(got, want))
-        rx_k = kernel_ms(rx, fec.KERNEL_IDS["rx_assemble"], reps)
+        # frame rows and payload rows timed alternately, on the same storage (placement time moves with
+        # the physical pages a batch gets): the median of 4 rounds each
+        pbats = [b.view(-1)[:n * G * ppitch].view(n, G, ppitch) for b in bats]
+        ppres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
+
+        def prx(r):
+            i = r % 2
+            ppres[i].zero_()
+            enc.rx_assemble(rings[i], lens, pbats[i], ppres[i], shard_size=S, pad=pad)
+
+        tf, tp = [], []
+        for rnd in range(4):
+            for fn, acc in (((rx, tf), (prx, tp)) if rnd % 2 == 0 else ((prx, tp), (rx, tf))):
+                fn(0)
+                fn(1)
+                acc.append(kernel_ms(fn, fec.KERNEL_IDS["rx_assemble"], reps))
+        rx_k, prx_k = float(np.median(tf)), float(np.median(tp))
+        del pbats, ppres
+        for r in range(2):  # the frame rows back for the recovery below
+            rx(r)
         rx_w = wall_ms(rx, reps)
         rec_k = kernel_ms(rec, (fec.KERNEL_IDS["reconstruct"], fec.KERNEL_IDS["prepare"]), reps)
         m = pres[0].cpu().numpy().view(np.uint64)
@@ -1560,7 +1579,7 @@ def rx_tx_leg(args, dev_index, reps=12):
         # the payload layout (ugo_fec_rx_assemble: realigned payload rows at column 0) on the same rings,
         # checked against the frame rows, then timed with its list recovery
         pl = payload_layout_case(enc, rings, lens, pad, bats, pres, lsts, cnts, louts, G, n, p, S, FS, ppitch,
-                                 kernel_ms, reps)
+                                 kernel_ms, reps, prx_k)
         # ceilings: the compute-free twins of both forms on the same buffers (after the checks: wrong bytes)
         twin_ms = probe_recover_twin_ms(bats, outs, pres, None, None, G, FS, pitch, bats[0].stride(0),
                                         outs[0].stride(0), outs[0].stride(1), reps, stream.cuda_stream)
@@ -1588,6 +1607,8 @@ def rx_tx_leg(args, dev_index, reps=12):
             "verify_recover_data": ok_rd,
             "stats": stats, "verify_spot_4096": ok,
             "layout": "frames: [13][G][1536] rows = decrypted packets, payload at column 6 (rx_assemble_frames)",
+            "rx_rounds_ms": {"frames": [round(x, 4) for x in tf], "payload": [round(x, 4) for x in tp],
+                             "note": "alternating rounds on the same storage; rx_assemble_ms = median of frames"},
             "payload_layout": {**pl, "rx_frac": frac(rx_bytes, pl["rx_assemble_ms"]),
                                "reconstruct_list_frac": frac(rec_bytes, pl["reconstruct_list_ms"])}}
         del rings, bats, pres, outs, lsts, cnts, louts
