@@ -656,6 +656,27 @@ static uint32_t rx_frame_lds() {
   return cap;
 }
 
+// Residency cap of the payload place kernel too (round 6): 3 blocks per CU
+// by unused LDS, as the frame kernel -- against its VGPR-limited 5 waves per
+// SIMD the payload rows' gap to frame rows on the same storage shrank from
+// 1.1-1.7 % to 0.3-0.8 % in order (4 blocks: 0.8-1.0 %), one box, three
+// allocations (profiles/r6/rx_frames/place_cap_ab.jsonl).  0: no cap.
+#ifndef UGO_RX_PLACE_BLOCKS
+#define UGO_RX_PLACE_BLOCKS 3
+#endif
+static uint32_t rx_place_lds() {
+  static const uint32_t cap = [] {
+    if (UGO_RX_PLACE_BLOCKS <= 0) return 0u;
+    int dev = 0, lds = 160 * 1024;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
+        lds <= 4096)
+      lds = 160 * 1024;
+    return static_cast<uint32_t>(lds / UGO_RX_PLACE_BLOCKS - 1024);
+  }();
+  return cap;
+}
+
 hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
   uint32_t blocks = rx_blocks(a);
   if (a.gate && blocks > kRxGatedBlocks) blocks = static_cast<uint32_t>(kRxGatedBlocks);
@@ -676,11 +697,12 @@ hipError_t launch_rx_scatter(const RxArgs& a, hipStream_t s) {
   // (a linear copy of the same bytes: 487 us; tools/rxvariants 15 cold)
   // the header from the payload's first chunk, the realignment's neighbour
   // chunks by ds_bpermute: no header or neighbour loads
+  const uint32_t plds = rx_place_lds();
   switch (passes) {
-    case 1: launch(kKRx, k_rx_place_h<1, 3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 2: launch(kKRx, k_rx_place_h<2, 3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 3: launch(kKRx, k_rx_place_h<3, 3>, dim3(blocks), dim3(256), 0, s, a); break;
-    case 4: launch(kKRx, k_rx_place_h<4, 3>, dim3(blocks), dim3(256), 0, s, a); break;
+    case 1: launch(kKRx, k_rx_place_h<1, 3>, dim3(blocks), dim3(256), plds, s, a); break;
+    case 2: launch(kKRx, k_rx_place_h<2, 3>, dim3(blocks), dim3(256), plds, s, a); break;
+    case 3: launch(kKRx, k_rx_place_h<3, 3>, dim3(blocks), dim3(256), plds, s, a); break;
+    case 4: launch(kKRx, k_rx_place_h<4, 3>, dim3(blocks), dim3(256), plds, s, a); break;
     default: launch(kKRx, k_rx_scatter, dim3(blocks), dim3(256), 0, s, a); break;
   }
   return hipGetLastError();
