@@ -1336,55 +1336,63 @@ def lost_and_recoverable(pm, d, n):
     return ed, have >= d
 
 
-def payload_layout_case(enc, rings, lens, pad, fbats, fpres, flsts, fcnts, flouts, G, n, p, S, FS, ppitch,
-                        kernel_ms, reps, rx_ms):
-    """The RX ring into the payload layout (ugo_fec_rx_assemble: [n][G][ppitch],
-    the payload realigned to column 0) and its list recovery: checked equal to
-    the frame layout's presence masks, lossy list and recovered payload columns
-    (fpres / flsts / fcnts / flouts of the frame run on rings[0]), then its
+RX_LAYOUTS = {  # W = bytes a row carries, off = the payload's column (include/ugo_fec.h)
+    "payload": {"frames": False, "W": 1470, "pitch": 1472, "off": 0,
+                "rows": "[13][G][1472], the payload realigned to column 0 (ugo_fec_rx_assemble)"},
+    "frames": {"frames": True, "W": 1476, "pitch": 1536, "off": 6,
+               "rows": "[13][G][1536], each row the decrypted packet, payload at column 6 (ugo_fec_rx_assemble_frames)"},
+}
+RX_PRIMARY = "payload"  # the library's default (the host RX path's) layout; the other is timed beside it
+
+
+def alt_layout_case(enc, rings, lens, pad, pbats, ppres, plsts, pcnts, plouts, G, n, p, S, L, P, kernel_ms, reps,
+                    rx_ms):
+    """The RX ring into the other layout L (views of the primary batches'
+    storage pbats, overwritten) and its list recovery: checked equal to the
+    primary layout P's presence masks, lossy list and recovered payload columns
+    (ppres / plsts / pcnts / plouts of the primary run on rings[0]), then its
     recovery timed (its placement time, rx_ms, comes from the caller's
-    alternating rounds).
-    Its batches are views of the frame batches' storage (fbats, overwritten):
-    placement time depends on which physical pages back a batch (up to 15 %
-    between allocations of one process, tools/rx_frames_ab.py same), so both
-    layouts are timed on the same pages."""
+    alternating rounds).  Placement time depends on which physical pages back a
+    batch (up to 15 % between allocations of one process, tools/rx_frames_ab.py
+    same), so both layouts are timed on the same pages."""
     import torch
 
     from ugo_amd import fec
 
     dev = rings[0].device
-    bats = [fb.view(-1)[:n * G * ppitch].view(n, G, ppitch) for fb in fbats]
+    bats = [b.view(-1)[:n * G * L["pitch"]].view(n, G, L["pitch"]) for b in pbats]
     pres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
     lsts = [torch.empty(G, dtype=torch.int32, device=dev) for _ in range(2)]
     cnts = [torch.empty(1, dtype=torch.int32, device=dev) for _ in range(2)]
-    outs = [torch.empty((G, p, ppitch), dtype=torch.uint8, device=dev) for _ in range(2)]
+    outs = [torch.empty((G, p, L["pitch"]), dtype=torch.uint8, device=dev) for _ in range(2)]
 
     def rx(r):
         i = r % 2
         pres[i].zero_()
-        enc.rx_assemble(rings[i], lens, bats[i], pres[i], shard_size=S, pad=pad)
+        enc.rx_assemble(rings[i], lens, bats[i], pres[i], shard_size=S, pad=pad, frames=L["frames"])
 
     def rec_list(r):
         i = r % 2
         enc.lossy_groups(pres[i], data_only=True, out=lsts[i], count=cnts[i])
-        enc.reconstruct_list(bats[i], pres[i], lsts[i], cnts[i], outs[i], shard_size=S, data_only=True)
+        enc.reconstruct_list(bats[i], pres[i], lsts[i], cnts[i], outs[i], shard_size=L["W"], data_only=True)
 
     for r in range(4):
         rx(r)
         rec_list(r)
     torch.cuda.synchronize()
     k = int(cnts[0].item())
-    ok = k == int(fcnts[0].item()) and bool(torch.equal(pres[0], fpres[0])) and bool(
-        torch.equal(lsts[0][:k], flsts[0][:k]))
+    ok = k == int(pcnts[0].item()) and bool(torch.equal(pres[0], ppres[0])) and bool(
+        torch.equal(lsts[0][:k], plsts[0][:k]))
     if ok:  # each entry's recovered rows (slots past its erasure count are not written by either)
         ed, okg = lost_and_recoverable(pres[0][lsts[0][:k].long()], n - p, n)
         for i in range(p):
             sel = (ed > i) & okg
-            ok = ok and bool(torch.equal(outs[0][:k][sel, i, :S], flouts[0][:k][sel, i, 6:FS]))
+            ok = ok and bool(torch.equal(outs[0][:k][sel, i, L["off"]:L["off"] + S],
+                                         plouts[0][:k][sel, i, P["off"]:P["off"] + S]))
     rec_k = kernel_ms(rec_list, fec.KERNEL_IDS["reconstruct"], reps)
-    return {"rows": f"[{n}][G][{ppitch}] payload at column 0 (rx_assemble)", "rx_assemble_ms": round(rx_ms, 4),
-            "reconstruct_list_ms": round(rec_k, 4), "verify_eq_frames": ok,
-            "timing": "rx_assemble_ms: the median of 4 rounds alternating with the frame rows' on the same storage"}
+    return {"rows": L["rows"], "rx_assemble_ms": round(rx_ms, 4), "reconstruct_list_ms": round(rec_k, 4),
+            "verify_eq_primary": ok,
+            "timing": "rx_assemble_ms: the median of 4 rounds alternating with the primary layout's on the same storage"}
 
 
 def rx_tx_leg(args, dev_index, reps=12):
@@ -1396,12 +1404,13 @@ def rx_tx_leg(args, dev_index, reps=12):
       * rx_assemble (ugo/conn.go:387-406 decrypt, ugo/fec.go:78-89 decode,
         :107-175 grouping / dedupe / placement): a ring of 65,536 (10+3) groups
         minus 5% uniform loss, 1476-B packets in 1488-B slots, RC4, into a
-        planar batch in the frame layout (ugo_fec_rx_assemble_frames, the one
-        the host RX path uses: [13][G][1536], each row the decrypted packet,
-        payload S = 1470 at column 6; the recovery below runs on the 1476-B frame
-        window), with the payload layout ([13][G][1472], realigned payload at
-        column 0) timed beside it (`payload_layout`); arrival in seqid order
-        (what a UDP flow mostly delivers) and shuffled (worst case);
+        planar batch in the library's default layout (RX_PRIMARY: payload rows
+        [13][G][1472], the payload realigned to column 0, as the host RX path
+        builds them), with the other layout (frame rows [13][G][1536], each row
+        the decrypted packet, payload at column 6, recovered on the 1476-B frame
+        window) timed beside it on the same storage (`alt_layout`); arrival in
+        seqid order (what a UDP flow mostly delivers) and shuffled (worst
+        case);
       * reconstruct_into, data only, of the lossy groups of that batch
         (input's Reconstruct, ugo/fec.go:196-207), over every group, and its
         list form (lossy_groups + reconstruct_list: only the lossy groups,
@@ -1422,7 +1431,11 @@ def rx_tx_leg(args, dev_index, reps=12):
     from ugo_amd import fec
 
     d, p, n, S, slot = 10, 3, 13, 1470, 1488
-    FS, pitch, ppitch = S + 6, 1536, 1472  # frame rows (64-B pitch) / the payload layout's rows
+    PL = RX_LAYOUTS[RX_PRIMARY]
+    alt = [k for k in RX_LAYOUTS if k != RX_PRIMARY][0]
+    AL = RX_LAYOUTS[alt]
+    W, pitch, off = PL["W"], PL["pitch"], PL["off"]
+    span = max(L["pitch"] for L in RX_LAYOUTS.values())  # storage per row for either layout's view
     G = 65536
     dev = torch.device("cuda", dev_index)
     stream = torch.cuda.current_stream(dev)
@@ -1470,7 +1483,8 @@ def rx_tx_leg(args, dev_index, reps=12):
             w[:, :6] = hdr ^ pad[:6]
             rings.append(w)
         lens = torch.full((npk,), 1476, dtype=torch.int16, device=dev)
-        bats = [torch.empty((n, G, pitch), dtype=torch.uint8, device=dev) for _ in range(2)]
+        bats = [torch.empty(n * G * span, dtype=torch.uint8, device=dev)[:n * G * pitch].view(n, G, pitch)
+                for _ in range(2)]
         pres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
         outs = [torch.empty((p, G, pitch), dtype=torch.uint8, device=dev) for _ in range(2)]
         st = torch.zeros(5, dtype=torch.int32, device=dev)
@@ -1478,11 +1492,11 @@ def rx_tx_leg(args, dev_index, reps=12):
         def rx(r):
             i = r % 2
             pres[i].zero_()
-            enc.rx_assemble(rings[i], lens, bats[i], pres[i], shard_size=S, pad=pad, stats=st, frames=True)
+            enc.rx_assemble(rings[i], lens, bats[i], pres[i], shard_size=S, pad=pad, stats=st, frames=PL["frames"])
 
         def rec(r):
             i = r % 2
-            enc.reconstruct_into(bats[i], pres[i], outs[i], shard_size=FS, data_only=True, shard_major=True)
+            enc.reconstruct_into(bats[i], pres[i], outs[i], shard_size=W, data_only=True, shard_major=True)
 
         for r in range(4):
             rx(r)
@@ -1494,28 +1508,28 @@ def rx_tx_leg(args, dev_index, reps=12):
         # spot check of the placement: 4,096 packets' payloads, decrypted, in their rows
         pick = torch.randint(0, npk, (4096,), device=dev, generator=gen)
         sq = seq[pick]
-        want = rings[0][pick, :FS] ^ pad[:FS]
-        got = bats[0][sq % n, sq // n, :FS]
+        want = rings[0][pick, 6 - off:6 - off + W] ^ pad[6 - off:6 - off + W]
+        got = bats[0][sq % n, sq // n, :W]
         ok = stats == [npk, 0, 0, 0, 0] and bool(torch.equal(got, want))
-        # frame rows and payload rows timed alternately, on the same storage (placement time moves with
-        # the physical pages a batch gets): the median of 4 rounds each
-        pbats = [b.view(-1)[:n * G * ppitch].view(n, G, ppitch) for b in bats]
-        ppres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
+        # both layouts timed alternately, on the same storage (placement time moves with the physical pages
+        # a batch gets): the median of 4 rounds each
+        abats = [b.view(-1)[:n * G * AL["pitch"]].view(n, G, AL["pitch"]) for b in bats]
+        apres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
 
-        def prx(r):
+        def arx(r):
             i = r % 2
-            ppres[i].zero_()
-            enc.rx_assemble(rings[i], lens, pbats[i], ppres[i], shard_size=S, pad=pad)
+            apres[i].zero_()
+            enc.rx_assemble(rings[i], lens, abats[i], apres[i], shard_size=S, pad=pad, frames=AL["frames"])
 
-        tf, tp = [], []
+        tp, ta = [], []
         for rnd in range(4):
-            for fn, acc in (((rx, tf), (prx, tp)) if rnd % 2 == 0 else ((prx, tp), (rx, tf))):
+            for fn, acc in (((rx, tp), (arx, ta)) if rnd % 2 == 0 else ((arx, ta), (rx, tp))):
                 fn(0)
                 fn(1)
                 acc.append(kernel_ms(fn, fec.KERNEL_IDS["rx_assemble"], reps))
-        rx_k, prx_k = float(np.median(tf)), float(np.median(tp))
-        del pbats, ppres
-        for r in range(2):  # the frame rows back for the recovery below
+        rx_k, arx_k = float(np.median(tp)), float(np.median(ta))
+        del abats, apres
+        for r in range(2):  # the primary rows back for the recovery below
             rx(r)
         rx_w = wall_ms(rx, reps)
         rec_k = kernel_ms(rec, (fec.KERNEL_IDS["reconstruct"], fec.KERNEL_IDS["prepare"]), reps)
@@ -1537,7 +1551,7 @@ def rx_tx_leg(args, dev_index, reps=12):
         def rec_list(r):
             i = r % 2
             enc.lossy_groups(pres[i], data_only=True, out=lsts[i], count=cnts[i])
-            enc.reconstruct_list(bats[i], pres[i], lsts[i], cnts[i], louts[i], shard_size=FS, data_only=True)
+            enc.reconstruct_list(bats[i], pres[i], lsts[i], cnts[i], louts[i], shard_size=W, data_only=True)
 
         for r in range(4):
             rx(r)
@@ -1551,7 +1565,8 @@ def rx_tx_leg(args, dev_index, reps=12):
         ok_list = k == int((lost_data > 0).sum())
         for i in range(p):
             sel = (ed > i) & okg  # groups below d shards: no output in either form
-            ok_list = ok_list and bool(torch.equal(louts[0][:k][sel, i, 6:FS], outs[0][i, lg[sel], 6:FS]))
+            ok_list = ok_list and bool(torch.equal(louts[0][:k][sel, i, off:off + S],
+                                                   outs[0][i, lg[sel], off:off + S]))
         rec_list_k = kernel_ms(rec_list, fec.KERNEL_IDS["reconstruct"], reps)
         # the same recovery as `input` returns it (ugo_fec_recover_data): the lost data shards
         # row-compact in `recovered` order with their places, the count on the device
@@ -1561,7 +1576,7 @@ def rx_tx_leg(args, dev_index, reps=12):
 
         def rec_data(r):
             i = r % 2
-            enc.recover_data(bats[i], pres[i], rdo[i], rdi[i], count=rdc[i], shard_size=FS)
+            enc.recover_data(bats[i], pres[i], rdo[i], rdi[i], count=rdc[i], shard_size=W)
 
         for r in range(2):
             rx(r)
@@ -1573,17 +1588,16 @@ def rx_tx_leg(args, dev_index, reps=12):
         jj, rr = torch.nonzero(lost, as_tuple=True)
         want_rows = louts[0][:k][torch.arange(p, device=dev)[None, :] < lost.sum(1)[:, None]]
         ok_rd = nr == int(jj.numel()) and bool(torch.equal(rdi[0][:nr].long(), lg[jj] * n + rr)) and bool(
-            torch.equal(rdo[0][:nr, 6:FS], want_rows[:, 6:FS]))
+            torch.equal(rdo[0][:nr, off:off + S], want_rows[:, off:off + S]))
         rec_data_k = kernel_ms(rec_data, fec.KERNEL_IDS["reconstruct"], reps)
         del rdo, rdi, rdc
-        # the payload layout (ugo_fec_rx_assemble: realigned payload rows at column 0) on the same rings,
-        # checked against the frame rows, then timed with its list recovery
-        pl = payload_layout_case(enc, rings, lens, pad, bats, pres, lsts, cnts, louts, G, n, p, S, FS, ppitch,
-                                 kernel_ms, reps, prx_k)
+        # the other layout on the same rings and storage, checked against the primary one, with its recovery
+        al = alt_layout_case(enc, rings, lens, pad, bats, pres, lsts, cnts, louts, G, n, p, S, AL, PL, kernel_ms,
+                             reps, arx_k)
         # ceilings: the compute-free twins of both forms on the same buffers (after the checks: wrong bytes)
-        twin_ms = probe_recover_twin_ms(bats, outs, pres, None, None, G, FS, pitch, bats[0].stride(0),
+        twin_ms = probe_recover_twin_ms(bats, outs, pres, None, None, G, W, pitch, bats[0].stride(0),
                                         outs[0].stride(0), outs[0].stride(1), reps, stream.cuda_stream)
-        ltwin_ms = probe_recover_twin_ms(bats, louts, pres, lsts, cnts, G, FS, pitch, bats[0].stride(0),
+        ltwin_ms = probe_recover_twin_ms(bats, louts, pres, lsts, cnts, G, W, pitch, bats[0].stride(0),
                                          louts[0].stride(1), louts[0].stride(0), reps, stream.cuda_stream)
         cb = min(rx_bytes // 2, rings[0].numel(), bats[0].numel())  # each copy stays inside both buffers
         copy_ms = probe_nt_copy_ms([rings[i].data_ptr() for i in range(2)], [bats[(i + 1) % 2].data_ptr()
@@ -1606,11 +1620,11 @@ def rx_tx_leg(args, dev_index, reps=12):
             "recover_data_ms": round(rec_data_k, 4), "recover_data_frac": frac(rec_bytes, rec_data_k),
             "verify_recover_data": ok_rd,
             "stats": stats, "verify_spot_4096": ok,
-            "layout": "frames: [13][G][1536] rows = decrypted packets, payload at column 6 (rx_assemble_frames)",
-            "rx_rounds_ms": {"frames": [round(x, 4) for x in tf], "payload": [round(x, 4) for x in tp],
-                             "note": "alternating rounds on the same storage; rx_assemble_ms = median of frames"},
-            "payload_layout": {**pl, "rx_frac": frac(rx_bytes, pl["rx_assemble_ms"]),
-                               "reconstruct_list_frac": frac(rec_bytes, pl["reconstruct_list_ms"])}}
+            "layout": f"{RX_PRIMARY}: {PL['rows']}",
+            "rx_rounds_ms": {RX_PRIMARY: [round(x, 4) for x in tp], alt: [round(x, 4) for x in ta],
+                             "note": f"alternating rounds on the same storage; rx_assemble_ms = median of {RX_PRIMARY}"},
+            "alt_layout": {"name": alt, **al, "rx_frac": frac(rx_bytes, al["rx_assemble_ms"]),
+                           "reconstruct_list_frac": frac(rec_bytes, al["reconstruct_list_ms"])}}
         del rings, bats, pres, outs, lsts, cnts, louts
         torch.cuda.empty_cache()
 

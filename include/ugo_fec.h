@@ -58,8 +58,7 @@ extern "C" {
  *    ugo_fec_reconstruct_list, ugo_fec_recover_data, ugo_fec_rx_recover_host,
  *    ugo_fec_tx_assemble_host. */
 /* 9: ugo_fec_rx_assemble_frames (frame rows: each placed row holds its
- *    decrypted packet, payload at column 6); ugo_fec_rx_recover_host runs on
- *    frame rows internally (same results); the low-priority host copy queue is
+ *    decrypted packet, payload at column 6); the low-priority host copy queue is
  *    on by default, and the service pool holds at most 3 queues (8 hardware
  *    queues per process, see ugo_fec_set_host_copy_queue). */
 #define UGO_FEC_ABI_VERSION 9

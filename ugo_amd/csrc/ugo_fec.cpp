@@ -1797,8 +1797,14 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
 // copy lands, so copies and kernels overlap; then the lossy-group list, the
 // data-only Reconstruct of those groups into a row-compact output (the
 // `recovered` list of ugo/fec.go:203-207), and the D2H of those rows only.
+// The host RX path's batch layout: payload rows (0, the default) or frame rows
+// (1, ugo_fec_rx_assemble_frames).  Measured the same end to end (22.7 ms for
+// the bench's ring either way, the call being PCIe-bound:
+// profiles/r6/host_rx/frames_vs_payload.jsonl); with both place kernels at 3
+// blocks per CU the payload rows' placement ties or wins on the device
+// (DESIGN.md §3.4), and it needs no row shift before the D2H.
 #ifndef UGO_RX_FRAMES
-#define UGO_RX_FRAMES 1
+#define UGO_RX_FRAMES 0
 #endif
 constexpr bool kRxFrames = UGO_RX_FRAMES != 0;
 #ifndef UGO_RX_STAGE_MIB
@@ -1825,9 +1831,9 @@ int ugo_fec_rx_recover_host(ugo_fec* c, const uint8_t* wire, size_t slot_stride,
   int st = ensure_streams(c);
   if (st) return st;
   const hipStream_t s0 = c->streams[0];  // assembly and recovery; copies on streams[1]
-  // frame rows (ugo_fec_rx_assemble_frames): each row holds its decrypted packet, the payload at
-  // column 6, so placement needs no realignment; the recovery runs over the frame window
-  // (GF columns are independent) and only the payload columns of a recovered row come back
+  // with frame rows (kRxFrames, ugo_fec_rx_assemble_frames) each row holds its decrypted packet, the
+  // payload at column 6; the recovery then runs over the frame window (GF columns are independent) and
+  // only the payload columns of a recovered row come back
   const size_t fo = kRxFrames ? 6 : 0, FS = S + fo;
   // (frame rows at a 64-B pitch: whole 64-B lines per row, rx_frame_fill)
   const size_t n = size_t(c->n), pitch = round_up(FS, kRxFrames ? 64 : 16), slots = size_t(std::min(c->d, c->p));
