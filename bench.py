@@ -1345,10 +1345,10 @@ RX_LAYOUTS = {  # W = bytes a row carries, off = the payload's column (include/u
 RX_PRIMARY = "payload"  # the library's default (the host RX path's) layout; the other is timed beside it
 
 
-def alt_layout_case(enc, rings, lens, pad, pbats, ppres, plsts, pcnts, plouts, G, n, p, S, L, P, kernel_ms, reps,
+def alt_layout_case(enc, rings, lens, pad, flats, ppres, plsts, pcnts, plouts, G, n, p, S, L, P, kernel_ms, reps,
                     rx_ms):
     """The RX ring into the other layout L (views of the primary batches'
-    storage pbats, overwritten) and its list recovery: checked equal to the
+    flat storage, overwritten) and its list recovery: checked equal to the
     primary layout P's presence masks, lossy list and recovered payload columns
     (ppres / plsts / pcnts / plouts of the primary run on rings[0]), then its
     recovery timed (its placement time, rx_ms, comes from the caller's
@@ -1360,7 +1360,7 @@ def alt_layout_case(enc, rings, lens, pad, pbats, ppres, plsts, pcnts, plouts, G
     from ugo_amd import fec
 
     dev = rings[0].device
-    bats = [b.view(-1)[:n * G * L["pitch"]].view(n, G, L["pitch"]) for b in pbats]
+    bats = [f[:n * G * L["pitch"]].view(n, G, L["pitch"]) for f in flats]
     pres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
     lsts = [torch.empty(G, dtype=torch.int32, device=dev) for _ in range(2)]
     cnts = [torch.empty(1, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -1483,8 +1483,8 @@ def rx_tx_leg(args, dev_index, reps=12):
             w[:, :6] = hdr ^ pad[:6]
             rings.append(w)
         lens = torch.full((npk,), 1476, dtype=torch.int16, device=dev)
-        bats = [torch.empty(n * G * span, dtype=torch.uint8, device=dev)[:n * G * pitch].view(n, G, pitch)
-                for _ in range(2)]
+        flats = [torch.empty(n * G * span, dtype=torch.uint8, device=dev) for _ in range(2)]  # either layout's view
+        bats = [f[:n * G * pitch].view(n, G, pitch) for f in flats]
         pres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
         outs = [torch.empty((p, G, pitch), dtype=torch.uint8, device=dev) for _ in range(2)]
         st = torch.zeros(5, dtype=torch.int32, device=dev)
@@ -1513,7 +1513,7 @@ def rx_tx_leg(args, dev_index, reps=12):
         ok = stats == [npk, 0, 0, 0, 0] and bool(torch.equal(got, want))
         # both layouts timed alternately, on the same storage (placement time moves with the physical pages
         # a batch gets): the median of 4 rounds each
-        abats = [b.view(-1)[:n * G * AL["pitch"]].view(n, G, AL["pitch"]) for b in bats]
+        abats = [f[:n * G * AL["pitch"]].view(n, G, AL["pitch"]) for f in flats]
         apres = [torch.zeros(G, dtype=torch.int64, device=dev) for _ in range(2)]
 
         def arx(r):
@@ -1592,7 +1592,7 @@ def rx_tx_leg(args, dev_index, reps=12):
         rec_data_k = kernel_ms(rec_data, fec.KERNEL_IDS["reconstruct"], reps)
         del rdo, rdi, rdc
         # the other layout on the same rings and storage, checked against the primary one, with its recovery
-        al = alt_layout_case(enc, rings, lens, pad, bats, pres, lsts, cnts, louts, G, n, p, S, AL, PL, kernel_ms,
+        al = alt_layout_case(enc, rings, lens, pad, flats, pres, lsts, cnts, louts, G, n, p, S, AL, PL, kernel_ms,
                              reps, arx_k)
         # ceilings: the compute-free twins of both forms on the same buffers (after the checks: wrong bytes)
         twin_ms = probe_recover_twin_ms(bats, outs, pres, None, None, G, W, pitch, bats[0].stride(0),
@@ -1625,7 +1625,7 @@ def rx_tx_leg(args, dev_index, reps=12):
                              "note": f"alternating rounds on the same storage; rx_assemble_ms = median of {RX_PRIMARY}"},
             "alt_layout": {"name": alt, **al, "rx_frac": frac(rx_bytes, al["rx_assemble_ms"]),
                            "reconstruct_list_frac": frac(rec_bytes, al["reconstruct_list_ms"])}}
-        del rings, bats, pres, outs, lsts, cnts, louts
+        del rings, bats, flats, pres, outs, lsts, cnts, louts
         torch.cuda.empty_cache()
 
     # ---- TX
