@@ -1342,7 +1342,7 @@ RX_LAYOUTS = {  # W = bytes a row carries, off = the payload's column (include/u
     "frames": {"frames": True, "W": 1476, "pitch": 1536, "off": 6,
                "rows": "[13][G][1536], each row the decrypted packet, payload at column 6 (ugo_fec_rx_assemble_frames)"},
 }
-RX_PRIMARY = "payload"  # the library's default (the host RX path's) layout; the other is timed beside it
+RX_PRIMARY = "frames"  # ahead in 2 of 3 final-tree runs; the other layout is timed beside it
 
 
 def alt_layout_case(enc, rings, lens, pad, flats, ppres, plsts, pcnts, plouts, G, n, p, S, L, P, kernel_ms, reps,
@@ -1404,11 +1404,11 @@ def rx_tx_leg(args, dev_index, reps=12):
       * rx_assemble (ugo/conn.go:387-406 decrypt, ugo/fec.go:78-89 decode,
         :107-175 grouping / dedupe / placement): a ring of 65,536 (10+3) groups
         minus 5% uniform loss, 1476-B packets in 1488-B slots, RC4, into a
-        planar batch in the library's default layout (RX_PRIMARY: payload rows
-        [13][G][1472], the payload realigned to column 0, as the host RX path
-        builds them), with the other layout (frame rows [13][G][1536], each row
-        the decrypted packet, payload at column 6, recovered on the 1476-B frame
-        window) timed beside it on the same storage (`alt_layout`); arrival in
+        planar batch in the RX_PRIMARY layout (frame rows [13][G][1536], each
+        row the decrypted packet, payload at column 6, recovered on the 1476-B
+        frame window), with the other layout (payload rows [13][G][1472], the
+        payload realigned to column 0, as the host RX path builds them) timed
+        beside it on the same storage (`alt_layout`); arrival in
         seqid order (what a UDP flow mostly delivers) and shuffled (worst
         case);
       * reconstruct_into, data only, of the lossy groups of that batch
