@@ -338,7 +338,9 @@ __global__ __launch_bounds__(256) void k_rx_place_h(RxArgs a) {
 // TX already keeps (k_tx_c: a lane holds packet bytes [16m, 16m + 16)).
 // Presence, first-copy rule, stats and gated passes as k_rx_place_h.
 // Measured (round 6, tools/rx_frames_ab.py, one box, same storage): 2.4-4 %
-// under the payload kernel; residency 3 blocks/CU (0.512 vs 0.539-0.553 ms at
+// under the uncapped payload kernel; against the payload kernel capped as this
+// one, a tie (4 bench runs: -4.0 / -4.0 / +1.3 / +2.8 % in order, within 0.6 %
+// shuffled; profiles/r6/rx_frames/final_tree_runs.json); residency 3 blocks/CU (0.512 vs 0.539-0.553 ms at
 // 5 or uncapped, pitch 1488); rows at a 64-B pitch written to whole lines
 // (1536 for S = 1470: 0.40-0.46 vs 0.51-0.55 ms at the 1488 pitch); the same
 // frames one chunk per thread over the whole ring (the P2 shape, every lane

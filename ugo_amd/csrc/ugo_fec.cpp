@@ -1801,8 +1801,9 @@ int ugo_fec_tx_assemble(ugo_fec* c, const uint8_t* pkts, size_t slot_in, const u
 // (1, ugo_fec_rx_assemble_frames).  Measured the same end to end (22.7 ms for
 // the bench's ring either way, the call being PCIe-bound:
 // profiles/r6/host_rx/frames_vs_payload.jsonl); with both place kernels at 3
-// blocks per CU the payload rows' placement ties or wins on the device
-// (DESIGN.md §3.4), and it needs no row shift before the D2H.
+// blocks per CU the two placements tie on the device (frames 1 % ahead in order
+// on the mean of four runs, 4 % either way box to box), and
+// payload rows need no row shift before the D2H.
 #ifndef UGO_RX_FRAMES
 #define UGO_RX_FRAMES 0
 #endif
